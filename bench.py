@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Benchmark: Msplats/s of the full frame (preprocess -> scan -> duplicate ->
+radix sort -> tile ranges -> composite [-> exchange -> gather]) on
+BASELINE.json's headline workload: 6M-splat scene @ 1920x1080, SH degree 3
+(configs[2]; a seeded synthetic scene with 3DGS statistics — no garden .ply
+exists offline).  Inputs are resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Multi-GPU is weak scaling: every rank holds its own 6M-splat shard of a
+(6M x N)-splat scene and owns 1/N of the tile rows; value = all splats / frame
+time (max over ranks).  Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 78.6     # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s (fp32 non-FMA)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--splats", type=int, default=6_000_000, help="splats per GPU")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--sh", type=int, default=3)
+    ap.add_argument("--mode", default="tile")
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="splats in the CPU baseline sample")
+    ap.add_argument("--no-stage-timing", action="store_true")
+    return ap.parse_args()
+
+
+def stage_summary(stats_list):
+    keys = ["preprocess", "scan", "duplicate", "sort", "ranges", "composite"]
+    out = {}
+    for k in keys:
+        ms = float(np.mean([s[f"ms_{k}"] for s in stats_list]))
+        by = float(np.mean([s[f"bytes_{k}"] for s in stats_list]))
+        out[k] = {"ms": ms, "bytes": by, "gbs": by / (ms * 1e6) if ms > 0 else 0.0}
+    return out
+
+
+def cpu_baseline(scene, view, proj, w, h, sh, sample):
+    from oracle import oracle_py as O
+
+    n = min(sample, scene.n)
+    sub = scene.subset(slice(0, n))
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    O.render(sub.subset(slice(0, min(n, 20000))), view, proj, w, h, sh_degree=sh, nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    O.render(sub, view, proj, w, h, sh_degree=sh, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt / 1e6, "unit": "Msplats/s", "cores": threads, "kind": "port",
+            "sample": f"one {w}x{h} SH{sh} frame of the first {n} splats of the same scene "
+                      f"(oracle/gs_oracle.c, OpenMP), {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from gaussian_splat_amd import scene as S
+    from gaussian_splat_amd.api import InstancedSplatRenderer, Options, default_camera
+
+    W, H = args.width, args.height
+    # each rank generates its own shard (distinct seeds): weak scaling
+    scene = S.synthetic_scene(args.splats, seed=args.seed + 1000 * rank, sh_degree=args.sh, aspect=W / H)
+    cam = default_camera(W, H)
+    view, proj = cam.getViewMatrix(), cam.getProjectionMatrix()
+    opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=not args.no_stage_timing)
+
+    if world == 1:
+        r = InstancedSplatRenderer(scene, opts)
+        r.initialize(local)
+        out = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        step = lambda: r.render(view, proj, W, H, out=out)
+        stats_of = r.last_stats
+    else:
+        from gaussian_splat_amd.distributed import HipShardBackend, ShardedRenderer
+
+        be = HipShardBackend(scene, rank, world, rank * args.splats, opts, local)
+        sr = ShardedRenderer(be, rank, world)
+        step = lambda: sr.render(view, proj, W, H, gather=True)
+        stats_of = be.r.last_stats
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stats = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stats.append(stats_of())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt * 1e3 / args.steps
+    total_splats = args.splats * world
+    value = total_splats / (ms * 1e-3) / 1e6
+
+    line = None
+    if rank == 0:
+        st = stage_summary(stats) if not args.no_stage_timing else {}
+        s0 = stats[-1]
+        rl = None
+        if st:
+            dom = max(st, key=lambda k: st[k]["ms"])
+            d = st[dom]
+            rl = {"bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(d["gbs"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                  "kernel_ms": round(d["ms"], 4)}
+        line = {
+            "metric": "Msplats/sec (6M-splat scene @1080p, SH3, full frame)",
+            "value": round(value, 2), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded 3DGS-statistics scene; no garden .ply offline)",
+            "config": {"workload": f"{args.splats} splats/GPU @ {W}x{H}, SH{args.sh}, {args.mode} contract",
+                       "global_splats": total_splats, "width": W, "height": H, "sh_degree": args.sh,
+                       "parallelism": f"splat-shard x{world}, tile-row ownership" if world > 1 else "single GPU",
+                       "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
+            "roofline": rl,
+            "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
+        }
+        if world == 1 and args.cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(scene, view, proj, W, H, args.sh, args.cpu_sample)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

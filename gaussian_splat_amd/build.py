@@ -1,0 +1,99 @@
+"""Build libgsplat.so in-tree (hipcc, gfx950) and the oracle (gcc).
+
+The product library is compiled ahead of time for gfx950 only; the .so lives
+next to this file so it travels with the repo snapshot to the GPU box.
+Every translation unit is built with -ffp-contract=off: the pipeline's
+floating-point contract spells out every fused op explicitly.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build" / "gsplat"
+LIB = PKG / "libgsplat.so"
+ARCH = os.environ.get("GSPLAT_ARCH", "gfx950")
+
+HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "host" / "renderer.cpp"]
+CXX_SOURCES = [CSRC / "host" / "ply_loader.cpp", CSRC / "host" / "camera.cpp",
+               CSRC / "host" / "instanced_splat_renderer.cpp", CSRC / "host" / "renderable.cpp"]
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+          f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def _stale(out: Path, deps: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _headers() -> list[Path]:
+    return (list((ROOT / "include").rglob("*.h")) + list(CSRC.rglob("*.h")))
+
+
+def build_lib(verbose: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    hdrs = _headers()
+    jobs = []
+    objs = []
+    for src in HIP_SOURCES:
+        obj = BUILD / (src.name + ".o")
+        objs.append(obj)
+        if _stale(obj, [src, *hdrs]):
+            jobs.append([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, "-c", str(src), "-o", str(obj)])
+    for src in CXX_SOURCES:
+        if not src.exists():
+            continue
+        obj = BUILD / (src.name + ".o")
+        objs.append(obj)
+        if _stale(obj, [src, *hdrs]):
+            jobs.append(["g++", *COMMON, "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-c", str(src),
+                         "-o", str(obj)])
+    workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")) or 1) if jobs else 1
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        for cmd in jobs:
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+        list(ex.map(_run, jobs))
+    if jobs or _stale(LIB, objs):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+              "-lpthread"])
+    return LIB
+
+
+def build_oracle() -> None:
+    """Test infrastructure: the C oracle and, when /root/reference exists, oracle/_ref."""
+    _run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"])
+
+
+def build_all(verbose: bool = False) -> Path:
+    lib = build_lib(verbose)
+    build_oracle()
+    return lib
+
+
+if __name__ == "__main__":
+    print(build_all(verbose="-v" in sys.argv))

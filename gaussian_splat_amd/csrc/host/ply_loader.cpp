@@ -1,0 +1,182 @@
+// ply_loader.cpp — PLYLoader drop-in.
+//
+// Reproduces the reference's observable results (src/ply_loader.cpp:22-205):
+// property mapping by name, sigmoid(opacity), exp(scale), DC->RGB with clamp
+// and the all-zero skip, 4 bytes per property regardless of declared type,
+// and (compat) the ASCII resize()+push_back() doubling.  Different mechanics:
+// the binary payload is read in one bulk read and converted on all host
+// cores (the reference converts one vertex at a time on one thread).
+#include "gsplat/ply_loader.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <thread>
+
+namespace {
+
+constexpr float kShC0 = 0.28209479177387814f;  // ply_loader.cpp:9
+
+enum Slot {
+    S_X, S_Y, S_Z, S_NX, S_NY, S_NZ, S_R, S_G, S_B, S_OP, S_SX, S_SY, S_SZ, S_R0, S_R1, S_R2, S_R3, S_REST
+};
+
+int slot_of(const std::string& n) {
+    static const char* names[] = {"x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2",
+                                  "opacity", "scale_0", "scale_1", "scale_2", "rot_0", "rot_1",
+                                  "rot_2", "rot_3"};
+    for (int i = 0; i < 17; ++i)
+        if (n == names[i]) return i;
+    if (n.compare(0, 7, "f_rest_") == 0) {
+        const char* s = n.c_str() + 7;
+        char* end = nullptr;
+        long v = std::strtol(s, &end, 10);
+        if (end != s && v >= 0 && v < 45) return S_REST + (int)v;
+    }
+    return -1;
+}
+
+inline void store(PointData& p, int slot, float v) {
+    float* f = &p.x;
+    if (slot < 0) return;
+    if (slot == S_OP) f[S_OP] = 1.0f / (1.0f + std::exp(-v));
+    else if (slot >= S_SX && slot <= S_SZ) f[slot] = std::exp(v);
+    else f[slot] = v;
+}
+
+inline void dc_to_rgb(PointData& p) {
+    if (p.r != 0 || p.g != 0 || p.b != 0) {
+        float* c = &p.r;
+        for (int k = 0; k < 3; ++k) {
+            float v = 0.5f + kShC0 * c[k];
+            c[k] = std::max(0.0f, std::min(1.0f, v));
+        }
+    }
+}
+
+}  // namespace
+
+bool PLYLoader::parseHeader(std::istream& file, int& vertexCount, std::vector<PropertyInfo>& properties,
+                            bool& isBinary) {
+    std::string line;
+    if (!std::getline(file, line) || line != "ply") return false;
+    properties.clear();
+    while (std::getline(file, line)) {
+        std::istringstream ls(line);
+        std::string tok;
+        ls >> tok;
+        if (tok == "format") {
+            std::string f;
+            ls >> f;
+            isBinary = f == "binary_little_endian" || f == "binary_big_endian";
+        } else if (tok == "element") {
+            std::string kind;
+            ls >> kind;
+            if (kind == "vertex") ls >> vertexCount;
+        } else if (tok == "property") {
+            PropertyInfo pi;
+            ls >> pi.type >> pi.name;
+            properties.push_back(pi);
+        } else if (tok == "end_header") {
+            break;
+        }
+    }
+    return vertexCount > 0 && !properties.empty();
+}
+
+bool PLYLoader::load(const std::string& filepath, std::vector<PointData>& points) {
+    return load(filepath, points, nullptr, true);
+}
+
+bool PLYLoader::load(const std::string& filepath, std::vector<PointData>& points, std::vector<float>* raw_dc,
+                     bool compat) {
+    std::ifstream file(filepath, std::ios::binary);
+    if (!file.is_open()) return false;
+    int vcount = 0;
+    bool binary = false;
+    std::vector<PropertyInfo> props;
+    if (!parseHeader(file, vcount, props, binary)) return false;
+
+    const size_t np = props.size();
+    std::vector<int> slot(np);
+    for (size_t j = 0; j < np; ++j) slot[j] = slot_of(props[j].name);
+    int dc_col[3] = {-1, -1, -1};
+    for (size_t j = 0; j < np; ++j)
+        if (slot[j] >= S_R && slot[j] <= S_B) dc_col[slot[j] - S_R] = (int)j;
+
+    points.clear();
+    points.resize(vcount);
+    if (raw_dc) raw_dc->assign((size_t)vcount * 3, 0.0f);
+
+    if (binary) {
+        const size_t stride = np * 4;
+        const size_t want = (size_t)vcount * stride;
+        std::vector<float> data((want + 3) / 4);
+        file.read(reinterpret_cast<char*>(data.data()), (std::streamsize)want);
+        size_t got = (size_t)file.gcount();
+        if (got < want) {
+            // Truncated file: replay the reference's reuse of one 10000-vertex
+            // chunk buffer (ply_loader.cpp:89-95) so stale bytes match.
+            const size_t chunk_bytes = (size_t)10000 * stride;
+            std::vector<char> buf(chunk_bytes, 0);
+            const char* src = reinterpret_cast<const char*>(data.data());
+            char* dst = reinterpret_cast<char*>(data.data());
+            std::vector<char> out(want);
+            size_t pos = 0;
+            for (size_t c0 = 0; c0 < (size_t)vcount; c0 += 10000) {
+                size_t cn = std::min<size_t>(10000, (size_t)vcount - c0);
+                size_t bytes = cn * stride;
+                size_t avail = pos < got ? std::min(bytes, got - pos) : 0;
+                std::memcpy(buf.data(), src + pos, avail);
+                pos += avail;
+                if (avail < bytes) pos = got;  // stream failed: later reads get nothing
+                std::memcpy(out.data() + c0 * stride, buf.data(), bytes);
+            }
+            std::memcpy(dst, out.data(), want);
+        }
+        const float* vals = data.data();
+        auto work = [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) {
+                PointData& p = points[i];
+                const float* v = vals + i * np;
+                for (size_t j = 0; j < np; ++j) store(p, slot[j], v[j]);
+                if (raw_dc)
+                    for (int c = 0; c < 3; ++c) (*raw_dc)[i * 3 + c] = dc_col[c] >= 0 ? v[dc_col[c]] : 0.0f;
+                dc_to_rgb(p);
+            }
+        };
+        size_t nthreads = std::max(1u, std::thread::hardware_concurrency());
+        nthreads = std::min<size_t>(nthreads, 64);
+        if ((size_t)vcount < 65536) nthreads = 1;
+        std::vector<std::thread> pool;
+        size_t per = ((size_t)vcount + nthreads - 1) / nthreads;
+        for (size_t t = 0; t < nthreads; ++t) {
+            size_t b = t * per, e = std::min((size_t)vcount, b + per);
+            if (b < e) pool.emplace_back(work, b, e);
+        }
+        for (auto& th : pool) th.join();
+    } else {
+        // ASCII (ply_loader.cpp:150-200).  compat: resize() + push_back() -> 2N.
+        if (!compat) points.clear();
+        std::string line;
+        for (int i = 0; i < vcount; ++i) {
+            if (!std::getline(file, line)) break;
+            std::istringstream iss(line);
+            PointData p;
+            float dc[3] = {0, 0, 0};
+            for (size_t j = 0; j < np; ++j) {
+                float value = 0.0f;
+                iss >> value;
+                store(p, slot[j], value);
+                if (slot[j] >= S_R && slot[j] <= S_B) dc[slot[j] - S_R] = value;
+            }
+            dc_to_rgb(p);
+            points.push_back(p);
+            if (raw_dc) raw_dc->insert(raw_dc->end(), dc, dc + 3);
+        }
+        if (raw_dc && !compat) raw_dc->erase(raw_dc->begin(), raw_dc->begin() + (size_t)vcount * 3);
+    }
+    return !points.empty();
+}

@@ -1,0 +1,655 @@
+// renderer.cpp — libgsplat C-ABI: scene ownership, HBM layout, frame pipeline.
+//
+// Replaces InstancedSplatRenderer's host side (src/instanced_splat_renderer.mm):
+//   ctor (:339-393)        -> gs_create*: PLY load, crop, host SoA
+//   initialize (:399-422)  -> gs_initialize: HBM SoA upload (no shader compile,
+//                             no hot-reload watcher: kernels are AOT for gfx950)
+//   render (:424-578)      -> gs_render: preprocess -> scan -> duplicate ->
+//                             radix sort -> tile ranges -> composite, all on
+//                             the caller's stream, into a caller-owned fp32
+//                             RGBA framebuffer (no 504 B/pixel list buffer,
+//                             no per-frame ~1 GB clear).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../kernels/gs_kernels.h"
+#include "gsplat.h"
+#include "gsplat/ply_loader.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+gs_status fail(gs_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define GS_HIP(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(e_ == hipErrorOutOfMemory ? GS_ERR_OOM : GS_ERR_DEVICE,                    \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                        \
+    } while (0)
+
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    // Grows monotonically (never shrinks; reused across frames).
+    hipError_t reserve(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        release();
+        size_t b = std::max<size_t>(want + want / 8, 256);
+        b = (b + 255) & ~size_t(255);
+        hipError_t e = hipMalloc(&ptr, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(ptr); }
+};
+
+int sh_coeffs(int deg) { return deg <= 0 ? 0 : (deg == 1 ? 3 : (deg == 2 ? 8 : 15)); }
+
+}  // namespace
+
+struct gs_handle {
+    gs_options opt{};
+    // host SoA (post-crop)
+    int64_t n = 0;
+    std::vector<float> pos, rot, scale, opacity, color, sh_rest;
+    bool has_sh = false;
+    // device
+    int device = -1;
+    bool initialized = false;
+    DevBuf p0, p1, p2, p3, sh4, sh1;
+    // per-frame scratch
+    DevBuf rec, dkey, ntiles, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb;
+    DevBuf xmask, xcounts, xtotal, rdkey, rntiles, roffsets, rpartials;  // multi-GPU exchange
+    uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
+    uint64_t* host_total = nullptr;  // pinned
+    hipEvent_t ev[8] = {};
+    bool events = false;
+    uint32_t* last_keys = nullptr;  // sorted pair arrays of the last frame
+    uint32_t* last_vals = nullptr;
+    gs_stats stats{};
+    // multi-GPU shard config
+    int32_t rank = 0, world = 1;
+    int64_t index_base = 0;
+
+    ~gs_handle() {
+        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &ntiles, &offsets, &partials, &total,
+                          &keys, &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &xmask, &xcounts, &xtotal,
+                          &rdkey, &rntiles, &roffsets, &rpartials})
+            b->release();
+        if (host_total) (void)hipHostFree(host_total);
+        if (host_xtotal) (void)hipHostFree(host_xtotal);
+        if (events)
+            for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+
+    gs::SceneDev scene_dev() const {
+        gs::SceneDev s;
+        s.p0 = p0.as<const float4>();
+        s.p1 = p1.as<const float4>();
+        s.p2 = p2.as<const float4>();
+        s.p3 = p3.as<const float2>();
+        s.sh4 = sh4.as<const float4>();
+        s.sh1 = sh1.as<const float>();
+        s.n = (uint32_t)n;
+        return s;
+    }
+};
+
+namespace {
+
+// Crop (instanced_splat_renderer.mm:382-386) and store SoA.
+gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& opt) {
+    if (!sc || sc->n < 0 || (sc->n > 0 && (!sc->pos || !sc->rot || !sc->scale || !sc->opacity || !sc->color)))
+        return fail(GS_ERR_INVALID_ARG, "gs_scene_soa: null array");
+    if (opt.sh_degree < 0 || opt.sh_degree > 3) return fail(GS_ERR_INVALID_ARG, "sh_degree must be 0..3");
+    if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
+    if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
+    h->opt = opt;
+    h->has_sh = opt.sh_degree > 0;
+    std::vector<int64_t> keep;
+    keep.reserve((size_t)sc->n);
+    const float r = opt.crop_radius;
+    for (int64_t i = 0; i < sc->n; ++i) {
+        const float* p = sc->pos + i * 3;
+        if (!opt.crop || (std::fabs(p[0]) < r && std::fabs(p[1]) < r && std::fabs(p[2]) < r)) keep.push_back(i);
+    }
+    const int64_t m = (int64_t)keep.size();
+    h->n = m;
+    h->pos.resize(m * 3);
+    h->rot.resize(m * 4);
+    h->scale.resize(m * 3);
+    h->opacity.resize(m);
+    h->color.resize(m * 3);
+    if (h->has_sh) h->sh_rest.resize(m * 45);
+    for (int64_t k = 0; k < m; ++k) {
+        int64_t i = keep[k];
+        std::memcpy(&h->pos[k * 3], sc->pos + i * 3, 12);
+        std::memcpy(&h->rot[k * 4], sc->rot + i * 4, 16);
+        std::memcpy(&h->scale[k * 3], sc->scale + i * 3, 12);
+        h->opacity[k] = sc->opacity[i];
+        std::memcpy(&h->color[k * 3], sc->color + i * 3, 12);
+        if (h->has_sh) std::memcpy(&h->sh_rest[k * 45], sc->sh_rest + i * 45, 45 * 4);
+    }
+    return GS_OK;
+}
+
+gs_status scene_from_points(const PointData* pts, int64_t n, const std::vector<float>* raw_dc,
+                            const gs_options& opt, gs_handle* h) {
+    std::vector<float> pos(n * 3), rot(n * 4), scale(n * 3), op(n), col(n * 3), rest;
+    const bool sh = opt.sh_degree > 0;
+    if (sh) rest.resize(n * 45);
+    for (int64_t i = 0; i < n; ++i) {
+        const PointData& p = pts[i];
+        pos[i * 3 + 0] = p.x; pos[i * 3 + 1] = p.y; pos[i * 3 + 2] = p.z;
+        rot[i * 4 + 0] = p.rot_0; rot[i * 4 + 1] = p.rot_1; rot[i * 4 + 2] = p.rot_2; rot[i * 4 + 3] = p.rot_3;
+        scale[i * 3 + 0] = p.scale_x; scale[i * 3 + 1] = p.scale_y; scale[i * 3 + 2] = p.scale_z;
+        op[i] = p.opacity;
+        if (sh && raw_dc) {
+            for (int c = 0; c < 3; ++c) col[i * 3 + c] = (*raw_dc)[i * 3 + c];
+        } else {
+            col[i * 3 + 0] = p.r; col[i * 3 + 1] = p.g; col[i * 3 + 2] = p.b;
+        }
+        if (sh) std::memcpy(&rest[i * 45], p.sh_rest, 45 * 4);
+    }
+    gs_scene_soa sc{n, pos.data(), rot.data(), scale.data(), op.data(), col.data(), sh ? rest.data() : nullptr};
+    return build_scene(h, &sc, opt);
+}
+
+// Host-side frame uniforms; VP = P·V with the contract's summation order.
+gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
+    gs::FrameUniforms u{};
+    std::memcpy(u.V, V, 64);
+    std::memcpy(u.P, P, 64);
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r)
+            u.VP[c * 4 + r] = ((P[0 * 4 + r] * V[c * 4 + 0] + P[1 * 4 + r] * V[c * 4 + 1]) +
+                               P[2 * 4 + r] * V[c * 4 + 2]) + P[3 * 4 + r] * V[c * 4 + 3];
+    for (int j = 0; j < 3; ++j)
+        u.campos[j] = -((V[j * 4 + 0] * V[12] + V[j * 4 + 1] * V[13]) + V[j * 4 + 2] * V[14]);
+    u.campos[3] = 0.0f;
+    u.width = W;
+    u.height = H;
+    u.tiles_x = (W + gs::kTile - 1) / gs::kTile;
+    u.tiles_y = (H + gs::kTile - 1) / gs::kTile;
+    return u;
+}
+
+int bits_for(uint32_t v) {  // bits needed to represent values < v
+    int b = 0;
+    while (b < 32 && (1ull << b) < v) ++b;
+    return b;
+}
+
+gs_status check_ready(gs_handle* h) {
+    if (!h) return fail(GS_ERR_INVALID_ARG, "null handle");
+    if (!h->initialized) return fail(GS_ERR_STATE, "gs_initialize not called");
+    GS_HIP(hipSetDevice(h->device));
+    return GS_OK;
+}
+
+gs_status ensure_frame_scratch(gs_handle* h) {
+    const size_t n = (size_t)std::max<int64_t>(h->n, 1);
+    GS_HIP(h->rec.reserve(n * sizeof(gs::Record3)));
+    GS_HIP(h->dkey.reserve(n * 4));
+    GS_HIP(h->ntiles.reserve(n * 4));
+    GS_HIP(h->offsets.reserve(n * 4));
+    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 8));
+    GS_HIP(h->total.reserve(8));
+    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 8, hipHostMallocDefault));
+    if (h->opt.stage_timing && !h->events) {
+        for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
+        h->events = true;
+    }
+    return GS_OK;
+}
+
+void mark(gs_handle* h, int k, hipStream_t st) {
+    if (h->opt.stage_timing && h->events) (void)hipEventRecord(h->ev[k], st);
+}
+
+float elapsed(gs_handle* h, int a, int b) {
+    float ms = 0.0f;
+    if (h->opt.stage_timing && h->events) (void)hipEventElapsedTime(&ms, h->ev[a], h->ev[b]);
+    return ms;
+}
+
+// Stages 1-2: project all splats and prefix-sum the tile counts; returns P.
+gs_status project_and_count(gs_handle* h, const gs::FrameUniforms& U, hipStream_t st, uint64_t* pairs) {
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(),
+                                 h->dkey.as<uint32_t>(), h->ntiles.as<uint32_t>(), st));
+    mark(h, 1, st);
+    GS_HIP(gs::launch_exclusive_scan(h->ntiles.as<uint32_t>(), h->offsets.as<uint32_t>(),
+                                     h->partials.as<uint64_t>(), h->total.as<uint64_t>(), (uint32_t)h->n, st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
+    mark(h, 2, st);
+    GS_HIP(hipStreamSynchronize(st));  // P sizes the pair buffers and sort grids
+    *pairs = *h->host_total;
+    if (*pairs >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,tile) pairs");
+    return GS_OK;
+}
+
+gs_status ensure_pair_scratch(gs_handle* h, uint64_t P, uint32_t T) {
+    const size_t p = (size_t)std::max<uint64_t>(P, 1);
+    GS_HIP(h->keys.reserve(p * 4));
+    GS_HIP(h->vals.reserve(p * 4));
+    GS_HIP(h->tkeys.reserve(p * 4));
+    GS_HIP(h->tvals.reserve(p * 4));
+    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
+    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
+    return GS_OK;
+}
+
+// Stages 3-6 on the pairs already emitted into h->keys/h->vals.
+gs_status sort_and_composite(gs_handle* h, uint64_t P, const gs::FrameUniforms& U, const float4* rec,
+                             int rec_stride, int row_mod, int row_rem, int compact, float4* out, hipStream_t st) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    const int bits = bits_for(T) + gs::kDepthBits;
+    bool in_tmp = false;
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(),
+                                 h->tvals.as<uint32_t>(), (uint32_t)P, bits, h->sort_scratch.as<uint32_t>(),
+                                 &in_tmp, st));
+    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+    h->last_keys = sk;
+    h->last_vals = sv;
+    mark(h, 4, st);
+    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
+    mark(h, 5, st);
+    gs::CompositeArgs ca;
+    ca.vals = sv;
+    ca.ranges = h->ranges.as<uint2>();
+    ca.rec = rec;
+    ca.rec_stride = rec_stride;
+    ca.width = U.width;
+    ca.height = U.height;
+    ca.tiles_x = U.tiles_x;
+    ca.tiles_y = U.tiles_y;
+    ca.row_mod = row_mod;
+    ca.row_rem = row_rem;
+    ca.compact = compact;
+    ca.out = out;
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, st));
+    mark(h, 6, st);
+    h->stats.sort_bits = bits;
+    h->stats.sort_passes = (bits + 7) / 8;
+    return GS_OK;
+}
+
+void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
+    gs_stats& s = h->stats;
+    s.splats = h->n;
+    s.pairs = (int64_t)P;
+    s.tiles = (int64_t)U.tiles_x * U.tiles_y;
+    s.width = U.width;
+    s.height = U.height;
+    const int64_t N = h->n, T = s.tiles;
+    const int64_t bin = 56 + (h->opt.sh_degree > 0 ? 4 * 3 * sh_coeffs(h->opt.sh_degree) : 0);
+    // Algorithmic bytes: what each stage must move at minimum.
+    s.bytes_preprocess = N * (bin + 48 + 8);
+    s.bytes_scan = N * 8;
+    s.bytes_duplicate = N * (16 + 8) + (int64_t)P * 8;
+    s.bytes_sort = (int64_t)s.sort_passes * (int64_t)P * 20;
+    s.bytes_ranges = (int64_t)P * 4 + T * 8;
+    s.bytes_composite = T * 8 + (int64_t)P * (4 + 48) + (int64_t)U.width * U.height * 16;
+    if (h->opt.stage_timing && h->events) {
+        (void)hipEventSynchronize(h->ev[6]);
+        s.ms_preprocess = elapsed(h, 0, 1);
+        s.ms_scan = elapsed(h, 1, 2);
+        s.ms_duplicate = elapsed(h, 2, 3);
+        s.ms_sort = elapsed(h, 3, 4);
+        s.ms_ranges = elapsed(h, 4, 5);
+        s.ms_composite = elapsed(h, 5, 6);
+        s.ms_total = elapsed(h, 0, 6);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t gs_abi_version(void) { return GSPLAT_ABI_VERSION; }
+
+const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+void gs_default_options(gs_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof *o);
+    o->mode = GS_MODE_TILE;
+    o->sh_degree = 0;
+    o->crop = 1;
+    o->crop_radius = 5.0f;
+    o->stage_timing = 0;
+}
+
+gs_status gs_create_from_soa(const gs_scene_soa* scene, const gs_options* opt, gs_handle** out) {
+    if (!out) return fail(GS_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    gs_options o;
+    gs_default_options(&o);
+    if (opt) o = *opt;
+    gs_handle* h = new gs_handle();
+    gs_status s = build_scene(h, scene, o);
+    if (s != GS_OK) {
+        delete h;
+        return s;
+    }
+    *out = h;
+    return GS_OK;
+}
+
+gs_status gs_create_from_points(const float* points, int64_t n, const gs_options* opt, gs_handle** out) {
+    if (!out || (!points && n > 0) || n < 0) return fail(GS_ERR_INVALID_ARG, "bad points");
+    *out = nullptr;
+    gs_options o;
+    gs_default_options(&o);
+    if (opt) o = *opt;
+    if (o.sh_degree != 0) return fail(GS_ERR_INVALID_ARG, "PointData carries converted colour only: sh_degree 0");
+    gs_handle* h = new gs_handle();
+    gs_status s = scene_from_points(reinterpret_cast<const PointData*>(points), n, nullptr, o, h);
+    if (s != GS_OK) {
+        delete h;
+        return s;
+    }
+    *out = h;
+    return GS_OK;
+}
+
+gs_status gs_create(const char* ply_path, const gs_options* opt, gs_handle** out) {
+    if (!out || !ply_path) return fail(GS_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    gs_options o;
+    gs_default_options(&o);
+    if (opt) o = *opt;
+    std::vector<PointData> pts;
+    std::vector<float> dc;
+    if (!PLYLoader::load(ply_path, pts, &dc, true))
+        return fail(GS_ERR_IO, std::string("failed to load PLY: ") + ply_path);
+    gs_handle* h = new gs_handle();
+    gs_status s = scene_from_points(pts.data(), (int64_t)pts.size(), &dc, o, h);
+    if (s != GS_OK) {
+        delete h;
+        return s;
+    }
+    *out = h;
+    return GS_OK;
+}
+
+gs_status gs_initialize(gs_handle* h, int32_t device) {
+    if (!h) return fail(GS_ERR_INVALID_ARG, "null handle");
+    int count = 0;
+    GS_HIP(hipGetDeviceCount(&count));
+    if (device < 0 || device >= count) return fail(GS_ERR_DEVICE, "no such HIP device");
+    GS_HIP(hipSetDevice(device));
+    h->device = device;
+    const size_t n = (size_t)std::max<int64_t>(h->n, 1);
+    // HBM layout: four SoA float4/float2 planes, optional SH planes.
+    std::vector<float> a((size_t)n * 4), b((size_t)n * 4), c((size_t)n * 4), d((size_t)n * 2);
+    for (int64_t i = 0; i < h->n; ++i) {
+        a[i * 4 + 0] = h->pos[i * 3 + 0]; a[i * 4 + 1] = h->pos[i * 3 + 1];
+        a[i * 4 + 2] = h->pos[i * 3 + 2]; a[i * 4 + 3] = h->opacity[i];
+        std::memcpy(&b[i * 4], &h->rot[i * 4], 16);
+        c[i * 4 + 0] = h->scale[i * 3 + 0]; c[i * 4 + 1] = h->scale[i * 3 + 1];
+        c[i * 4 + 2] = h->scale[i * 3 + 2]; c[i * 4 + 3] = h->color[i * 3 + 0];
+        d[i * 2 + 0] = h->color[i * 3 + 1]; d[i * 2 + 1] = h->color[i * 3 + 2];
+    }
+    GS_HIP(h->p0.reserve(n * 16));
+    GS_HIP(h->p1.reserve(n * 16));
+    GS_HIP(h->p2.reserve(n * 16));
+    GS_HIP(h->p3.reserve(n * 8));
+    GS_HIP(hipMemcpy(h->p0.ptr, a.data(), n * 16, hipMemcpyHostToDevice));
+    GS_HIP(hipMemcpy(h->p1.ptr, b.data(), n * 16, hipMemcpyHostToDevice));
+    GS_HIP(hipMemcpy(h->p2.ptr, c.data(), n * 16, hipMemcpyHostToDevice));
+    GS_HIP(hipMemcpy(h->p3.ptr, d.data(), n * 8, hipMemcpyHostToDevice));
+    if (h->has_sh) {
+        // k-major, rgb-interleaved coefficient stream: flat j = 3k + ch
+        // (k = 0..K-1) <- f_rest[ch*15 + k] (PLY channel-major order).
+        const int K = sh_coeffs(h->opt.sh_degree), NF = 3 * K, NP4 = NF / 4;
+        std::vector<float> planes((size_t)std::max(NP4, 1) * n * 4), tail(n);
+        for (int64_t i = 0; i < h->n; ++i) {
+            float flat[45];
+            for (int k = 0; k < K; ++k)
+                for (int ch = 0; ch < 3; ++ch) flat[3 * k + ch] = h->sh_rest[i * 45 + ch * 15 + k];
+            for (int m = 0; m < NP4; ++m) std::memcpy(&planes[((size_t)m * n + i) * 4], &flat[4 * m], 16);
+            if (NF % 4) tail[i] = flat[NF - 1];
+        }
+        GS_HIP(h->sh4.reserve(planes.size() * 4));
+        GS_HIP(hipMemcpy(h->sh4.ptr, planes.data(), planes.size() * 4, hipMemcpyHostToDevice));
+        GS_HIP(h->sh1.reserve(n * 4));
+        GS_HIP(hipMemcpy(h->sh1.ptr, tail.data(), n * 4, hipMemcpyHostToDevice));
+    }
+    h->initialized = true;
+    return GS_OK;
+}
+
+int64_t gs_point_count(const gs_handle* h) { return h ? h->n : 0; }
+
+void gs_destroy(gs_handle* h) {
+    if (!h) return;
+    if (h->device >= 0) (void)hipSetDevice(h->device);
+    delete h;
+}
+
+gs_status gs_set_mode(gs_handle* h, int32_t mode) {
+    if (!h || (mode != GS_MODE_TILE && mode != GS_MODE_LIVE50)) return fail(GS_ERR_INVALID_ARG, "bad mode");
+    h->opt.mode = mode;
+    return GS_OK;
+}
+
+gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, float* out_rgba,
+                    int32_t out_is_device, void* stream) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if (!view || !proj || !out_rgba || W <= 0 || H <= 0 || W > 65535 || H > 65535)
+        return fail(GS_ERR_INVALID_ARG, "gs_render: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    if (bits_for(T) + gs::kDepthBits > 32) return fail(GS_ERR_UNSUPPORTED, "too many tiles for 32-bit keys");
+    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    float4* out = reinterpret_cast<float4*>(out_rgba);
+    if (!out_is_device) {
+        GS_HIP(h->fb.reserve((size_t)W * H * 16));
+        out = h->fb.as<float4>();
+    }
+    std::memset(&h->stats, 0, sizeof h->stats);
+    mark(h, 0, st);
+    uint64_t P = 0;
+    if ((s = project_and_count(h, U, st, &P)) != GS_OK) return s;
+    if ((s = ensure_pair_scratch(h, P, T)) != GS_OK) return s;
+    GS_HIP(gs::launch_duplicate(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->ntiles.as<uint32_t>(),
+                                h->offsets.as<uint32_t>(), (uint32_t)h->n, (uint32_t)U.tiles_x,
+                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    mark(h, 3, st);
+    if ((s = sort_and_composite(h, P, U, h->rec.as<float4>(), 3, 1, 0, 0, out, st)) != GS_OK) return s;
+    if (!out_is_device) {
+        GS_HIP(hipMemcpyAsync(out_rgba, out, (size_t)W * H * 16, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+    }
+    fill_stats(h, P, U);
+    return GS_OK;
+}
+
+gs_status gs_last_stats(const gs_handle* h, gs_stats* out) {
+    if (!h || !out) return fail(GS_ERR_INVALID_ARG, "null argument");
+    *out = h->stats;
+    return GS_OK;
+}
+
+gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
+                          void* records, uint32_t* dkeys, uint32_t* ntiles) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "bad arguments");
+    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    hipStream_t st = nullptr;
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
+                                 h->ntiles.as<uint32_t>(), st));
+    GS_HIP(hipStreamSynchronize(st));
+    const size_t n = (size_t)h->n;
+    if (records) GS_HIP(hipMemcpy(records, h->rec.ptr, n * sizeof(gs::Record3), hipMemcpyDeviceToHost));
+    if (dkeys) GS_HIP(hipMemcpy(dkeys, h->dkey.ptr, n * 4, hipMemcpyDeviceToHost));
+    if (ntiles) GS_HIP(hipMemcpy(ntiles, h->ntiles.ptr, n * 4, hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int64_t cap, int64_t* count) {
+    if (!h || !count) return fail(GS_ERR_INVALID_ARG, "null argument");
+    int64_t P = h->stats.pairs;
+    *count = P;
+    if (!h->last_keys || P == 0) return GS_OK;
+    int64_t m = std::min(P, cap);
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(hipDeviceSynchronize());
+    if (keys) GS_HIP(hipMemcpy(keys, h->last_keys, (size_t)m * 4, hipMemcpyDeviceToHost));
+    if (vals) GS_HIP(hipMemcpy(vals, h->last_vals, (size_t)m * 4, hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+gs_status gs_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, int64_t n,
+                              int32_t bits, void* stream) {
+    if (n < 0 || n >= (int64_t)UINT32_MAX || bits < 0 || bits > 32 || (n > 0 && (!keys || !vals || !tmp_keys || !tmp_vals)))
+        return fail(GS_ERR_INVALID_ARG, "gs_radix_sort_pairs: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint32_t* scratch = nullptr;
+    GS_HIP(hipMalloc(&scratch, gs::radix_sort_scratch_words((uint32_t)n) * 4));
+    bool in_tmp = false;
+    hipError_t e = gs::launch_radix_sort(keys, vals, tmp_keys, tmp_vals, (uint32_t)n, bits, scratch, &in_tmp, st);
+    if (e == hipSuccess && in_tmp) {
+        e = hipMemcpyAsync(keys, tmp_keys, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(vals, tmp_vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(scratch);
+    GS_HIP(e);
+    return GS_OK;
+}
+
+// ---- multi-GPU: tile-row ownership ---------------------------
+int32_t gs_exchange_record_bytes(void) { return gs::kXRecFloat4 * 16; }
+
+gs_status gs_shard_configure(gs_handle* h, int32_t rank, int32_t world, int64_t index_base) {
+    if (!h || world < 1 || world > gs::kMaxWorld || rank < 0 || rank >= world || index_base < 0 ||
+        index_base + h->n >= (int64_t)UINT32_MAX)
+        return fail(GS_ERR_INVALID_ARG, "gs_shard_configure: bad rank/world/index_base");
+    h->rank = rank;
+    h->world = world;
+    h->index_base = index_base;
+    return GS_OK;
+}
+
+gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, void* send,
+                           int64_t send_cap_bytes, int64_t* send_counts, void* stream) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if (!view || !proj || !send_counts || W <= 0 || H <= 0 || W > 65535 || H > 65535)
+        return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    const uint32_t n = (uint32_t)h->n;
+    const uint32_t nb = (n + gs::kScanItems - 1) / gs::kScanItems;
+    GS_HIP(h->xmask.reserve((size_t)std::max<uint32_t>(n, 1) * 4));
+    GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
+    GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
+    if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
+                                 h->ntiles.as<uint32_t>(), st));
+    GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
+    GS_HIP(gs::launch_shard_count(h->rec.as<float4>(), h->ntiles.as<uint32_t>(), n, h->world,
+                                  h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
+    GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
+    GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    int64_t total = 0;
+    for (int d = 0; d < h->world; ++d) {
+        send_counts[d] = h->host_xtotal[d];
+        total += h->host_xtotal[d];
+    }
+    if (total * gs_exchange_record_bytes() > send_cap_bytes)
+        return fail(GS_ERR_OOM, "gs_shard_project: send buffer too small (" +
+                                    std::to_string(total * gs_exchange_record_bytes()) + " bytes needed)");
+    if (total > 0 && !send) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: null send buffer");
+    GS_HIP(gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
+                                 (uint32_t)h->index_base, h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
+                                 static_cast<float4*>(send), st));
+    return GS_OK;
+}
+
+gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
+                          void* stream) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !out_rgba || W <= 0 || H <= 0 || W > 65535 ||
+        H > 65535)
+        return fail(GS_ERR_INVALID_ARG, "gs_shard_render: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const gs::FrameUniforms U = make_uniforms(I, I, W, H);
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    const size_t mm = (size_t)std::max<int64_t>(m, 1);
+    GS_HIP(h->rdkey.reserve(mm * 4));
+    GS_HIP(h->rntiles.reserve(mm * 4));
+    GS_HIP(h->roffsets.reserve(mm * 4));
+    GS_HIP(h->rpartials.reserve((mm + gs::kScanItems - 1) / gs::kScanItems * 8 + 8));
+    const float4* rv = static_cast<const float4*>(recv);
+    GS_HIP(gs::launch_recv_count(rv, (uint32_t)m, h->world, h->rank, h->rntiles.as<uint32_t>(),
+                                 h->rdkey.as<uint32_t>(), st));
+    GS_HIP(gs::launch_exclusive_scan(h->rntiles.as<uint32_t>(), h->roffsets.as<uint32_t>(),
+                                     h->rpartials.as<uint64_t>(), h->total.as<uint64_t>(), (uint32_t)m, st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    const uint64_t P = *h->host_total;
+    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "too many pairs");
+    if ((s = ensure_pair_scratch(h, P, T)) != GS_OK) return s;
+    GS_HIP(gs::launch_recv_duplicate(rv, h->rdkey.as<uint32_t>(), h->rntiles.as<uint32_t>(),
+                                     h->roffsets.as<uint32_t>(), (uint32_t)m, (uint32_t)U.tiles_x, h->world, h->rank,
+                                     h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    if ((s = sort_and_composite(h, P, U, rv, gs::kXRecFloat4, h->world, h->rank, 1,
+                                reinterpret_cast<float4*>(out_rgba), st)) != GS_OK)
+        return s;
+    h->stats.pairs = (int64_t)P;
+    h->stats.tiles = T;
+    return GS_OK;
+}
+
+// ---- PLY / camera -----------------------------------------------------------
+gs_status gs_ply_load(const char* path, int32_t compat, float** points, int64_t* n) {
+    if (!path || !points || !n) return fail(GS_ERR_INVALID_ARG, "null argument");
+    *points = nullptr;
+    *n = 0;
+    std::vector<PointData> pts;
+    bool ok = PLYLoader::load(path, pts, nullptr, compat != 0);
+    if (!pts.empty()) {
+        float* buf = static_cast<float*>(std::malloc(pts.size() * sizeof(PointData)));
+        if (!buf) return fail(GS_ERR_OOM, "malloc");
+        std::memcpy(buf, pts.data(), pts.size() * sizeof(PointData));
+        *points = buf;
+        *n = (int64_t)pts.size();
+    }
+    return ok ? GS_OK : fail(GS_ERR_IO, std::string("PLY load failed: ") + path);
+}
+
+void gs_ply_free(float* points) { std::free(points); }
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// gs_device.h — device-side building blocks of the splat pipeline (gfx950).
+//
+// Arithmetic follows DESIGN.md §2 op for op (explicit __builtin_fmaf where
+// the contract fuses, plain ops elsewhere; the whole library is compiled with
+// -ffp-contract=off), so records and framebuffers agree bit for bit with the
+// CPU oracle.  Reference lines are cited on each step.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+constexpr int kTile = 16;                 // 16x16-pixel tiles (gaussian_splat_types.h:9 budget)
+constexpr int kTileThreads = kTile * kTile;
+constexpr int kDepthBits = 15;            // positive half bit patterns are < 0x7C01
+constexpr uint32_t kDepthInf = 0x7C00u;
+constexpr float kQMax = 9.21034037197618f;  // 2 ln 100: exp(-q/2) >= 0.01 (tile.metal:193)
+constexpr float kSat = 0.99f;             // tile.metal:261
+constexpr float kTMin = 0.01f;            // 50layer.metal:219
+
+// Uniforms of one frame (tile.metal:16-21 plus derived values).
+struct FrameUniforms {
+    float V[16];      // view, column-major
+    float P[16];      // projection
+    float VP[16];     // P·V (instanced_splat_renderer.mm:453), host-computed
+    float campos[4];  // eye position for SH view directions
+    int32_t width, height;
+    int32_t tiles_x, tiles_y;
+};
+
+// Scene SoA resident in HBM: coalesced 16-B loads per lane.
+struct SceneDev {
+    const float4* p0;   // x, y, z, opacity
+    const float4* p1;   // qw, qx, qy, qz
+    const float4* p2;   // sx, sy, sz, c0   (c = rgb for SH0, raw f_dc otherwise)
+    const float2* p3;   // c1, c2
+    const float4* sh4;  // [plane][n] coefficient planes, k-major (r,g,b interleaved)
+    const float* sh1;   // [n] trailing coefficient (deg 1 and 3)
+    uint32_t n;
+};
+
+// 48-byte record = 3 float4: (cx, cy, ax, ay) (bx, by, op, r) (g, b, rect_lo, rect_hi)
+struct Record3 {
+    float4 a, b, c;
+};
+
+__device__ __forceinline__ float xform_row(const float* m, int r, float x, float y, float z) {
+    return __builtin_fmaf(m[8 + r], z, __builtin_fmaf(m[4 + r], y, __builtin_fmaf(m[0 + r], x, m[12 + r])));
+}
+
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return __builtin_fmaf(a2, b2, __builtin_fmaf(a1, b1, a0 * b0));
+}
+
+// exp(x), x in [-4.61, 0]: 2^(x log2 e) by rint + degree-6 fma chain + ldexp.
+// Same op sequence as oracle ora_expf.
+__device__ __forceinline__ float gs_exp(float x) {
+    float t = x * 1.44269504088896341f;
+    float n = __builtin_rintf(t);
+    float f = t - n;
+    float p = 1.5403530393381606e-4f;
+    p = __builtin_fmaf(p, f, 1.3333558146428443e-3f);
+    p = __builtin_fmaf(p, f, 9.6181291076284772e-3f);
+    p = __builtin_fmaf(p, f, 5.5504108664821580e-2f);
+    p = __builtin_fmaf(p, f, 2.4022650695910071e-1f);
+    p = __builtin_fmaf(p, f, 6.9314718055994531e-1f);
+    p = __builtin_fmaf(p, f, 1.0f);
+    return __builtin_ldexpf(p, (int)n);
+}
+
+// IEEE half bits, round to nearest even (v_cvt_f16_f32).
+__device__ __forceinline__ uint32_t half_bits(float f) {
+    _Float16 h = (_Float16)f;
+    return (uint32_t)__builtin_bit_cast(unsigned short, h);
+}
+
+__device__ __forceinline__ float4 ldg4(const float4* p) { return *p; }
+
+}  // namespace gs

@@ -1,0 +1,79 @@
+// gs_kernels.h — host-side launchers of the HIP kernels (one translation unit
+// per stage).  All launches are asynchronous on the given stream.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_device.h"
+
+namespace gs {
+
+// ---- preprocess.hip ------------------------------------------------------
+hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
+                             uint32_t* dkey, uint32_t* ntiles, hipStream_t st);
+
+// ---- scan.hip --------------------------------------------------------------
+constexpr int kScanItems = 4096;  // per block
+// Exclusive scan of counts[n] into offsets[n]; *total (device u64) = sum.
+// partials: ceil(n / kScanItems) u64 scratch.
+hipError_t launch_exclusive_scan(const uint32_t* counts, uint32_t* offsets, uint64_t* partials, uint64_t* total,
+                                 uint32_t n, hipStream_t st);
+
+// ---- binning.hip -----------------------------------------------------------
+// Emit (tile << 15 | dkey, splat index + index_base) for every tile of every
+// splat rect, at offsets[i].
+hipError_t launch_duplicate(const float4* rec, const uint32_t* dkey, const uint32_t* ntiles,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, uint32_t* keys,
+                            uint32_t* vals, hipStream_t st);
+// ranges[tile] = [start, end) in the sorted pair array (zero-initialised here).
+hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* ranges, uint32_t ntiles_total,
+                              hipStream_t st);
+
+// ---- radix_sort.hip --------------------------------------------------------
+constexpr int kSortTile = 4096;  // items per block
+constexpr int kSortBins = 256;
+// Scratch elements (uint32) needed by launch_radix_sort for n items.
+size_t radix_sort_scratch_words(uint32_t n);
+// Stable LSD sort of (keys, vals) on bits [0, bits).  Ping-pongs with
+// tmp_keys / tmp_vals; *result_in_tmp tells where the sorted data ended.
+hipError_t launch_radix_sort(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n,
+                             int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st);
+
+// ---- composite.hip ---------------------------------------------------------
+struct CompositeArgs {
+    const uint32_t* vals;   // sorted splat ids (index into rec)
+    const uint2* ranges;    // [tiles] -> [start, end) into vals
+    const float4* rec;      // records, rec_stride float4 apart (3 local, 4 exchange)
+    int rec_stride;
+    int width, height, tiles_x, tiles_y;
+    int row_mod, row_rem;   // composite tile rows ty with ty % row_mod == row_rem
+    int compact;            // 1: write owned tile rows stacked (band buffer)
+    float4* out;
+};
+// One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
+// break), 1 = live50 rule (T < 0.01 break).
+hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st);
+
+// ---- shard.hip (multi-GPU tile-row ownership) ------------------------------
+constexpr int kXRecFloat4 = 4;  // 64-B exchange record: 48-B record + dkey, global index
+constexpr int kMaxWorld = 32;
+// dest_mask[i]: bit r set iff splat i touches a tile row owned by rank r.
+// counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
+hipError_t launch_shard_count(const float4* rec, const uint32_t* ntiles, uint32_t n, int world,
+                              uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);
+// Exclusive scan of each destination row; dest_total[world].
+hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);
+// Pack exchange records grouped by destination, splat-index order inside.
+hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
+                             int world, uint32_t index_base, const uint32_t* counts, const uint32_t* dest_total,
+                             uint32_t nblocks, float4* send, hipStream_t st);
+// Per received record: tiles in owned rows, and dkey.
+hipError_t launch_recv_count(const float4* recv, uint32_t m, int world, int rank, uint32_t* ntiles,
+                             uint32_t* dkey, hipStream_t st);
+// duplicate for received records restricted to owned tile rows.
+hipError_t launch_recv_duplicate(const float4* recv, const uint32_t* dkey, const uint32_t* ntiles,
+                                 const uint32_t* offsets, uint32_t m, uint32_t tiles_x, int world, int rank,
+                                 uint32_t* keys, uint32_t* vals, hipStream_t st);
+
+}  // namespace gs

@@ -1,0 +1,254 @@
+// preprocess.hip — per-splat projection.
+//
+// One lane per splat, SoA float4 loads (fully coalesced 16 B/lane), output the
+// 48-byte composite record, the 15-bit depth key and the tile count.  This is
+// the reference's vertex_main (shaders/gaussian_splat_tile.metal:85-157) run
+// ONCE per splat instead of six times per instance, plus the closed form of
+// Metal's fixed-function quad raster (K6) reduced to a conservative pixel
+// rectangle.  Memory-bound: N·(B_in + 56) bytes per frame.
+#include "gs_device.h"
+#include "gs_kernels.h"
+
+namespace gs {
+
+
+template <int DEG>
+__device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px, float py, float pz,
+                                         const float* campos, float c0, float c1, float c2,
+                                         float& r, float& g, float& b) {
+    if constexpr (DEG == 0) {
+        r = c0; g = c1; b = c2;  // colour converted at load (ply_loader.cpp:132-139)
+    } else {
+        if (c0 == 0.0f && c1 == 0.0f && c2 == 0.0f) {  // all-zero f_dc quirk (ply_loader.cpp:133)
+            r = g = b = 0.0f;
+            return;
+        }
+        const float SH_C0 = 0.28209479177387814f;
+        const float C1 = 0.4886025119029199f;
+        float dx = px - campos[0], dy = py - campos[1], dz = pz - campos[2];
+        float l2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+        float inv = 1.0f / sqrtf(l2);
+        float x = dx * inv, y = dy * inv, z = dz * inv;
+        constexpr int K = DEG == 1 ? 3 : (DEG == 2 ? 8 : 15);
+        float bas[K];
+        bas[0] = (-C1) * y;
+        bas[1] = C1 * z;
+        bas[2] = (-C1) * x;
+        if constexpr (DEG >= 2) {
+            float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            bas[3] = 1.0925484305920792f * xy;
+            bas[4] = -1.0925484305920792f * yz;
+            bas[5] = 0.31539156525252005f * ((2.0f * zz - xx) - yy);
+            bas[6] = -1.0925484305920792f * xz;
+            bas[7] = 0.5462742152960396f * (xx - yy);
+            if constexpr (DEG >= 3) {
+                bas[8] = (-0.5900435899266435f * y) * (3.0f * xx - yy);
+                bas[9] = (2.890611442640554f * xy) * z;
+                bas[10] = (-0.4570457994644658f * y) * ((4.0f * zz - xx) - yy);
+                bas[11] = (0.3731763325901154f * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+                bas[12] = (-0.4570457994644658f * x) * ((4.0f * zz - xx) - yy);
+                bas[13] = (1.445305721320277f * z) * (xx - yy);
+                bas[14] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
+            }
+        }
+        // Coefficients are stored k-major with r,g,b interleaved: flat j = 3k + ch,
+        // in float4 planes (coalesced across lanes) plus one scalar plane.
+        constexpr int NF = 3 * K;
+        constexpr int NP4 = NF / 4;
+        float coef[NF];
+#pragma unroll
+        for (int m = 0; m < NP4; ++m) {
+            float4 v = s.sh4[(size_t)m * s.n + i];
+            coef[4 * m + 0] = v.x;
+            coef[4 * m + 1] = v.y;
+            coef[4 * m + 2] = v.z;
+            coef[4 * m + 3] = v.w;
+        }
+        if constexpr (NF % 4 != 0) coef[NF - 1] = s.sh1[i];
+        float acc0 = SH_C0 * c0, acc1 = SH_C0 * c1, acc2 = SH_C0 * c2;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc0 = __builtin_fmaf(bas[k], coef[3 * k + 0], acc0);
+            acc1 = __builtin_fmaf(bas[k], coef[3 * k + 1], acc1);
+            acc2 = __builtin_fmaf(bas[k], coef[3 * k + 2], acc2);
+        }
+        acc0 = acc0 + 0.5f;
+        acc1 = acc1 + 0.5f;
+        acc2 = acc2 + 0.5f;
+        r = fminf(fmaxf(acc0, 0.0f), 1.0f);
+        g = fminf(fmaxf(acc1, 0.0f), 1.0f);
+        b = fminf(fmaxf(acc2, 0.0f), 1.0f);
+    }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const FrameUniforms U,
+                                                         float4* __restrict__ rec, uint32_t* __restrict__ dkey,
+                                                         uint32_t* __restrict__ ntiles) {
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= s.n) return;
+    const float* V = U.V;
+    const float* VP = U.VP;
+    uint32_t count = 0;
+    uint32_t key = 0;
+
+    float4 a0 = s.p0[i];
+    float px = a0.x, py = a0.y, pz = a0.z;
+    // K3: view position, zFront (tile.metal:94-105)
+    float vx = xform_row(V, 0, px, py, pz);
+    float vy = xform_row(V, 1, px, py, pz);
+    float vz = xform_row(V, 2, px, py, pz);
+    float zf = -vz;
+    if (zf >= 1e-4f) {
+        // K6 z-clip on NDC z in [0,1] (tile.metal:145-152)
+        float clx = xform_row(VP, 0, px, py, pz);
+        float cly = xform_row(VP, 1, px, py, pz);
+        float clz = xform_row(VP, 2, px, py, pz);
+        float clw = xform_row(VP, 3, px, py, pz);
+        float invw = 1.0f / clw;
+        float ndcz = clz * invw;
+        if (ndcz >= 0.0f && ndcz <= 1.0f && zf >= 0.001f) {
+            float4 q = s.p1[i];
+            float4 a2 = s.p2[i];
+            // K1 (tile.metal:40-49)
+            float qs = q.x * q.x;
+            qs = __builtin_fmaf(q.y, q.y, qs);
+            qs = __builtin_fmaf(q.z, q.z, qs);
+            qs = __builtin_fmaf(q.w, q.w, qs);
+            float qi = 1.0f / sqrtf(qs);
+            float w = q.x * qi, x = q.y * qi, y = q.z * qi, z = q.w * qi;
+            float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+            float wx = w * x, wy = w * y, wz = w * z;
+            float R00 = 1.0f - 2.0f * (yy + zz), R10 = 2.0f * (xy + wz), R20 = 2.0f * (xz - wy);
+            float R01 = 2.0f * (xy - wz), R11 = 1.0f - 2.0f * (xx + zz), R21 = 2.0f * (yz + wx);
+            float R02 = 2.0f * (xz + wy), R12 = 2.0f * (yz - wx), R22 = 1.0f - 2.0f * (xx + yy);
+            // K2: M = R S, Sigma = M M^T (tile.metal:51-60)
+            float M00 = R00 * a2.x, M01 = R01 * a2.y, M02 = R02 * a2.z;
+            float M10 = R10 * a2.x, M11 = R11 * a2.y, M12 = R12 * a2.z;
+            float M20 = R20 * a2.x, M21 = R21 * a2.y, M22 = R22 * a2.z;
+            float S00 = dot3(M00, M01, M02, M00, M01, M02);
+            float S01 = dot3(M00, M01, M02, M10, M11, M12);
+            float S02 = dot3(M00, M01, M02, M20, M21, M22);
+            float S10 = dot3(M10, M11, M12, M00, M01, M02);
+            float S11 = dot3(M10, M11, M12, M10, M11, M12);
+            float S12 = dot3(M10, M11, M12, M20, M21, M22);
+            float S20 = dot3(M20, M21, M22, M00, M01, M02);
+            float S21 = dot3(M20, M21, M22, M10, M11, M12);
+            float S22 = dot3(M20, M21, M22, M20, M21, M22);
+            // K3: Sigma_view = (W Sigma) W^T, W(r,c) = V[c*4+r] (tile.metal:109-115)
+            float W00 = V[0], W01 = V[4], W02 = V[8];
+            float W10 = V[1], W11 = V[5], W12 = V[9];
+            float W20 = V[2], W21 = V[6], W22 = V[10];
+            float T00 = dot3(W00, W01, W02, S00, S10, S20);
+            float T01 = dot3(W00, W01, W02, S01, S11, S21);
+            float T02 = dot3(W00, W01, W02, S02, S12, S22);
+            float T10 = dot3(W10, W11, W12, S00, S10, S20);
+            float T11 = dot3(W10, W11, W12, S01, S11, S21);
+            float T12 = dot3(W10, W11, W12, S02, S12, S22);
+            float T20 = dot3(W20, W21, W22, S00, S10, S20);
+            float T21 = dot3(W20, W21, W22, S01, S11, S21);
+            float T22 = dot3(W20, W21, W22, S02, S12, S22);
+            float V00 = dot3(T00, T01, T02, W00, W01, W02);
+            float V01 = dot3(T00, T01, T02, W10, W11, W12);
+            float V02 = dot3(T00, T01, T02, W20, W21, W22);
+            float V10 = dot3(T10, T11, T12, W00, W01, W02);
+            float V11 = dot3(T10, T11, T12, W10, W11, W12);
+            float V12 = dot3(T10, T11, T12, W20, W21, W22);
+            float V20 = dot3(T20, T21, T22, W00, W01, W02);
+            float V21 = dot3(T20, T21, T22, W10, W11, W12);
+            float V22 = dot3(T20, T21, T22, W20, W21, W22);
+            // Jacobian, reference sign convention (tile.metal:117-123)
+            float fx = U.P[0] * ((float)U.width * 0.5f);
+            float fy = U.P[5] * ((float)U.height * 0.5f);
+            float iz = 1.0f / zf;
+            float iz2 = iz * iz;
+            float J00 = fx * iz, J01 = 0.0f, J02 = ((-fx) * vx) * iz2;
+            float J10 = 0.0f, J11 = fy * iz, J12 = ((-fy) * vy) * iz2;
+            float SJ00 = dot3(V00, V01, V02, J00, J01, J02);
+            float SJ01 = dot3(V10, V11, V12, J00, J01, J02);
+            float SJ02 = dot3(V20, V21, V22, J00, J01, J02);
+            float SJ10 = dot3(V00, V01, V02, J10, J11, J12);
+            float SJ11 = dot3(V10, V11, V12, J10, J11, J12);
+            float SJ12 = dot3(V20, V21, V22, J10, J11, J12);
+            float ca = dot3(J00, J01, J02, SJ00, SJ01, SJ02);
+            float cb = dot3(J00, J01, J02, SJ10, SJ11, SJ12);
+            float cc = dot3(J10, J11, J12, SJ10, SJ11, SJ12);
+            ca = ca + 1e-4f;  // tile.metal:129-131
+            cc = cc + 1e-4f;
+            // K4 eigenSym2x2 (tile.metal:62-83) and radii (:136-140)
+            float tr = ca + cc;
+            float det = ca * cc - cb * cb;
+            float disc = fmaxf(0.0f, (0.25f * tr) * tr - det);
+            float sq = sqrtf(disc);
+            float l1 = 0.5f * tr + sq;
+            float l2 = 0.5f * tr - sq;
+            float e1x, e1y;
+            if (fabsf(cb) > 1e-8f) {
+                float ux = l1 - cc, uy = cb;
+                float il = 1.0f / sqrtf(__builtin_fmaf(uy, uy, ux * ux));
+                e1x = ux * il;
+                e1y = uy * il;
+            } else if (ca >= cc) {
+                e1x = 1.0f;
+                e1y = 0.0f;
+            } else {
+                e1x = 0.0f;
+                e1y = 1.0f;
+            }
+            float e2x = -e1y, e2y = e1x;
+            l1 = fmaxf(l1, 0.0f);
+            l2 = fmaxf(l2, 0.0f);
+            float r1 = 3.0f * sqrtf(l1);
+            float r2 = 3.0f * sqrtf(l2);
+            if (r1 > 0.0f && r2 > 0.0f) {
+                float W_ = (float)U.width, H_ = (float)U.height;
+                float ndcx = clx * invw, ndcy = cly * invw;
+                float cx = (ndcx + 1.0f) * (W_ * 0.5f);
+                float cy = (1.0f - ndcy) * (H_ * 0.5f);
+                float k1 = 3.0f / r1, k2 = 3.0f / r2;
+                float hbx = r1 * fabsf(e1x) + r2 * fabsf(e2x);
+                float hby = r1 * fabsf(e1y) + r2 * fabsf(e2y);
+                float hex = 1.0117f * sqrtf((r1 * e1x) * (r1 * e1x) + (r2 * e2x) * (r2 * e2x));
+                float hey = 1.0117f * sqrtf((r1 * e1y) * (r1 * e1y) + (r2 * e2y) * (r2 * e2y));
+                float hx = fminf(hbx, hex) * 1.0001f + 1.0f;
+                float hy = fminf(hby, hey) * 1.0001f + 1.0f;
+                float x0f = ceilf(cx - hx - 0.5f), x1f = floorf(cx + hx - 0.5f);
+                float y0f = ceilf(cy - hy - 0.5f), y1f = floorf(cy + hy - 0.5f);
+                x0f = fmaxf(x0f, 0.0f);
+                y0f = fmaxf(y0f, 0.0f);
+                x1f = fminf(x1f, W_ - 1.0f);
+                y1f = fminf(y1f, H_ - 1.0f);
+                if (x0f <= x1f && y0f <= y1f) {
+                    uint32_t x0 = (uint32_t)x0f, x1 = (uint32_t)x1f, y0 = (uint32_t)y0f, y1 = (uint32_t)y1f;
+                    float cr, cg, cbl;
+                    float2 a3 = s.p3[i];
+                    sh_color<DEG>(s, i, px, py, pz, U.campos, a2.w, a3.x, a3.y, cr, cg, cbl);
+                    float4* o = rec + 3 * (size_t)i;
+                    o[0] = make_float4(cx, cy, e1x * k1, e1y * k1);
+                    o[1] = make_float4(e2x * k2, e2y * k2, a0.w, cr);
+                    o[2] = make_float4(cg, cbl, __uint_as_float(x0 | (y0 << 16)), __uint_as_float(x1 | (y1 << 16)));
+                    key = kDepthInf - half_bits(zf);
+                    count = ((x1 >> 4) - (x0 >> 4) + 1) * ((y1 >> 4) - (y0 >> 4) + 1);
+                }
+            }
+        }
+    }
+    dkey[i] = key;
+    ntiles[i] = count;
+}
+
+hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
+                             uint32_t* dkey, uint32_t* ntiles, hipStream_t st) {
+    if (s.n == 0) return hipSuccess;
+    dim3 grid((s.n + 255) / 256), block(256);
+    switch (sh_degree) {
+    case 0: preprocess_kernel<0><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
+    case 1: preprocess_kernel<1><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
+    case 2: preprocess_kernel<2><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
+    case 3: preprocess_kernel<3><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gs

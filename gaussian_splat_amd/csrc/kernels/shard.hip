@@ -1,0 +1,211 @@
+// shard.hip — multi-GPU exchange kernels.
+//
+// Scenes are sharded by splat index (rank r holds a contiguous index range).
+// Tiles are owned by rank (tile_row % world): every rank projects its shard,
+// then sends each visible splat's 64-B exchange record to the ranks owning a
+// tile row its rect touches.  Received records arrive in source-rank order,
+// i.e. in global index order, so the receiving rank's stable sort reproduces
+// the single-GPU per-tile order exactly (bit-identical composite).
+#include "gs_kernels.h"
+#include "gs_wave.h"
+
+namespace gs {
+
+constexpr int kShWaves = 4;
+constexpr int kShIpt = kScanItems / 256;  // 16 rounds of 64 per wave
+constexpr int kShWaveItems = 64 * kShIpt;
+
+__device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, int world) {
+    if (ty1 - ty0 + 1 >= (uint32_t)world) return world >= 32 ? 0xFFFFFFFFu : ((1u << world) - 1u);
+    uint32_t m = 0;
+    for (uint32_t t = ty0; t <= ty1; ++t) m |= 1u << (t % (uint32_t)world);
+    return m;
+}
+
+__global__ __launch_bounds__(256) void shard_count_kernel(const float4* __restrict__ rec,
+                                                          const uint32_t* __restrict__ ntiles, uint32_t n,
+                                                          int world, uint32_t* __restrict__ dest_mask,
+                                                          uint32_t* __restrict__ counts, uint32_t nblocks) {
+    __shared__ uint32_t wc[kShWaves][kMaxWorld];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t base = blockIdx.x * kScanItems + wave * kShWaveItems;
+    uint32_t cnt = 0;  // lane d holds this wave's count for destination d
+    for (int k = 0; k < kShIpt; ++k) {
+        uint32_t i = base + k * 64 + lane;
+        uint32_t m = 0;
+        if (i < n && ntiles[i] > 0) {
+            float4 c = rec[3 * (size_t)i + 2];
+            uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+            m = row_mask((lo >> 16) >> 4, (hi >> 16) >> 4, world);
+        }
+        if (i < n) dest_mask[i] = m;
+        for (int d = 0; d < world; ++d) {
+            uint64_t b = __ballot((m >> d) & 1u);
+            if (lane == (uint32_t)d) cnt += (uint32_t)__popcll(b);
+        }
+    }
+    if (lane < (uint32_t)kMaxWorld) wc[wave][lane] = cnt;
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)world) {
+        uint32_t d = threadIdx.x;
+        counts[(size_t)d * nblocks + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+    }
+}
+
+__global__ __launch_bounds__(256) void rows_scan_kernel(uint32_t* __restrict__ counts, uint32_t nblocks,
+                                                        uint32_t* __restrict__ row_total) {
+    __shared__ uint32_t tmp[4];
+    uint32_t* row = counts + (size_t)blockIdx.x * nblocks;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += 256) {
+        uint32_t i = b0 + threadIdx.x;
+        uint32_t v = i < nblocks ? row[i] : 0u;
+        uint32_t t;
+        uint32_t ex = block256_exclusive_scan<uint32_t>(v, tmp, &t);
+        if (i < nblocks) row[i] = carry + ex;
+        carry += t;
+    }
+    if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restrict__ rec,
+                                                         const uint32_t* __restrict__ dkey,
+                                                         const uint32_t* __restrict__ dest_mask, uint32_t n,
+                                                         int world, uint32_t index_base,
+                                                         const uint32_t* __restrict__ counts,
+                                                         const uint32_t* __restrict__ dest_total,
+                                                         uint32_t nblocks, float4* __restrict__ send) {
+    __shared__ uint32_t wc[kShWaves][kMaxWorld];   // per-wave counts -> per-wave offsets
+    __shared__ uint32_t base_d[kMaxWorld];         // this block's start in destination d
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t base = blockIdx.x * kScanItems + wave * kShWaveItems;
+    uint32_t cnt = 0;
+    for (int k = 0; k < kShIpt; ++k) {
+        uint32_t i = base + k * 64 + lane;
+        uint32_t m = i < n ? dest_mask[i] : 0u;
+        for (int d = 0; d < world; ++d) {
+            uint64_t b = __ballot((m >> d) & 1u);
+            if (lane == (uint32_t)d) cnt += (uint32_t)__popcll(b);
+        }
+    }
+    if (lane < (uint32_t)kMaxWorld) wc[wave][lane] = cnt;
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)world) {
+        uint32_t d = threadIdx.x, s = 0;
+        for (int w = 0; w < kShWaves; ++w) {
+            uint32_t c = wc[w][d];
+            wc[w][d] = s;
+            s += c;
+        }
+        uint32_t pre = 0;
+        for (uint32_t e = 0; e < d; ++e) pre += dest_total[e];
+        base_d[d] = pre + counts[(size_t)d * nblocks + blockIdx.x];
+    }
+    __syncthreads();
+    for (int k = 0; k < kShIpt; ++k) {
+        uint32_t i = base + k * 64 + lane;
+        uint32_t m = i < n ? dest_mask[i] : 0u;
+        for (int d = 0; d < world; ++d) {
+            bool bit = (m >> d) & 1u;
+            uint64_t b = __ballot(bit);
+            if (b == 0) continue;
+            uint32_t run = wc[wave][d];
+            if (bit) {
+                uint32_t pos = base_d[d] + run + mbcnt(b);
+                const float4* src = rec + 3 * (size_t)i;
+                float4* dst = send + (size_t)kXRecFloat4 * pos;
+                dst[0] = src[0];
+                dst[1] = src[1];
+                dst[2] = src[2];
+                dst[3] = make_float4(__uint_as_float(dkey[i]), __uint_as_float(index_base + i), 0.0f, 0.0f);
+            }
+            if (lane == 0) wc[wave][d] = run + (uint32_t)__popcll(b);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t first_owned(uint32_t a, int world, int rank) {
+    uint32_t w = (uint32_t)world;
+    return a + ((uint32_t)rank + w - a % w) % w;
+}
+
+__global__ __launch_bounds__(256) void recv_count_kernel(const float4* __restrict__ recv, uint32_t m, int world,
+                                                         int rank, uint32_t* __restrict__ ntiles,
+                                                         uint32_t* __restrict__ dkey) {
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= m) return;
+    const float4* r = recv + (size_t)kXRecFloat4 * i;
+    float4 c = r[2];
+    float4 x = r[3];
+    uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+    uint32_t ty0 = (lo >> 16) >> 4, ty1 = (hi >> 16) >> 4;
+    uint32_t tx0 = (lo & 0xFFFFu) >> 4, tx1 = (hi & 0xFFFFu) >> 4;
+    uint32_t f = first_owned(ty0, world, rank);
+    uint32_t rows = f > ty1 ? 0u : (ty1 - f) / (uint32_t)world + 1u;
+    ntiles[i] = rows * (tx1 - tx0 + 1);
+    dkey[i] = __float_as_uint(x.x);
+}
+
+__global__ __launch_bounds__(256) void recv_duplicate_kernel(const float4* __restrict__ recv,
+                                                             const uint32_t* __restrict__ dkey,
+                                                             const uint32_t* __restrict__ ntiles,
+                                                             const uint32_t* __restrict__ offsets, uint32_t m,
+                                                             uint32_t tiles_x, int world, int rank,
+                                                             uint32_t* __restrict__ keys,
+                                                             uint32_t* __restrict__ vals) {
+    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= m || ntiles[i] == 0) return;
+    float4 c = recv[(size_t)kXRecFloat4 * i + 2];
+    uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+    uint32_t ty0 = (lo >> 16) >> 4, ty1 = (hi >> 16) >> 4;
+    uint32_t tx0 = (lo & 0xFFFFu) >> 4, tx1 = (hi & 0xFFFFu) >> 4;
+    uint32_t off = offsets[i], dk = dkey[i];
+    for (uint32_t ty = first_owned(ty0, world, rank); ty <= ty1; ty += (uint32_t)world) {
+        for (uint32_t tx = tx0; tx <= tx1; ++tx) {
+            keys[off] = ((ty * tiles_x + tx) << kDepthBits) | dk;
+            vals[off] = i;
+            ++off;
+        }
+    }
+}
+
+hipError_t launch_shard_count(const float4* rec, const uint32_t* ntiles, uint32_t n, int world,
+                              uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st) {
+    if (world < 1 || world > kMaxWorld) return hipErrorInvalidValue;
+    if (nblocks == 0) return hipSuccess;
+    shard_count_kernel<<<nblocks, 256, 0, st>>>(rec, ntiles, n, world, dest_mask, counts, nblocks);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* row_total, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    rows_scan_kernel<<<rows, 256, 0, st>>>(counts, nblocks, row_total);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
+                             int world, uint32_t index_base, const uint32_t* counts, const uint32_t* dest_total,
+                             uint32_t nblocks, float4* send, hipStream_t st) {
+    if (nblocks == 0) return hipSuccess;
+    shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, dkey, dest_mask, n, world, index_base, counts, dest_total,
+                                               nblocks, send);
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_count(const float4* recv, uint32_t m, int world, int rank, uint32_t* ntiles,
+                             uint32_t* dkey, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    recv_count_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, world, rank, ntiles, dkey);
+    return hipGetLastError();
+}
+
+hipError_t launch_recv_duplicate(const float4* recv, const uint32_t* dkey, const uint32_t* ntiles,
+                                 const uint32_t* offsets, uint32_t m, uint32_t tiles_x, int world, int rank,
+                                 uint32_t* keys, uint32_t* vals, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    recv_duplicate_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, dkey, ntiles, offsets, m, tiles_x, world, rank,
+                                                           keys, vals);
+    return hipGetLastError();
+}
+
+}  // namespace gs

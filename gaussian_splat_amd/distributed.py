@@ -1,0 +1,171 @@
+"""Multi-GPU rendering: splat-index shards, tile-row ownership, RCCL exchange.
+
+DESIGN.md §6.  One process per GPU.  Rank r holds a contiguous splat-index
+range of the scene and owns the 16x16 tile rows ty with ty % world == r.
+Per frame:
+
+  1. gs_shard_project   project the local shard on the GPU and pack a 64-B
+                        exchange record for every (visible splat, owning
+                        rank) pair, grouped by destination, index order inside
+  2. all_to_all         exchange counts, then records (RCCL over xGMI)
+  3. gs_shard_render    bin/sort/composite the received records into the
+                        owned tile rows (a compact band buffer)
+  4. gather             bands -> rank 0, interleaved back into the frame
+
+Records arrive in source-rank order = global splat-index order, so each
+owned tile sees exactly the single-GPU list order: the assembled frame is
+bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
+tests/test_distributed.py).  The backend object does the per-rank compute:
+`HipShardBackend` (libgsplat.so) in production; the gloo tests plug in a
+CPU backend from tests/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+from .api import InstancedSplatRenderer, Options, Scene, _mat16
+from ._lib import check, lib
+
+TILE = 16
+
+
+def tiles(width: int, height: int) -> tuple[int, int]:
+    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+
+
+def band_rows(height: int, world: int) -> int:
+    """Pixel rows of the (padded, equal-size) band buffer of every rank."""
+    ty = (height + TILE - 1) // TILE
+    return ((ty + world - 1) // world) * TILE
+
+
+def assemble(bands, width: int, height: int, world: int):
+    """Interleave rank bands (tile row ty <- band[ty % world], row ty // world) into a frame."""
+    import torch
+
+    th = (height + TILE - 1) // TILE
+    frame = torch.zeros((th * TILE, width, 4), dtype=torch.float32, device=bands[0].device)
+    ft = frame.view(th, TILE, width, 4)
+    for r, b in enumerate(bands):
+        k = len(range(r, th, world))
+        if k:
+            ft[r::world] = b.view(-1, TILE, width, 4)[:k]
+    return frame[:height]
+
+
+class HipShardBackend:
+    """Per-rank compute through libgsplat.so (device buffers are torch tensors)."""
+
+    def __init__(self, shard: Scene, rank: int, world: int, index_base: int, options: Options, device: int):
+        import torch
+
+        self.r = InstancedSplatRenderer(shard, options)
+        self.r.initialize(device)
+        check(lib().gs_shard_configure(self.r._h, rank, world, index_base), "gs_shard_configure")
+        self.world, self.rank, self.device = world, rank, torch.device(f"cuda:{device}")
+        self.xbytes = int(lib().gs_exchange_record_bytes())
+        self.send = torch.empty(max(1, shard.n * world * self.xbytes), dtype=torch.uint8, device=self.device)
+
+    def project(self, view, proj, width, height):
+        import torch
+
+        counts = (C.c_int64 * self.world)()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_shard_project(self.r._h, _mat16(view), _mat16(proj), width, height,
+                                     C.c_void_p(self.send.data_ptr()), self.send.numel(), counts,
+                                     C.c_void_p(stream)), "gs_shard_project")
+        return self.send, [int(c) for c in counts]
+
+    def empty(self, nbytes):
+        import torch
+
+        return torch.empty(max(1, nbytes), dtype=torch.uint8, device=self.device)
+
+    def render(self, recv, nrec, width, height):
+        import torch
+
+        band = torch.empty((band_rows(height, self.world), width, 4), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_shard_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
+                                    C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_shard_render")
+        return band
+
+
+def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous index range of rank `rank` (balanced)."""
+    b = n * rank // world
+    e = n * (rank + 1) // world
+    return b, e
+
+
+def exchange(send, counts, xbytes, world, group=None):
+    """all_to_all of counts then of records (bytes); returns (recv, nrec)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = send.device
+    sc = torch.tensor(counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = [int(x) for x in rc.cpu().tolist()]
+    total = sum(rcounts)
+    recv = torch.empty(max(1, total * xbytes), dtype=torch.uint8, device=dev)
+    ssz = sum(counts) * xbytes
+    dist.all_to_all_single(recv[: total * xbytes], send[:ssz], [c * xbytes for c in rcounts],
+                           [c * xbytes for c in counts], group=group)
+    return recv, total
+
+
+class ShardedRenderer:
+    """One rank of a multi-GPU frame (torch.distributed must be initialised)."""
+
+    def __init__(self, backend, rank: int, world: int, group=None):
+        self.b, self.rank, self.world, self.group = backend, rank, world, group
+
+    def render(self, view, proj, width, height, gather: bool = True):
+        """Returns the full frame on rank 0 (None elsewhere) when gather=True,
+        else this rank's band buffer."""
+        import torch.distributed as dist
+
+        send, counts = self.b.project(view, proj, width, height)
+        recv, nrec = exchange(send, counts, self.b.xbytes, self.world, self.group)
+        band = self.b.render(recv, nrec, width, height)
+        if not gather:
+            return band
+        if self.world == 1:
+            return assemble([band], width, height, 1)
+        bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(band, bands, dst=0, group=self.group)
+        return assemble(bands, width, height, self.world) if self.rank == 0 else None
+
+
+def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,
+                          mode: str = "tile", device: int = 0) -> np.ndarray:
+    """All `world` ranks in one process on one GPU, exchange by slicing —
+    the same kernels and record protocol as the multi-process path."""
+    import torch
+
+    opts = Options(mode=mode, sh_degree=sh_degree, crop=False)
+    backends = []
+    for r in range(world):
+        b, e = shard_bounds(scene.n, world, r)
+        backends.append(HipShardBackend(scene.subset(slice(b, e)), r, world, b, opts, device))
+    sends = [be.project(view, proj, width, height) for be in backends]
+    xb = backends[0].xbytes
+    bands = []
+    for dst in range(world):
+        parts = []
+        for src in range(world):
+            buf, counts = sends[src]
+            off = sum(counts[:dst]) * xb
+            parts.append(buf[off: off + counts[dst] * xb])
+        recv = torch.cat(parts) if parts else backends[dst].empty(0)
+        nrec = recv.numel() // xb
+        bands.append(backends[dst].render(recv if recv.numel() else backends[dst].empty(xb), nrec, width, height))
+    frame = assemble(bands, width, height, world)
+    torch.cuda.synchronize()
+    return frame.cpu().numpy()

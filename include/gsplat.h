@@ -1,0 +1,164 @@
+/*
+ * gsplat.h — C-ABI of libgsplat.so, the MI355X-native Gaussian-splat tile
+ * rasterizer.  Plain pointers and sizes only; no C++ or torch types cross it.
+ *
+ * It replaces the reference's splat renderer host class and its Metal passes
+ * (nshelton/gaussian_splat):
+ *
+ *   reference                                             here
+ *   ----------------------------------------------------- -----------------------------
+ *   InstancedSplatRenderer(std::string)                   gs_create()
+ *     src/instanced_splat_renderer.h:15, .mm:339-393       (PLY load + crop + upload prep)
+ *   bool initialize(void* device)                         gs_initialize()
+ *     src/instanced_splat_renderer.h:18, .mm:399-422
+ *   void render(cmdBuf, drawable, view, proj, w, h)       gs_render()
+ *     src/instanced_splat_renderer.h:21-26, .mm:424-578    (offscreen fp32 RGBA in HBM)
+ *   int getPointCount() const                             gs_point_count()
+ *     src/instanced_splat_renderer.h:28
+ *   PLYLoader::load(path, vector<PointData>&)             gs_ply_load() / gs_ply_free()
+ *     src/ply_loader.h:33, src/ply_loader.cpp:22-205
+ *   (Metal GPU time, src/metal_renderer.mm:123-126)       gs_last_stats()
+ *   (stderr + bool returns)                               gs_status + gs_last_error()
+ *
+ * Matrices are column-major float[16] exactly like simd_float4x4 (m[col*4+row]).
+ * All GPU work of one call is enqueued on the caller's HIP stream; gs_render is
+ * asynchronous when `out_rgba` is device memory.
+ */
+#ifndef GSPLAT_H
+#define GSPLAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSPLAT_ABI_VERSION 1
+
+typedef enum {
+    GS_OK = 0,
+    GS_ERR_INVALID_ARG = 1,
+    GS_ERR_IO = 2,
+    GS_ERR_PARSE = 3,
+    GS_ERR_DEVICE = 4,
+    GS_ERR_OOM = 5,
+    GS_ERR_COMM = 6,
+    GS_ERR_UNSUPPORTED = 7,
+    GS_ERR_STATE = 8
+} gs_status;
+
+/* Composite rule.  TILE = gaussian_splat_tile.metal:251-266 (contract
+ * default); LIVE50 = gaussian_splat_50layer.metal:208-222. */
+typedef enum { GS_MODE_TILE = 0, GS_MODE_LIVE50 = 1 } gs_mode;
+
+typedef struct gs_options {
+    int32_t mode;          /* gs_mode */
+    int32_t sh_degree;     /* 0..3; 0 = loader-converted DC colour (reference behaviour) */
+    int32_t crop;          /* 1 = keep |x|,|y|,|z| < crop_radius (instanced_splat_renderer.mm:382-386) */
+    float crop_radius;     /* 5.0 in the reference */
+    int32_t stage_timing;  /* 1 = record HIP events around every kernel (gs_last_stats) */
+    int32_t reserved[7];
+} gs_options;
+
+/* Scene as SoA host arrays (all float32, n splats).  Used by
+ * gs_create_from_soa; gs_create fills the same fields from a .ply. */
+typedef struct gs_scene_soa {
+    int64_t n;
+    const float *pos;      /* n*3 x,y,z */
+    const float *rot;      /* n*4 w,x,y,z (raw; normalised on device, tile.metal:41) */
+    const float *scale;    /* n*3 activated: exp(scale_i) (ply_loader.cpp:117-119) */
+    const float *opacity;  /* n activated: sigmoid (ply_loader.cpp:116) */
+    const float *color;    /* n*3: rgb (sh_degree 0) or raw f_dc (sh_degree > 0) */
+    const float *sh_rest;  /* n*45 f_rest in PLY (channel-major) order, or NULL */
+} gs_scene_soa;
+
+/* Per-frame statistics of the last gs_render on a handle. */
+typedef struct gs_stats {
+    int64_t splats;        /* N on the device (post-crop) */
+    int64_t visible;       /* splats that touch >= 1 tile */
+    int64_t pairs;         /* P = (splat, tile) pairs */
+    int64_t tiles;         /* T */
+    int32_t width, height;
+    int32_t sort_bits;     /* significant key bits sorted */
+    int32_t sort_passes;
+    /* stage times in ms (valid when options.stage_timing = 1) */
+    float ms_preprocess, ms_scan, ms_duplicate, ms_sort, ms_ranges, ms_composite, ms_total;
+    int64_t bytes_preprocess, bytes_scan, bytes_duplicate, bytes_sort, bytes_ranges, bytes_composite;
+} gs_stats;
+
+typedef struct gs_handle gs_handle;
+
+/* ---- library ---------------------------------------------------------- */
+int32_t gs_abi_version(void);
+const char *gs_last_error(void);          /* thread-local; valid until next call on this thread */
+void gs_default_options(gs_options *opt); /* tile mode, sh 0, crop on (r = 5) */
+
+/* ---- scene / handle (InstancedSplatRenderer) -------------------------- */
+gs_status gs_create(const char *ply_path, const gs_options *opt, gs_handle **out);
+gs_status gs_create_from_soa(const gs_scene_soa *scene, const gs_options *opt, gs_handle **out);
+/* PointData array (62 floats per point, src/ply_loader.h:7-28), sh_degree 0. */
+gs_status gs_create_from_points(const float *points, int64_t n, const gs_options *opt, gs_handle **out);
+gs_status gs_initialize(gs_handle *h, int32_t device_ordinal); /* uploads the scene to HBM */
+int64_t gs_point_count(const gs_handle *h);
+void gs_destroy(gs_handle *h);
+gs_status gs_set_mode(gs_handle *h, int32_t mode);
+
+/* ---- frame (InstancedSplatRenderer::render) --------------------------- */
+/* out_rgba: width*height*4 float32, row-major, y down.  out_is_device = 1:
+ * HBM pointer, async on `hip_stream`; 0: host pointer, the call syncs. */
+gs_status gs_render(gs_handle *h, const float view[16], const float proj[16], int32_t width,
+                    int32_t height, float *out_rgba, int32_t out_is_device, void *hip_stream);
+gs_status gs_last_stats(const gs_handle *h, gs_stats *out);
+
+/* ---- stage-level entry points (tests, multi-GPU orchestration) --------- */
+/* Project all splats; copies the 48-byte records (gs_record layout below),
+ * depth keys and tile counts to HOST arrays of length gs_point_count(). */
+gs_status gs_project_host(gs_handle *h, const float view[16], const float proj[16], int32_t width,
+                          int32_t height, void *records, uint32_t *dkeys, uint32_t *ntiles);
+/* Sorted (key, value) pairs of the last frame copied to host; returns count. */
+gs_status gs_sorted_pairs_host(gs_handle *h, uint32_t *keys, uint32_t *vals, int64_t cap, int64_t *count);
+/* Stand-alone LSD radix sort of device arrays (stable, key bits [0, bits)).
+ * tmp_keys/tmp_vals: n elements each; result ends in keys/vals. */
+gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals,
+                              int64_t n, int32_t bits, void *hip_stream);
+
+/* ---- multi-GPU: tile-band ownership across ranks --- */
+/* Shard = contiguous splat-index range [index_base, index_base + n) of the
+ * global scene.  Tiles are owned by rank r iff (tile_row % world) == r. */
+gs_status gs_shard_configure(gs_handle *h, int32_t rank, int32_t world, int64_t index_base);
+/* Project the local shard and pack per-destination records into `send`
+ * (device memory, capacity `send_cap_bytes`).  Writes world send counts
+ * (in records) to host `send_counts`.  Record size: gs_exchange_record_bytes(). */
+gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[16], int32_t width,
+                           int32_t height, void *send, int64_t send_cap_bytes, int64_t *send_counts,
+                           void *hip_stream);
+/* Bin, sort and composite the received records (concatenated in source-rank
+ * order) into the owned tiles of out_rgba (device, width*height*4; tiles not
+ * owned are left untouched). */
+gs_status gs_shard_render(gs_handle *h, const void *recv, int64_t recv_count, int32_t width, int32_t height,
+                          float *out_rgba, void *hip_stream);
+int32_t gs_exchange_record_bytes(void);
+
+/* ---- PLY loader (PLYLoader::load drop-in) ----------------------------- */
+/* Loads into a malloc'd PointData array (62 floats/point).  compat = 1
+ * reproduces every reference quirk (ASCII 2N points). */
+gs_status gs_ply_load(const char *path, int32_t compat, float **points, int64_t *n);
+void gs_ply_free(float *points);
+
+/* ---- camera math (TrackballCamera::makeLookAt / makePerspective) ------ */
+void gs_look_at(const float eye[3], const float center[3], const float up[3], float out[16]);
+void gs_perspective(float fov_degrees, float aspect, float znear, float zfar, float out[16]);
+
+/* 48-byte per-splat record (preprocess output, composite input). */
+typedef struct gs_record {
+    float cx, cy, ax, ay;
+    float bx, by, opacity, r;
+    float g, b;
+    uint32_t rect_lo, rect_hi;
+} gs_record;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSPLAT_H */

@@ -1,0 +1,185 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) and of oracle/_ref.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+REF_LIB = HERE / "_ref" / "libref_ply.so"
+POINT_FLOATS = 62
+
+RECORD_DTYPE = np.dtype([("cx", "<f4"), ("cy", "<f4"), ("ax", "<f4"), ("ay", "<f4"), ("bx", "<f4"),
+                         ("by", "<f4"), ("opacity", "<f4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4"),
+                         ("rect_lo", "<u4"), ("rect_hi", "<u4")])
+
+
+class OraScene(C.Structure):
+    _fields_ = [("n", C.c_int64), ("pos", C.c_void_p), ("rot", C.c_void_p), ("scale", C.c_void_p),
+                ("opacity", C.c_void_p), ("color", C.c_void_p), ("sh_rest", C.c_void_p), ("sh_degree", C.c_int)]
+
+
+class OraOptions(C.Structure):
+    _fields_ = [("mode", C.c_int), ("cap", C.c_int), ("nthreads", C.c_int)]
+
+
+class OraStats(C.Structure):
+    _fields_ = [("visible", C.c_int64), ("pairs", C.c_int64), ("tiles", C.c_int64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            subprocess.run(["make", "-s", "-C", str(HERE), "liboracle.so"], check=True)
+        L = C.CDLL(str(LIB))
+        L.ora_ply_load.argtypes = [C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_int64)]
+        L.ora_ply_load.restype = C.c_int
+        L.ora_free.argtypes = [C.c_void_p]
+        L.ora_crop.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_void_p]
+        L.ora_crop.restype = C.c_int64
+        L.ora_look_at.argtypes = [C.c_void_p] * 4
+        L.ora_perspective.argtypes = [C.c_float] * 4 + [C.c_void_p]
+        L.ora_mat4_mul.argtypes = [C.c_void_p] * 3
+        L.ora_camera_position.argtypes = [C.c_void_p] * 2
+        L.ora_project_all.argtypes = [C.POINTER(OraScene), C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_int]
+        L.ora_render.argtypes = [C.POINTER(OraScene), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                 C.POINTER(OraOptions), C.c_void_p, C.POINTER(OraStats)]
+        L.ora_render.restype = C.c_int
+        L.ora_composite_list.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.ora_f32_to_f16_bits.argtypes = [C.c_float]
+        L.ora_f32_to_f16_bits.restype = C.c_uint16
+        L.ora_expf.argtypes = [C.c_float]
+        L.ora_expf.restype = C.c_float
+        _lib = L
+    return _lib
+
+
+def _col16(m) -> np.ndarray:
+    a = np.asarray(m, np.float32)
+    if a.shape == (4, 4):
+        a = a.T
+    return np.ascontiguousarray(a.reshape(16), np.float32)
+
+
+def _scene(scene, sh_degree: int):
+    keep = [np.ascontiguousarray(getattr(scene, f), np.float32) if getattr(scene, f) is not None else None
+            for f in ("pos", "rot", "scale", "opacity", "color", "sh_rest")]
+    s = OraScene()
+    s.n = keep[0].shape[0]
+    s.pos, s.rot, s.scale, s.opacity, s.color = (k.ctypes.data for k in keep[:5])
+    s.sh_rest = keep[5].ctypes.data if keep[5] is not None else None
+    s.sh_degree = int(sh_degree)
+    return s, keep
+
+
+def ply_load(path) -> tuple[bool, np.ndarray]:
+    ptr = C.POINTER(C.c_float)()
+    n = C.c_int64(0)
+    ok = lib().ora_ply_load(str(path).encode(), C.byref(ptr), C.byref(n))
+    pts = np.zeros((0, POINT_FLOATS), np.float32)
+    if n.value > 0:
+        pts = np.ctypeslib.as_array(ptr, shape=(n.value * POINT_FLOATS,)).reshape(-1, POINT_FLOATS).copy()
+    if ptr:
+        lib().ora_free(ptr)
+    return bool(ok), pts
+
+
+def crop(points: np.ndarray, radius: float = 5.0) -> np.ndarray:
+    p = np.ascontiguousarray(points, np.float32)
+    keep = np.zeros(p.shape[0], np.int64)
+    k = lib().ora_crop(p.ctypes.data, p.shape[0], float(radius), keep.ctypes.data)
+    return keep[:k]
+
+
+def look_at(eye, center, up) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    a = [np.asarray(v, np.float32) for v in (eye, center, up)]
+    lib().ora_look_at(a[0].ctypes.data, a[1].ctypes.data, a[2].ctypes.data, out.ctypes.data)
+    return out.reshape(4, 4).T.copy()
+
+
+def perspective(fov_deg, aspect, zn, zf) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    lib().ora_perspective(float(fov_deg), float(aspect), float(zn), float(zf), out.ctypes.data)
+    return out.reshape(4, 4).T.copy()
+
+
+def mat4_mul(a, b) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    A, B = _col16(a), _col16(b)
+    lib().ora_mat4_mul(A.ctypes.data, B.ctypes.data, out.ctypes.data)
+    return out.reshape(4, 4).T.copy()
+
+
+def project(scene, view, proj, width, height, sh_degree=0, nthreads=0):
+    s, keep = _scene(scene, sh_degree)
+    n = s.n
+    rec = np.zeros(n, RECORD_DTYPE)
+    dk = np.zeros(n, np.uint32)
+    nt = np.zeros(n, np.uint32)
+    V, P = _col16(view), _col16(proj)
+    lib().ora_project_all(C.byref(s), V.ctypes.data, P.ctypes.data, int(width), int(height), rec.ctypes.data,
+                          dk.ctypes.data, nt.ctypes.data, int(nthreads))
+    return rec, dk, nt
+
+
+def render(scene, view, proj, width, height, sh_degree=0, mode="tile", cap=0, nthreads=0):
+    s, keep = _scene(scene, sh_degree)
+    out = np.zeros((height, width, 4), np.float32)
+    o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
+    st = OraStats()
+    V, P = _col16(view), _col16(proj)
+    lib().ora_render(C.byref(s), V.ctypes.data, P.ctypes.data, int(width), int(height), C.byref(o),
+                     out.ctypes.data, C.byref(st))
+    return out, {"visible": st.visible, "pairs": st.pairs, "tiles": st.tiles}
+
+
+def composite_list(frags, mode="tile", cap=0) -> np.ndarray:
+    f = np.ascontiguousarray(frags, np.float32).reshape(-1, 5)
+    out = np.zeros(4, np.float32)
+    lib().ora_composite_list(f.ctypes.data, f.shape[0], 0 if mode == "tile" else 1, int(cap), out.ctypes.data)
+    return out
+
+
+def f16_bits(x: float) -> int:
+    return int(lib().ora_f32_to_f16_bits(float(x)))
+
+
+def expf(x: float) -> float:
+    return float(lib().ora_expf(float(x)))
+
+
+# ---- oracle/_ref: the reference's own loader, compiled from /root/reference ----
+_ref = None
+
+
+def ref_available() -> bool:
+    return REF_LIB.exists()
+
+
+def ref_ply_load(path) -> tuple[bool, np.ndarray]:
+    global _ref
+    if _ref is None:
+        _ref = C.CDLL(str(REF_LIB))
+        _ref.ref_ply_load.argtypes = [C.c_char_p, C.c_void_p, C.c_longlong]
+        _ref.ref_ply_load.restype = C.c_longlong
+    n = _ref.ref_ply_load(str(path).encode(), None, 0)
+    ok = n >= 0
+    cnt = n if ok else -1 - n
+    out = np.zeros((max(cnt, 0), POINT_FLOATS), np.float32)
+    if cnt > 0:
+        _ref.ref_ply_load(str(path).encode(), out.ctypes.data, cnt)
+    return ok, out
