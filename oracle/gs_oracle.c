@@ -644,37 +644,39 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
     free(ord);
 }
 
-int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, int H,
-               const ora_options *opt, float *out, ora_stats *st) {
+int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
+                          const ora_options *opt, int row_mod, int row_rem, int compact, float *out,
+                          ora_stats *st) {
     int mode = opt ? opt->mode : ORA_MODE_TILE;
     int cap = opt ? opt->cap : 0;
     int nth = opt ? opt->nthreads : 0;
 #ifdef _OPENMP
     if (nth > 0) omp_set_num_threads(nth);
 #endif
-    int64_t n = s->n;
-    ora_record *rec = (ora_record *)malloc(sizeof(ora_record) * (size_t)(n > 0 ? n : 1));
-    uint32_t *dkey = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
-    uint32_t *nt = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
-    ora_project_all(s, V, P, W, H, rec, dkey, nt, nth);
-
+    if (row_mod < 1) row_mod = 1;
     int TW = (W + TILE - 1) / TILE, TH = (H + TILE - 1) / TILE, T = TW * TH;
     /* Oracle binning uses the record rect widened by 2 px, so a too-tight
-     * product rect shows up as a framebuffer mismatch. */
+     * product rect shows up as a framebuffer mismatch.  Records with a zero
+     * rect (rect_hi == 0 && rect_lo == 0 && opacity == 0) are culled. */
     int64_t *cnt = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
     int64_t visible = 0, pairs = 0;
+#define ORA_RECT(i, X0, Y0, X1, Y1)                                                            \
+    int X0 = (int)(rec[i].rect_lo & 0xFFFF) - 2, Y0 = (int)(rec[i].rect_lo >> 16) - 2;          \
+    int X1 = (int)(rec[i].rect_hi & 0xFFFF) + 2, Y1 = (int)(rec[i].rect_hi >> 16) + 2;          \
+    if (X0 < 0) X0 = 0;                                                                        \
+    if (Y0 < 0) Y0 = 0;                                                                        \
+    if (X1 > W - 1) X1 = W - 1;                                                                \
+    if (Y1 > H - 1) Y1 = H - 1;
     for (int64_t i = 0; i < n; ++i) {
-        if (!nt[i]) continue;
+        if (!dkey[i] && !rec[i].rect_hi && !rec[i].opacity) continue;
         visible++;
-        pairs += nt[i];
-        int x0 = (int)(rec[i].rect_lo & 0xFFFF) - 2, y0 = (int)(rec[i].rect_lo >> 16) - 2;
-        int x1 = (int)(rec[i].rect_hi & 0xFFFF) + 2, y1 = (int)(rec[i].rect_hi >> 16) + 2;
-        if (x0 < 0) x0 = 0;
-        if (y0 < 0) y0 = 0;
-        if (x1 > W - 1) x1 = W - 1;
-        if (y1 > H - 1) y1 = H - 1;
-        for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty)
+        pairs += (int64_t)((rec[i].rect_hi & 0xFFFF) / TILE - (rec[i].rect_lo & 0xFFFF) / TILE + 1) *
+                 ((rec[i].rect_hi >> 16) / TILE - (rec[i].rect_lo >> 16) / TILE + 1);
+        ORA_RECT(i, x0, y0, x1, y1)
+        for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
+            if (ty % row_mod != row_rem) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) cnt[ty * TW + tx + 1]++;
+        }
     }
     for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
     int64_t total = cnt[T];
@@ -682,16 +684,14 @@ int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, 
     int64_t *cur = (int64_t *)malloc(sizeof(int64_t) * (size_t)T);
     memcpy(cur, cnt, sizeof(int64_t) * (size_t)T);
     for (int64_t i = 0; i < n; ++i) { /* index order = arrival order */
-        if (!nt[i]) continue;
-        int x0 = (int)(rec[i].rect_lo & 0xFFFF) - 2, y0 = (int)(rec[i].rect_lo >> 16) - 2;
-        int x1 = (int)(rec[i].rect_hi & 0xFFFF) + 2, y1 = (int)(rec[i].rect_hi >> 16) + 2;
-        if (x0 < 0) x0 = 0;
-        if (y0 < 0) y0 = 0;
-        if (x1 > W - 1) x1 = W - 1;
-        if (y1 > H - 1) y1 = H - 1;
-        for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty)
+        if (!dkey[i] && !rec[i].rect_hi && !rec[i].opacity) continue;
+        ORA_RECT(i, x0, y0, x1, y1)
+        for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
+            if (ty % row_mod != row_rem) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) list[cur[ty * TW + tx]++] = (uint32_t)i;
+        }
     }
+#undef ORA_RECT
     free(cur);
 
 #ifdef _OPENMP
@@ -706,6 +706,8 @@ int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, 
 #pragma omp for schedule(dynamic, 4)
 #endif
         for (int t = 0; t < T; ++t) {
+            int tx = t % TW, ty = t / TW;
+            if (ty % row_mod != row_rem) continue;
             int64_t b = cnt[t], e = cnt[t + 1], m = e - b;
             if ((size_t)m > kcap) {
                 kcap = (size_t)m;
@@ -720,10 +722,10 @@ int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, 
             /* S1 order: descending half depth == ascending dkey; ties keep
              * arrival (index) order. */
             if (cap == 0) qsort(ord, (size_t)m, sizeof(kv), kv_cmp);
-            int tx = t % TW, ty = t / TW;
             for (int py = ty * TILE; py < ty * TILE + TILE && py < H; ++py) {
+                int orow = compact ? (ty / row_mod) * TILE + (py - ty * TILE) : py;
                 for (int px = tx * TILE; px < tx * TILE + TILE && px < W; ++px) {
-                    float *o = out + ((size_t)py * W + px) * 4;
+                    float *o = out + ((size_t)orow * W + px) * 4;
                     int c = 0;
                     if (cap == 0) {
                         if (mode == ORA_MODE_TILE) { /* fused early-break walk */
@@ -783,8 +785,19 @@ int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, 
     }
     free(list);
     free(cnt);
+    return 1;
+}
+
+int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, int H,
+               const ora_options *opt, float *out, ora_stats *st) {
+    int64_t n = s->n;
+    ora_record *rec = (ora_record *)malloc(sizeof(ora_record) * (size_t)(n > 0 ? n : 1));
+    uint32_t *dkey = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+    uint32_t *nt = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+    ora_project_all(s, V, P, W, H, rec, dkey, nt, opt ? opt->nthreads : 0);
+    int ok = ora_composite_records(rec, dkey, n, W, H, opt, 1, 0, 0, out, st);
     free(rec);
     free(dkey);
     free(nt);
-    return 1;
+    return ok;
 }

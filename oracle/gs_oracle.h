@@ -124,6 +124,14 @@ void ora_project_all(const ora_scene *s, const float view[16], const float proj[
 int ora_render(const ora_scene *s, const float view[16], const float proj[16], int width,
                int height, const ora_options *opt, float *out_rgba, ora_stats *stats);
 
+/* Bin, sort (S1) and composite an explicit record list (index = arrival
+ * order) into the tile rows ty with ty % row_mod == row_rem; compact = 1
+ * writes those rows stacked (the multi-GPU band layout).  Culled records are
+ * all-zero (dkey 0, rect_hi 0, opacity 0). */
+int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int width, int height,
+                          const ora_options *opt, int row_mod, int row_rem, int compact, float *out,
+                          ora_stats *stats);
+
 /* Composite a single synthetic fragment list (depth, rgb, alpha) with the S1
  * sort and A1 / A1' rule — the unit the reference's tile_sort_composite and
  * compute_sort_composite operate on.  frags: n*5 floats (depth, r, g, b, a),

@@ -58,6 +58,10 @@ def lib() -> C.CDLL:
         L.ora_render.argtypes = [C.POINTER(OraScene), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                  C.POINTER(OraOptions), C.c_void_p, C.POINTER(OraStats)]
         L.ora_render.restype = C.c_int
+        L.ora_composite_records.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int,
+                                            C.POINTER(OraOptions), C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.POINTER(OraStats)]
+        L.ora_composite_records.restype = C.c_int
         L.ora_composite_list.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.ora_f32_to_f16_bits.argtypes = [C.c_float]
         L.ora_f32_to_f16_bits.restype = C.c_uint16
@@ -145,6 +149,22 @@ def render(scene, view, proj, width, height, sh_degree=0, mode="tile", cap=0, nt
     lib().ora_render(C.byref(s), V.ctypes.data, P.ctypes.data, int(width), int(height), C.byref(o),
                      out.ctypes.data, C.byref(st))
     return out, {"visible": st.visible, "pairs": st.pairs, "tiles": st.tiles}
+
+
+def composite_records(rec, dkey, width, height, row_mod=1, row_rem=0, compact=False, mode="tile", cap=0,
+                      nthreads=0):
+    """Bin/sort/composite an explicit record list (index = arrival order)."""
+    rec = np.ascontiguousarray(rec, RECORD_DTYPE)
+    dkey = np.ascontiguousarray(dkey, np.uint32)
+    th = (height + 15) // 16
+    rows = ((th + row_mod - 1) // row_mod) * 16 if compact else height
+    out = np.zeros((rows, width, 4), np.float32)
+    o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
+    st = OraStats()
+    lib().ora_composite_records(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
+                                C.byref(o), int(row_mod), int(row_rem), int(bool(compact)), out.ctypes.data,
+                                C.byref(st))
+    return out
 
 
 def composite_list(frags, mode="tile", cap=0) -> np.ndarray:

@@ -1,0 +1,56 @@
+"""CPU stand-in for HipShardBackend (test infrastructure).
+
+Per-rank compute by the oracle; the 64-B exchange record format, the
+destination rule (tile row % world) and the band layout are the product's,
+so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer exercise the
+real exchange / gather / assembly protocol on CPU.
+"""
+import numpy as np
+
+from oracle import oracle_py as O
+
+XREC = np.dtype(O.RECORD_DTYPE.descr + [("dkey", "<u4"), ("gidx", "<u4"), ("pad0", "<u4"), ("pad1", "<u4")])
+assert XREC.itemsize == 64
+
+
+class OracleShardBackend:
+    xbytes = 64
+
+    def __init__(self, shard, rank, world, index_base, sh_degree=0, mode="tile"):
+        self.shard, self.rank, self.world, self.base = shard, rank, world, index_base
+        self.sh, self.mode = sh_degree, mode
+
+    def project(self, view, proj, width, height):
+        import torch
+
+        rec, dk, nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
+        vis = nt > 0
+        ty0 = (rec["rect_lo"] >> 16) >> 4
+        ty1 = (rec["rect_hi"] >> 16) >> 4
+        w = self.world
+        parts, counts = [], []
+        for d in range(w):
+            first = ty0 + (d + w - ty0 % w) % w
+            idx = np.nonzero(vis & (first <= ty1))[0]
+            x = np.zeros(len(idx), XREC)
+            for f in O.RECORD_DTYPE.names:
+                x[f] = rec[f][idx]
+            x["dkey"] = dk[idx]
+            x["gidx"] = idx + self.base
+            parts.append(x)
+            counts.append(len(idx))
+        buf = np.concatenate(parts).view(np.uint8) if parts else np.zeros(0, np.uint8)
+        return torch.from_numpy(np.ascontiguousarray(buf).copy() if buf.size else np.zeros(1, np.uint8)), counts
+
+    def render(self, recv, nrec, width, height):
+        import torch
+
+        raw = recv.numpy()[: nrec * 64].copy().view(XREC)
+        rec = np.zeros(nrec, O.RECORD_DTYPE)
+        for f in O.RECORD_DTYPE.names:
+            rec[f] = raw[f]
+        # received order must be global index order (tie rule); check it
+        assert np.all(np.diff(raw["gidx"].astype(np.int64)) > 0)
+        band = O.composite_records(rec, raw["dkey"], width, height, row_mod=self.world, row_rem=self.rank,
+                                   compact=True, mode=self.mode)
+        return torch.from_numpy(band)

@@ -1,0 +1,128 @@
+"""Pin the oracle (CPU) against the golden vectors before trusting it.
+
+- PLY I1: every fixture in tests/golden/ply is compared with the output the
+  reference's OWN src/ply_loader.cpp produced for it (tools/make_golden.py via
+  oracle/_ref), bit for bit; plus a live cross-check against oracle/_ref when
+  that library is present.
+- C1 / K1-K6 / S1 / A1: hand-derived known answers (tests/golden/known_answers.json),
+  computed in float64 from the cited reference lines.  The Metal shaders
+  cannot be built here, so these are the pins ("parity unpinned" by
+  execution).
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import oracle_py as O
+
+GOLD = Path(__file__).resolve().parent / "golden"
+KA = json.loads((GOLD / "known_answers.json").read_text())
+MANIFEST = json.loads((GOLD / "ply" / "manifest.json").read_text())
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_oracle_ply_matches_reference_fixture(name):
+    ok, pts = O.ply_load(GOLD / "ply" / f"{name}.ply")
+    ref = np.load(GOLD / "ply" / f"{name}.ref.npy", allow_pickle=False)
+    assert ok == MANIFEST[name]["ok"]
+    assert pts.shape[0] == MANIFEST[name]["n"] == ref.shape[0]
+    np.testing.assert_array_equal(pts.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_ply_matches_live_reference(tmp_path):
+    from gaussian_splat_amd import scene as S
+    for seed, ascii in ((1, False), (2, True), (3, False)):
+        raw = S.synthetic_raw(500 if not ascii else 30, seed=seed, aspect=1.3)
+        raw.f_dc[::4] = 0
+        p = S.write_ply(tmp_path / f"r{seed}.ply", raw, ascii=ascii)
+        ok1, a = O.ref_ply_load(p)
+        ok2, b = O.ply_load(p)
+        assert ok1 == ok2
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_crop_restatement():
+    pts = np.load(GOLD / "ply" / "binary_62prop.ref.npy")
+    keep = O.crop(pts, 5.0)
+    ref = np.nonzero(np.all(np.abs(pts[:, :3]) < 5.0, axis=1))[0]
+    np.testing.assert_array_equal(keep, ref)
+    assert 0 < len(keep) < len(pts)
+
+
+def test_camera_known_answers():
+    V = O.look_at([0, 2, 5], [0, 0, 0], [0, -1, 0])
+    np.testing.assert_allclose(V, np.array(KA["default_view"]), rtol=0, atol=2e-7)
+    np.testing.assert_allclose(V[1, :3], [0, -0.9284767, 0.3713907], atol=1e-7)  # SURVEY §8c pin
+    P = O.perspective(45.0, np.float32(1920) / np.float32(1080), 0.1, 1000.0)
+    np.testing.assert_allclose(P, np.array(KA["proj_1080p"]), rtol=1e-6, atol=1e-7)
+    assert abs(P[0, 0] * 960 - KA["fx_1080p"]) < 1e-3
+    assert abs(P[0, 0] * 960 - 1303.675) < 1e-3
+    VP = O.mat4_mul(P, V)
+    np.testing.assert_allclose(VP, P.astype(np.float64) @ V.astype(np.float64), rtol=1e-6, atol=1e-6)
+
+
+def test_isotropic_splat_record():
+    """K1-K6 on a splat whose projection is hand-computable."""
+    from gaussian_splat_amd.api import Scene
+    k = KA["iso_splat"]
+    sc = Scene(pos=np.array([k["pos"]]), rot=np.array([k["rot"]]), scale=np.array([k["scale"]]),
+               opacity=np.array([0.8]), color=np.array([[0.1, 0.2, 0.3]]))
+    V = O.look_at([0, 2, 5], [0, 0, 0], [0, -1, 0])
+    P = O.perspective(45.0, 1.0, 0.1, 1000.0)
+    rec, dk, nt = O.project(sc, V, P, 256, 256)
+    r = rec[0]
+    for f in ("cx", "cy", "ax", "ay", "bx", "by"):
+        assert abs(float(r[f]) - k[f]) <= 2e-5 * max(1.0, abs(k[f])), f
+    x0, y0, x1, y1 = k["rect"]
+    assert int(r["rect_lo"]) == x0 | (y0 << 16) and int(r["rect_hi"]) == x1 | (y1 << 16)
+    assert nt[0] == k["ntiles"]
+    assert dk[0] == 0x7C00 - int(np.float16(k["zf"]).view(np.uint16))
+
+
+@pytest.mark.parametrize("case", sorted(KA["composite"]))
+@pytest.mark.parametrize("mode", ["tile", "live50"])
+def test_composite_known_answers(case, mode):
+    c = KA["composite"][case]
+    out = O.composite_list(np.array(c["frags"], np.float32).reshape(-1, 5), mode=mode, cap=c.get("cap", 0))
+    np.testing.assert_allclose(out, c[mode], rtol=0, atol=2e-7)
+
+
+def test_survey_depth_order_finding():
+    """descending distance -> the farthest (green) ends on top."""
+    out = O.composite_list(np.array(KA["composite"]["survey_rgb"]["frags"], np.float32), "tile")
+    np.testing.assert_allclose(out, [0.125, 0.5, 0.25, 0.875], atol=1e-7)
+
+
+def test_half_bits():
+    for v, bits in KA["half_bits"].items():
+        assert O.f16_bits(float(v)) == bits, v
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.uniform(1e-4, 2000, 20000), rng.uniform(1e-7, 1e-4, 2000)]).astype(np.float32)
+    got = np.array([O.f16_bits(float(x)) for x in xs], np.uint16)
+    np.testing.assert_array_equal(got, xs.astype(np.float16).view(np.uint16))
+
+
+def test_expf_accuracy():
+    xs = np.linspace(-4.7, 0.0, 20001, dtype=np.float32)
+    got = np.array([O.expf(float(x)) for x in xs], np.float64)
+    rel = np.abs(got / np.exp(xs.astype(np.float64)) - 1)
+    assert rel.max() < 5e-7
+    assert O.expf(0.0) == 1.0
+
+
+def test_oracle_render_invariants():
+    """Frame-level invariants of the contract on config 1."""
+    from gaussian_splat_amd import scene as S
+    sc = S.synthetic_scene(10000, seed=0, aspect=1.0)
+    V = O.look_at([0, 2, 5], [0, 0, 0], [0, -1, 0])
+    P = O.perspective(45.0, 1.0, 0.1, 1000.0)
+    img, st = O.render(sc, V, P, 256, 256)
+    a = img[..., 3]
+    assert (a >= 0).all() and (a <= 1.0 + 1e-6).all()
+    assert (img[..., :3] <= a[..., None] + 1e-6).all()  # premultiplied: C <= A when rgb <= 1
+    assert st["visible"] == 10000 and st["pairs"] > 10000
+    img2, _ = O.render(sc, V, P, 256, 256, nthreads=1)
+    np.testing.assert_array_equal(img.view(np.uint32), img2.view(np.uint32))  # thread-count independent
