@@ -1,42 +1,55 @@
 // composite.hip — per-tile front-to-back alpha composite.
 //
-// One 256-lane workgroup per 16x16 tile, one pixel per lane.  The tile's
-// depth-sorted splat list is streamed through LDS in batches of 256 records
-// (each lane gathers one 48-B record by splat id), then every lane walks the
-// batch: coverage (K6 closed form), gaussian + 0.01 cutoff (F1,
-// tile.metal:191-197), composite (A1: tile.metal:251-266, or A1': live
-// 50-layer rule, 50layer.metal:208-222).  Per-splat pixel rects give a
-// wave-uniform skip (the 64 lanes of a wave are 4 pixel rows of the tile),
-// and the workgroup stops fetching once every lane has saturated.
+// One 256-lane workgroup per 16x16 tile, one pixel per lane; wave w owns the
+// 16x4 pixel strip of rows 4w..4w+3.  The tile's depth-sorted splat list is
+// streamed through LDS in batches of 256 records (each lane gathers one 48-B
+// record by splat id).  Per batch every wave compacts, with one ballot per 64
+// records, the list of splats whose conservative pixel rect overlaps its
+// strip, then walks only that list: coverage (K6 closed
+// form), gaussian + 0.01 cutoff (F1, tile.metal:191-197) and the composite
+// (A1, tile.metal:251-266; or the live 50-layer rule, 50layer.metal:208-222).
+// The per-pixel body is branch-free (a non-covering splat contributes an
+// exact zero), a wave leaves the batch as soon as all 64 of its pixels are
+// saturated, and the workgroup stops fetching once all 256 are.
+// Tiles are dealt to workgroups XCD-aware: consecutive tiles of a row share
+// most of their splats, so they are placed on one XCD's L2.
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
 namespace gs {
 
 template <int MODE>
-__global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a) {
+__global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
+    __shared__ uint8_t wlist[4][kTileThreads];
+
+    // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
+    // residue class a contiguous run of tiles (cdna_hip_programming.md §5, T1).
+    const uint32_t orig = blockIdx.x;
+    const uint32_t xcd = orig & 7u, q = nwg >> 3, r = nwg & 7u;
+    const uint32_t wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+
     // Grid covers only the owned tile rows: ty = row_rem + k * row_mod.
-    const int owned_row = blockIdx.x / a.tiles_x;
-    const int tx = blockIdx.x - owned_row * a.tiles_x;
+    const int owned_row = (int)wg / a.tiles_x;
+    const int tx = (int)wg - owned_row * a.tiles_x;
     const int ty = a.row_rem + owned_row * a.row_mod;
     const int tile = ty * a.tiles_x + tx;
     const int width = a.width, height = a.height;
-    const uint32_t* __restrict__ sorted_vals = a.vals;
-    const float4* __restrict__ rec = a.rec;
     const int tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63;
     const int px = tx * kTile + (tid & 15);
     const int py = ty * kTile + (tid >> 4);
     const bool inside = px < width && py < height;
     const float fx = (float)px + 0.5f;
     const float fy = (float)py + 0.5f;
-    // pixel rows covered by this wave, tile columns
-    const uint32_t wy0 = (uint32_t)(ty * kTile + (tid >> 6) * 4), wy1 = wy0 + 3;
-    const uint32_t wx0 = (uint32_t)(tx * kTile), wx1 = wx0 + 15;
+    // this wave's strip: rows [wy0, wy0+3], tile columns [wx0, wx0+15]
+    const uint32_t wy0 = (uint32_t)(ty * kTile) + wave * 4u, wy1 = wy0 + 3u;
+    const uint32_t wx0 = (uint32_t)(tx * kTile), wx1 = wx0 + 15u;
 
     const uint2 rg = a.ranges[tile];
-    float A = 0.0f;  // tile: accumulated alpha; live50: transmittance stored as T
-    float T = 1.0f;
+    float A = 0.0f;  // tile rule: accumulated alpha
+    float T = 1.0f;  // live50 rule: transmittance
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     bool done = !inside;
     bool any = false;
@@ -45,45 +58,58 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a) {
         if (__syncthreads_count(!done) == 0) break;
         const uint32_t j = b + tid;
         if (j < rg.y) {
-            const uint32_t id = sorted_vals[j];
-            const float4* r = rec + (size_t)a.rec_stride * id;
-            s0[tid] = r[0];
-            s1[tid] = r[1];
-            s2[tid] = r[2];
+            const uint32_t id = a.vals[j];
+            const float4* rp = a.rec + (size_t)a.rec_stride * id;
+            s0[tid] = rp[0];
+            s1[tid] = rp[1];
+            s2[tid] = rp[2];
         }
         __syncthreads();
         const uint32_t cnt = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            if (__builtin_amdgcn_readfirstlane((int)__all(done))) break;
-            const float4 c = s2[k];
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(__float_as_uint(c.z));
-            const uint32_t hi = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
-            // wave-uniform rect skip (rect is conservative)
-            if ((hi >> 16) < wy0 || (lo >> 16) > wy1 || (hi & 0xFFFFu) < wx0 || (lo & 0xFFFFu) > wx1) continue;
+        // wave-level compaction of the splats overlapping this strip (index order kept)
+        uint32_t nl = 0;
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            bool hit = false;
+            if (k < cnt) {
+                const float4 c = s2[k];
+                const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+                hit = !((hi >> 16) < wy0 || (lo >> 16) > wy1 || (hi & 0xFFFFu) < wx0 || (lo & 0xFFFFu) > wx1);
+            }
+            const uint64_t m = __ballot(hit);
+            if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
+            nl += (uint32_t)__popcll(m);
+        }
+        // (wlist[wave] is only touched by this wave: DS ops of one wave are ordered)
+        for (uint32_t i = 0; i < nl; ++i) {
+            if (__ballot(!done) == 0) break;
+            const uint32_t k = wlist[wave][i];
             const float4 aa = s0[k];
             const float4 bb = s1[k];
+            const float4 cc = s2[k];
             const float dx = fx - aa.x;
             const float dy = aa.y - fy;
             const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
             const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
-            const float q = __builtin_fmaf(v, v, u * u);
-            if (!done && fabsf(u) <= 3.0f && fabsf(v) <= 3.0f && q <= kQMax) {
-                const float alpha = bb.z * gs_exp(-0.5f * q);
-                any = true;
-                if constexpr (MODE == 0) {
-                    const float sa = alpha * (1.0f - A);
-                    C0 = __builtin_fmaf(bb.w, sa, C0);
-                    C1 = __builtin_fmaf(c.x, sa, C1);
-                    C2 = __builtin_fmaf(c.y, sa, C2);
-                    A = A + sa;
-                    if (A >= kSat) done = true;
-                } else {
-                    C0 = __builtin_fmaf(bb.w, T, C0);
-                    C1 = __builtin_fmaf(c.x, T, C1);
-                    C2 = __builtin_fmaf(c.y, T, C2);
-                    T = T * (1.0f - alpha);
-                    if (T < kTMin) done = true;
-                }
+            const float qq = __builtin_fmaf(v, v, u * u);
+            const bool in = !done && fabsf(u) <= 3.0f && fabsf(v) <= 3.0f && qq <= kQMax;
+            const float alpha = bb.z * gs_exp(-0.5f * qq);
+            any |= in;
+            if constexpr (MODE == 0) {
+                // out-of-support lanes add an exact zero: bit-identical to skipping
+                const float sa = in ? alpha * (1.0f - A) : 0.0f;
+                C0 = __builtin_fmaf(bb.w, sa, C0);
+                C1 = __builtin_fmaf(cc.x, sa, C1);
+                C2 = __builtin_fmaf(cc.y, sa, C2);
+                A = A + sa;
+                done = done || A >= kSat;
+            } else {
+                const float tw = in ? T : 0.0f;
+                C0 = __builtin_fmaf(bb.w, tw, C0);
+                C1 = __builtin_fmaf(cc.x, tw, C1);
+                C2 = __builtin_fmaf(cc.y, tw, C2);
+                T = in ? T * (1.0f - alpha) : T;
+                done = done || T < kTMin;
             }
         }
     }
@@ -103,12 +129,12 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a) {
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st) {
     if (a.row_mod < 1 || a.row_rem < 0 || a.row_rem >= a.row_mod) return hipErrorInvalidValue;
     const int owned_rows = a.tiles_y > a.row_rem ? (a.tiles_y - a.row_rem + a.row_mod - 1) / a.row_mod : 0;
-    dim3 grid(a.tiles_x * owned_rows);
-    if (grid.x == 0) return hipSuccess;
+    const uint32_t nwg = (uint32_t)(a.tiles_x * owned_rows);
+    if (nwg == 0) return hipSuccess;
     if (mode == 0)
-        composite_kernel<0><<<grid, 256, 0, st>>>(a);
+        composite_kernel<0><<<nwg, 256, 0, st>>>(a, nwg);
     else
-        composite_kernel<1><<<grid, 256, 0, st>>>(a);
+        composite_kernel<1><<<nwg, 256, 0, st>>>(a, nwg);
     return hipGetLastError();
 }
 
