@@ -48,7 +48,7 @@ def parse():
 
 
 def stage_summary(stats_list):
-    keys = ["preprocess", "scan", "duplicate", "sort", "ranges", "composite"]
+    keys = ["preprocess", "depth_sort", "scan", "duplicate", "sort", "ranges", "composite"]
     out = {}
     for k in keys:
         ms = float(np.mean([s[f"ms_{k}"] for s in stats_list]))

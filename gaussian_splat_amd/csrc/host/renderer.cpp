@@ -77,8 +77,9 @@ struct gs_handle {
     bool initialized = false;
     DevBuf p0, p1, p2, p3, sh4, sh1;
     // per-frame scratch
-    DevBuf rec, dkey, ntiles, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb;
-    DevBuf xmask, xcounts, xtotal, rdkey, rntiles, roffsets, rpartials;  // multi-GPU exchange
+    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb;
+    DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
+    DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
     uint64_t* host_total = nullptr;  // pinned
     hipEvent_t ev[8] = {};
@@ -91,9 +92,9 @@ struct gs_handle {
     int64_t index_base = 0;
 
     ~gs_handle() {
-        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &ntiles, &offsets, &partials, &total,
-                          &keys, &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &xmask, &xcounts, &xtotal,
-                          &rdkey, &rntiles, &roffsets, &rpartials})
+        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
+                          &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
+                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi})
             b->release();
         if (host_total) (void)hipHostFree(host_total);
         if (host_xtotal) (void)hipHostFree(host_xtotal);
@@ -210,7 +211,8 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     const size_t n = (size_t)std::max<int64_t>(h->n, 1);
     GS_HIP(h->rec.reserve(n * sizeof(gs::Record3)));
     GS_HIP(h->dkey.reserve(n * 4));
-    GS_HIP(h->ntiles.reserve(n * 4));
+    GS_HIP(h->rlo.reserve(n * 4));
+    GS_HIP(h->rhi.reserve(n * 4));
     GS_HIP(h->offsets.reserve(n * 4));
     GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 8));
     GS_HIP(h->total.reserve(8));
@@ -232,22 +234,38 @@ float elapsed(gs_handle* h, int a, int b) {
     return ms;
 }
 
-// Stages 1-2: project all splats and prefix-sum the tile counts; returns P.
-gs_status project_and_count(gs_handle* h, const gs::FrameUniforms& U, hipStream_t st, uint64_t* pairs) {
-    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(),
-                                 h->dkey.as<uint32_t>(), h->ntiles.as<uint32_t>(), st));
-    mark(h, 1, st);
-    GS_HIP(gs::launch_exclusive_scan(h->ntiles.as<uint32_t>(), h->offsets.as<uint32_t>(),
-                                     h->partials.as<uint64_t>(), h->total.as<uint64_t>(), (uint32_t)h->n, st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
+// Binning + sort + composite over m items (local splats, or received
+// exchange records): depth sort -> ordered scan of tile counts (P to host) ->
+// duplicate in depth order -> stable sort by tile -> ranges -> composite.
+gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
+                             const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
+                             int world, int rank, int compact, float4* out, hipStream_t st) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    const size_t mm = (size_t)std::max<uint32_t>(m, 1);
+    for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth, &h->offsets})
+        GS_HIP(b->reserve(mm * 4));
+    GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 8));
+    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)mm) * 4));
+    // 1. splats by depth (descending zF == ascending dkey), ties by index,
+    //    carrying (index, rect) so everything downstream reads sequentially
+    bool in_tmp = false;
+    const uint32_t* vin[3] = {nullptr, rect_lo, rect_hi};
+    uint32_t* vout[3] = {h->dso.as<uint32_t>(), h->dsl.as<uint32_t>(), h->dsh.as<uint32_t>()};
+    uint32_t* vtmp[3] = {h->dto.as<uint32_t>(), h->dtl.as<uint32_t>(), h->dth.as<uint32_t>()};
+    GS_HIP(gs::launch_radix_sort3(dkey, vin, h->dsk.as<uint32_t>(), vout, h->dtk.as<uint32_t>(), vtmp, m,
+                                  gs::kDepthBits, h->sort_scratch.as<uint32_t>(), &in_tmp, st));
+    const uint32_t* order = in_tmp ? vtmp[0] : vout[0];
+    const uint32_t* slo = in_tmp ? vtmp[1] : vout[1];
+    const uint32_t* shi = in_tmp ? vtmp[2] : vout[2];
     mark(h, 2, st);
-    GS_HIP(hipStreamSynchronize(st));  // P sizes the pair buffers and sort grids
-    *pairs = *h->host_total;
-    if (*pairs >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,tile) pairs");
-    return GS_OK;
-}
-
-gs_status ensure_pair_scratch(gs_handle* h, uint64_t P, uint32_t T) {
+    // 2. tile counts in depth order -> pair offsets; P sizes the pair buffers
+    GS_HIP(gs::launch_tile_count_scan(slo, shi, m, world, rank, h->offsets.as<uint32_t>(), h->partials.as<uint64_t>(),
+                                      h->total.as<uint64_t>(), st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    mark(h, 3, st);
+    const uint64_t P = *h->host_total;
+    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,tile) pairs");
     const size_t p = (size_t)std::max<uint64_t>(P, 1);
     GS_HIP(h->keys.reserve(p * 4));
     GS_HIP(h->vals.reserve(p * 4));
@@ -255,25 +273,22 @@ gs_status ensure_pair_scratch(gs_handle* h, uint64_t P, uint32_t T) {
     GS_HIP(h->tvals.reserve(p * 4));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
-    return GS_OK;
-}
-
-// Stages 3-6 on the pairs already emitted into h->keys/h->vals.
-gs_status sort_and_composite(gs_handle* h, uint64_t P, const gs::FrameUniforms& U, const float4* rec,
-                             int rec_stride, int row_mod, int row_rem, int compact, float4* out, hipStream_t st) {
-    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    const int bits = bits_for(T) + gs::kDepthBits;
-    bool in_tmp = false;
-    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(),
-                                 h->tvals.as<uint32_t>(), (uint32_t)P, bits, h->sort_scratch.as<uint32_t>(),
-                                 &in_tmp, st));
+    // 3. pairs (tile, splat) in depth order
+    GS_HIP(gs::launch_duplicate(order, slo, shi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, world, rank,
+                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    mark(h, 4, st);
+    // 4. stable sort by tile id only
+    const int bits = bits_for(T);
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
+                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
+                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st));
     uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
     uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
     h->last_keys = sk;
     h->last_vals = sv;
-    mark(h, 4, st);
-    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
     mark(h, 5, st);
+    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
+    mark(h, 6, st);
     gs::CompositeArgs ca;
     ca.vals = sv;
     ca.ranges = h->ranges.as<uint2>();
@@ -283,14 +298,15 @@ gs_status sort_and_composite(gs_handle* h, uint64_t P, const gs::FrameUniforms& 
     ca.height = U.height;
     ca.tiles_x = U.tiles_x;
     ca.tiles_y = U.tiles_y;
-    ca.row_mod = row_mod;
-    ca.row_rem = row_rem;
+    ca.row_mod = world;
+    ca.row_rem = rank;
     ca.compact = compact;
     ca.out = out;
     GS_HIP(gs::launch_composite(ca, h->opt.mode, st));
-    mark(h, 6, st);
+    mark(h, 7, st);
+    h->stats.pairs = (int64_t)P;
     h->stats.sort_bits = bits;
-    h->stats.sort_passes = (bits + 7) / 8;
+    h->stats.sort_passes = gs::make_sort_plan(bits).passes;
     return GS_OK;
 }
 
@@ -304,21 +320,24 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     const int64_t N = h->n, T = s.tiles;
     const int64_t bin = 56 + (h->opt.sh_degree > 0 ? 4 * 3 * sh_coeffs(h->opt.sh_degree) : 0);
     // Algorithmic bytes: what each stage must move at minimum.
+    const int64_t Pi = (int64_t)P, dpass = gs::make_sort_plan(gs::kDepthBits).passes;
     s.bytes_preprocess = N * (bin + 48 + 8);
-    s.bytes_scan = N * 8;
-    s.bytes_duplicate = N * (16 + 8) + (int64_t)P * 8;
-    s.bytes_sort = (int64_t)s.sort_passes * (int64_t)P * 20;
-    s.bytes_ranges = (int64_t)P * 4 + T * 8;
-    s.bytes_composite = T * 8 + (int64_t)P * (4 + 48) + (int64_t)U.width * U.height * 16;
+    s.bytes_depth_sort = N * (4 + 16 * dpass);
+    s.bytes_scan = N * 20;
+    s.bytes_duplicate = N * 20 + Pi * 8;
+    s.bytes_sort = Pi * (4 + 16 * (int64_t)s.sort_passes);
+    s.bytes_ranges = Pi * 4 + T * 8;
+    s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
     if (h->opt.stage_timing && h->events) {
-        (void)hipEventSynchronize(h->ev[6]);
+        (void)hipEventSynchronize(h->ev[7]);
         s.ms_preprocess = elapsed(h, 0, 1);
-        s.ms_scan = elapsed(h, 1, 2);
-        s.ms_duplicate = elapsed(h, 2, 3);
-        s.ms_sort = elapsed(h, 3, 4);
-        s.ms_ranges = elapsed(h, 4, 5);
-        s.ms_composite = elapsed(h, 5, 6);
-        s.ms_total = elapsed(h, 0, 6);
+        s.ms_depth_sort = elapsed(h, 1, 2);
+        s.ms_scan = elapsed(h, 2, 3);
+        s.ms_duplicate = elapsed(h, 3, 4);
+        s.ms_sort = elapsed(h, 4, 5);
+        s.ms_ranges = elapsed(h, 5, 6);
+        s.ms_composite = elapsed(h, 6, 7);
+        s.ms_total = elapsed(h, 0, 7);
     }
 }
 
@@ -463,7 +482,7 @@ gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t 
     hipStream_t st = static_cast<hipStream_t>(stream);
     const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    if (bits_for(T) + gs::kDepthBits > 32) return fail(GS_ERR_UNSUPPORTED, "too many tiles for 32-bit keys");
+    if (T == 0 || bits_for(T) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     float4* out = reinterpret_cast<float4*>(out_rgba);
     if (!out_is_device) {
@@ -472,14 +491,13 @@ gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t 
     }
     std::memset(&h->stats, 0, sizeof h->stats);
     mark(h, 0, st);
-    uint64_t P = 0;
-    if ((s = project_and_count(h, U, st, &P)) != GS_OK) return s;
-    if ((s = ensure_pair_scratch(h, P, T)) != GS_OK) return s;
-    GS_HIP(gs::launch_duplicate(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->ntiles.as<uint32_t>(),
-                                h->offsets.as<uint32_t>(), (uint32_t)h->n, (uint32_t)U.tiles_x,
-                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
-    mark(h, 3, st);
-    if ((s = sort_and_composite(h, P, U, h->rec.as<float4>(), 3, 1, 0, 0, out, st)) != GS_OK) return s;
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
+    mark(h, 1, st);
+    if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 1, 0, 0, out, st)) != GS_OK)
+        return s;
+    const uint64_t P = (uint64_t)h->stats.pairs;
     if (!out_is_device) {
         GS_HIP(hipMemcpyAsync(out_rgba, out, (size_t)W * H * 16, hipMemcpyDeviceToHost, st));
         GS_HIP(hipStreamSynchronize(st));
@@ -503,12 +521,20 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
     const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
     hipStream_t st = nullptr;
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->ntiles.as<uint32_t>(), st));
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     GS_HIP(hipStreamSynchronize(st));
     const size_t n = (size_t)h->n;
     if (records) GS_HIP(hipMemcpy(records, h->rec.ptr, n * sizeof(gs::Record3), hipMemcpyDeviceToHost));
     if (dkeys) GS_HIP(hipMemcpy(dkeys, h->dkey.ptr, n * 4, hipMemcpyDeviceToHost));
-    if (ntiles) GS_HIP(hipMemcpy(ntiles, h->ntiles.ptr, n * 4, hipMemcpyDeviceToHost));
+    if (ntiles) {
+        std::vector<uint32_t> lo(n), hi(n);
+        GS_HIP(hipMemcpy(lo.data(), h->rlo.ptr, n * 4, hipMemcpyDeviceToHost));
+        GS_HIP(hipMemcpy(hi.data(), h->rhi.ptr, n * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t x0 = lo[i] & 0xFFFF, x1 = hi[i] & 0xFFFF, y0 = lo[i] >> 16, y1 = hi[i] >> 16;
+            ntiles[i] = x1 < x0 ? 0u : ((x1 >> 4) - (x0 >> 4) + 1) * ((y1 >> 4) - (y0 >> 4) + 1);
+        }
+    }
     return GS_OK;
 }
 
@@ -533,7 +559,8 @@ gs_status gs_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys
     uint32_t* scratch = nullptr;
     GS_HIP(hipMalloc(&scratch, gs::radix_sort_scratch_words((uint32_t)n) * 4));
     bool in_tmp = false;
-    hipError_t e = gs::launch_radix_sort(keys, vals, tmp_keys, tmp_vals, (uint32_t)n, bits, scratch, &in_tmp, st);
+    hipError_t e = gs::launch_radix_sort(keys, vals, keys, vals, tmp_keys, tmp_vals, (uint32_t)n, bits, scratch,
+                                         &in_tmp, st);
     if (e == hipSuccess && in_tmp) {
         e = hipMemcpyAsync(keys, tmp_keys, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(vals, tmp_vals, (size_t)n * 4, hipMemcpyDeviceToDevice, st);
@@ -573,9 +600,9 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
     GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
     if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->ntiles.as<uint32_t>(), st));
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
-    GS_HIP(gs::launch_shard_count(h->rec.as<float4>(), h->ntiles.as<uint32_t>(), n, h->world,
+    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
@@ -609,25 +636,16 @@ gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, 
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     const size_t mm = (size_t)std::max<int64_t>(m, 1);
     GS_HIP(h->rdkey.reserve(mm * 4));
-    GS_HIP(h->rntiles.reserve(mm * 4));
-    GS_HIP(h->roffsets.reserve(mm * 4));
-    GS_HIP(h->rpartials.reserve((mm + gs::kScanItems - 1) / gs::kScanItems * 8 + 8));
+    GS_HIP(h->rrlo.reserve(mm * 4));
+    GS_HIP(h->rrhi.reserve(mm * 4));
     const float4* rv = static_cast<const float4*>(recv);
-    GS_HIP(gs::launch_recv_count(rv, (uint32_t)m, h->world, h->rank, h->rntiles.as<uint32_t>(),
-                                 h->rdkey.as<uint32_t>(), st));
-    GS_HIP(gs::launch_exclusive_scan(h->rntiles.as<uint32_t>(), h->roffsets.as<uint32_t>(),
-                                     h->rpartials.as<uint64_t>(), h->total.as<uint64_t>(), (uint32_t)m, st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
-    GS_HIP(hipStreamSynchronize(st));
-    const uint64_t P = *h->host_total;
-    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "too many pairs");
-    if ((s = ensure_pair_scratch(h, P, T)) != GS_OK) return s;
-    GS_HIP(gs::launch_recv_duplicate(rv, h->rdkey.as<uint32_t>(), h->rntiles.as<uint32_t>(),
-                                     h->roffsets.as<uint32_t>(), (uint32_t)m, (uint32_t)U.tiles_x, h->world, h->rank,
-                                     h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
-    if ((s = sort_and_composite(h, P, U, rv, gs::kXRecFloat4, h->world, h->rank, 1,
+    GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
+                                  h->rrhi.as<uint32_t>(), st));
+    if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
+                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, h->world, h->rank, 1,
                                 reinterpret_cast<float4*>(out_rgba), st)) != GS_OK)
         return s;
+    const uint64_t P = (uint64_t)h->stats.pairs;
     h->stats.pairs = (int64_t)P;
     h->stats.tiles = T;
     return GS_OK;

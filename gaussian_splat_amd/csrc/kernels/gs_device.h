@@ -75,6 +75,23 @@ __device__ __forceinline__ uint32_t half_bits(float f) {
     return (uint32_t)__builtin_bit_cast(unsigned short, h);
 }
 
-__device__ __forceinline__ float4 ldg4(const float4* p) { return *p; }
+// Packed inclusive pixel rect: lo = x0 | y0 << 16, hi = x1 | y1 << 16.  A culled
+// splat carries the empty rect (lo = 0xFFFFFFFF, hi = 0).
+constexpr uint32_t kEmptyRectLo = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t first_owned_row(uint32_t a, uint32_t world, uint32_t rank) {
+    return a + (rank + world - a % world) % world;
+}
+
+// Tiles of the rect whose tile row is owned by `rank` (ty % world == rank).
+__device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, uint32_t world, uint32_t rank) {
+    const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
+    if (x1 < x0) return 0u;
+    const uint32_t ty0 = (lo >> 16) >> 4, ty1 = (hi >> 16) >> 4;
+    const uint32_t cols = (x1 >> 4) - (x0 >> 4) + 1u;
+    if (world == 1) return (ty1 - ty0 + 1u) * cols;
+    const uint32_t f = first_owned_row(ty0, world, rank);
+    return f > ty1 ? 0u : ((ty1 - f) / world + 1u) * cols;
+}
 
 }  // namespace gs

@@ -10,35 +10,53 @@
 namespace gs {
 
 // ---- preprocess.hip ------------------------------------------------------
+// Writes the 48-B record (visible splats), the 15-bit depth key and the packed
+// pixel rect (empty rect for culled splats).
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
-                             uint32_t* dkey, uint32_t* ntiles, hipStream_t st);
+                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st);
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
-// Exclusive scan of counts[n] into offsets[n]; *total (device u64) = sum.
-// partials: ceil(n / kScanItems) u64 scratch.
-hipError_t launch_exclusive_scan(const uint32_t* counts, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                 uint32_t n, hipStream_t st);
+// Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], world, rank) into
+// offsets[n]; *total (device u64) = sum.  partials: ceil(n / kScanItems) u64.
+hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
+                                  int rank, uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st);
 
 // ---- binning.hip -----------------------------------------------------------
-// Emit (tile << 15 | dkey, splat index + index_base) for every tile of every
-// splat rect, at offsets[i].
-hipError_t launch_duplicate(const float4* rec, const uint32_t* dkey, const uint32_t* ntiles,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, uint32_t* keys,
-                            uint32_t* vals, hipStream_t st);
-// ranges[tile] = [start, end) in the sorted pair array (zero-initialised here).
+// Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
+// rect_hi[j]) emits (tile, order[j]) for each tile of its rect whose row is
+// owned (ty % world == rank), starting at offsets[j].
+hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, int world, int rank,
+                            uint32_t* keys, uint32_t* vals, hipStream_t st);
+// ranges[tile] = [start, end) in the tile-sorted pair array (zeroed here).
 hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* ranges, uint32_t ntiles_total,
                               hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
-constexpr int kSortTile = 4096;  // items per block
-constexpr int kSortBins = 256;
-// Scratch elements (uint32) needed by launch_radix_sort for n items.
+constexpr int kSortTile = 8192;  // items per onesweep tile (512 lanes x 16)
+constexpr int kSortBins = 256;   // 8-bit digits
+constexpr int kMaxSortPasses = 4;
+struct SortPlan {
+    int passes;
+    int shift[kMaxSortPasses];
+    int width[kMaxSortPasses];
+    uint32_t mask[kMaxSortPasses];
+};
+SortPlan make_sort_plan(int bits);
+// Scratch words (uint32) needed by launch_radix_sort for n items.
 size_t radix_sort_scratch_words(uint32_t n);
-// Stable LSD sort of (keys, vals) on bits [0, bits).  Ping-pongs with
-// tmp_keys / tmp_vals; *result_in_tmp tells where the sorted data ended.
-hipError_t launch_radix_sort(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n,
-                             int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st);
+// Stable LSD sort on key bits [0, bits).  Reads (keys_in, vals_in) — vals_in
+// may be null (value = index) — and leaves the result in (keys, vals), or in
+// (tmp_keys, tmp_vals) when *result_in_tmp (only if the inputs alias the
+// outputs and the pass count is odd).
+hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
+                             uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
+                             bool* result_in_tmp, hipStream_t st);
+// Same with three value arrays (vals_in[0] may be null: value = index).
+hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
+                              uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
+                              int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st);
 
 // ---- composite.hip ---------------------------------------------------------
 struct CompositeArgs {
@@ -60,7 +78,7 @@ constexpr int kXRecFloat4 = 4;  // 64-B exchange record: 48-B record + dkey, glo
 constexpr int kMaxWorld = 32;
 // dest_mask[i]: bit r set iff splat i touches a tile row owned by rank r.
 // counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
-hipError_t launch_shard_count(const float4* rec, const uint32_t* ntiles, uint32_t n, int world,
+hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);
 // Exclusive scan of each destination row; dest_total[world].
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);
@@ -68,12 +86,7 @@ hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32
 hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
                              int world, uint32_t index_base, const uint32_t* counts, const uint32_t* dest_total,
                              uint32_t nblocks, float4* send, hipStream_t st);
-// Per received record: tiles in owned rows, and dkey.
-hipError_t launch_recv_count(const float4* recv, uint32_t m, int world, int rank, uint32_t* ntiles,
-                             uint32_t* dkey, hipStream_t st);
-// duplicate for received records restricted to owned tile rows.
-hipError_t launch_recv_duplicate(const float4* recv, const uint32_t* dkey, const uint32_t* ntiles,
-                                 const uint32_t* offsets, uint32_t m, uint32_t tiles_x, int world, int rank,
-                                 uint32_t* keys, uint32_t* vals, hipStream_t st);
-
+// Unpack dkey and packed rect of every received exchange record.
+hipError_t launch_recv_unpack(const float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+                              uint32_t* rect_hi, hipStream_t st);
 }  // namespace gs

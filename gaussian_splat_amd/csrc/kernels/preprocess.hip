@@ -84,13 +84,14 @@ __device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px
 template <int DEG>
 __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
-                                                         uint32_t* __restrict__ ntiles) {
+                                                         uint32_t* __restrict__ rect_lo,
+                                                         uint32_t* __restrict__ rect_hi) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= s.n) return;
     const float* V = U.V;
     const float* VP = U.VP;
-    uint32_t count = 0;
     uint32_t key = 0;
+    uint32_t rlo = kEmptyRectLo, rhi = 0u;
 
     float4 a0 = s.p0[i];
     float px = a0.x, py = a0.y, pz = a0.z;
@@ -228,24 +229,26 @@ __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const Frame
                     o[1] = make_float4(e2x * k2, e2y * k2, a0.w, cr);
                     o[2] = make_float4(cg, cbl, __uint_as_float(x0 | (y0 << 16)), __uint_as_float(x1 | (y1 << 16)));
                     key = kDepthInf - half_bits(zf);
-                    count = ((x1 >> 4) - (x0 >> 4) + 1) * ((y1 >> 4) - (y0 >> 4) + 1);
+                    rlo = x0 | (y0 << 16);
+                    rhi = x1 | (y1 << 16);
                 }
             }
         }
     }
     dkey[i] = key;
-    ntiles[i] = count;
+    rect_lo[i] = rlo;
+    rect_hi[i] = rhi;
 }
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
-                             uint32_t* dkey, uint32_t* ntiles, hipStream_t st) {
+                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st) {
     if (s.n == 0) return hipSuccess;
     dim3 grid((s.n + 255) / 256), block(256);
     switch (sh_degree) {
-    case 0: preprocess_kernel<0><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
-    case 1: preprocess_kernel<1><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
-    case 2: preprocess_kernel<2><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
-    case 3: preprocess_kernel<3><<<grid, block, 0, st>>>(s, U, rec, dkey, ntiles); break;
+    case 0: preprocess_kernel<0><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 1: preprocess_kernel<1><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 2: preprocess_kernel<2><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 3: preprocess_kernel<3><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -1,5 +1,5 @@
-// scan.hip — exclusive prefix sum of per-splat tile counts (reduce-then-scan).
-// 8 B/splat of HBM traffic (read counts twice from L2/HBM, write offsets).
+// scan.hip — exclusive prefix sum of per-splat tile counts (reduce-then-scan);
+// the counts are derived from the depth-sorted packed rects on the fly.
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -7,15 +7,25 @@ namespace gs {
 
 constexpr int kScanIpt = kScanItems / 256;  // 16 consecutive items per lane
 
-__global__ __launch_bounds__(256) void scan_reduce_kernel(const uint32_t* __restrict__ counts, uint32_t n,
+struct CountSrc {
+    const uint32_t* lo;
+    const uint32_t* hi;
+    uint32_t world, rank;
+};
+
+__device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
+    return rect_tile_count(c.lo[i], c.hi[i], c.world, c.rank);
+}
+
+__global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials) {
     __shared__ uint64_t tmp[4];
     const uint32_t base = blockIdx.x * kScanItems;
     uint64_t s = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
-        uint32_t idx = base + k * 256 + threadIdx.x;
-        if (idx < n) s += counts[idx];
+        uint32_t i = base + k * 256 + threadIdx.x;
+        if (i < n) s += count_at(src, i);
     }
     uint64_t total;
     block256_exclusive_scan<uint64_t>(s, tmp, &total);
@@ -38,7 +48,7 @@ __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict
     if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ __launch_bounds__(256) void scan_down_kernel(const uint32_t* __restrict__ counts, uint32_t n,
+__global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n,
                                                         const uint64_t* __restrict__ partials,
                                                         uint32_t* __restrict__ offsets) {
     __shared__ uint32_t tmp[4];
@@ -48,7 +58,7 @@ __global__ __launch_bounds__(256) void scan_down_kernel(const uint32_t* __restri
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         uint32_t idx = base + k;
-        v[k] = idx < n ? counts[idx] : 0u;
+        v[k] = idx < n ? count_at(src, idx) : 0u;
         s += v[k];
     }
     uint32_t t;
@@ -62,15 +72,16 @@ __global__ __launch_bounds__(256) void scan_down_kernel(const uint32_t* __restri
     }
 }
 
-hipError_t launch_exclusive_scan(const uint32_t* counts, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                 uint32_t n, hipStream_t st) {
+hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
+                                  int rank, uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st) {
+    const CountSrc src{rect_lo, rect_hi, (uint32_t)world, (uint32_t)rank};
     uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
         return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
     }
-    scan_reduce_kernel<<<nb, 256, 0, st>>>(counts, n, partials);
+    scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials);
     scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total);
-    scan_down_kernel<<<nb, 256, 0, st>>>(counts, n, partials, offsets);
+    scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
     return hipGetLastError();
 }
 

@@ -22,8 +22,8 @@ __device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, int wor
     return m;
 }
 
-__global__ __launch_bounds__(256) void shard_count_kernel(const float4* __restrict__ rec,
-                                                          const uint32_t* __restrict__ ntiles, uint32_t n,
+__global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __restrict__ rect_lo,
+                                                          const uint32_t* __restrict__ rect_hi, uint32_t n,
                                                           int world, uint32_t* __restrict__ dest_mask,
                                                           uint32_t* __restrict__ counts, uint32_t nblocks) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];
@@ -33,10 +33,9 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const float4* __restri
     for (int k = 0; k < kShIpt; ++k) {
         uint32_t i = base + k * 64 + lane;
         uint32_t m = 0;
-        if (i < n && ntiles[i] > 0) {
-            float4 c = rec[3 * (size_t)i + 2];
-            uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
-            m = row_mask((lo >> 16) >> 4, (hi >> 16) >> 4, world);
+        if (i < n) {
+            const uint32_t lo = rect_lo[i], hi = rect_hi[i];
+            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> 4, (hi >> 16) >> 4, world);
         }
         if (i < n) dest_mask[i] = m;
         for (int d = 0; d < world; ++d) {
@@ -124,56 +123,23 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
     }
 }
 
-__device__ __forceinline__ uint32_t first_owned(uint32_t a, int world, int rank) {
-    uint32_t w = (uint32_t)world;
-    return a + ((uint32_t)rank + w - a % w) % w;
-}
-
-__global__ __launch_bounds__(256) void recv_count_kernel(const float4* __restrict__ recv, uint32_t m, int world,
-                                                         int rank, uint32_t* __restrict__ ntiles,
-                                                         uint32_t* __restrict__ dkey) {
-    uint32_t i = blockIdx.x * 256u + threadIdx.x;
+__global__ __launch_bounds__(256) void recv_unpack_kernel(const float4* __restrict__ recv, uint32_t m,
+                                                          uint32_t* __restrict__ dkey, uint32_t* __restrict__ rect_lo,
+                                                          uint32_t* __restrict__ rect_hi) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= m) return;
     const float4* r = recv + (size_t)kXRecFloat4 * i;
-    float4 c = r[2];
-    float4 x = r[3];
-    uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
-    uint32_t ty0 = (lo >> 16) >> 4, ty1 = (hi >> 16) >> 4;
-    uint32_t tx0 = (lo & 0xFFFFu) >> 4, tx1 = (hi & 0xFFFFu) >> 4;
-    uint32_t f = first_owned(ty0, world, rank);
-    uint32_t rows = f > ty1 ? 0u : (ty1 - f) / (uint32_t)world + 1u;
-    ntiles[i] = rows * (tx1 - tx0 + 1);
-    dkey[i] = __float_as_uint(x.x);
+    const float4 c = r[2];
+    dkey[i] = __float_as_uint(r[3].x);
+    rect_lo[i] = __float_as_uint(c.z);
+    rect_hi[i] = __float_as_uint(c.w);
 }
 
-__global__ __launch_bounds__(256) void recv_duplicate_kernel(const float4* __restrict__ recv,
-                                                             const uint32_t* __restrict__ dkey,
-                                                             const uint32_t* __restrict__ ntiles,
-                                                             const uint32_t* __restrict__ offsets, uint32_t m,
-                                                             uint32_t tiles_x, int world, int rank,
-                                                             uint32_t* __restrict__ keys,
-                                                             uint32_t* __restrict__ vals) {
-    uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= m || ntiles[i] == 0) return;
-    float4 c = recv[(size_t)kXRecFloat4 * i + 2];
-    uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
-    uint32_t ty0 = (lo >> 16) >> 4, ty1 = (hi >> 16) >> 4;
-    uint32_t tx0 = (lo & 0xFFFFu) >> 4, tx1 = (hi & 0xFFFFu) >> 4;
-    uint32_t off = offsets[i], dk = dkey[i];
-    for (uint32_t ty = first_owned(ty0, world, rank); ty <= ty1; ty += (uint32_t)world) {
-        for (uint32_t tx = tx0; tx <= tx1; ++tx) {
-            keys[off] = ((ty * tiles_x + tx) << kDepthBits) | dk;
-            vals[off] = i;
-            ++off;
-        }
-    }
-}
-
-hipError_t launch_shard_count(const float4* rec, const uint32_t* ntiles, uint32_t n, int world,
+hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st) {
     if (world < 1 || world > kMaxWorld) return hipErrorInvalidValue;
     if (nblocks == 0) return hipSuccess;
-    shard_count_kernel<<<nblocks, 256, 0, st>>>(rec, ntiles, n, world, dest_mask, counts, nblocks);
+    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, dest_mask, counts, nblocks);
     return hipGetLastError();
 }
 
@@ -192,19 +158,10 @@ hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint
     return hipGetLastError();
 }
 
-hipError_t launch_recv_count(const float4* recv, uint32_t m, int world, int rank, uint32_t* ntiles,
-                             uint32_t* dkey, hipStream_t st) {
+hipError_t launch_recv_unpack(const float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+                              uint32_t* rect_hi, hipStream_t st) {
     if (m == 0) return hipSuccess;
-    recv_count_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, world, rank, ntiles, dkey);
-    return hipGetLastError();
-}
-
-hipError_t launch_recv_duplicate(const float4* recv, const uint32_t* dkey, const uint32_t* ntiles,
-                                 const uint32_t* offsets, uint32_t m, uint32_t tiles_x, int world, int rank,
-                                 uint32_t* keys, uint32_t* vals, hipStream_t st) {
-    if (m == 0) return hipSuccess;
-    recv_duplicate_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, dkey, ntiles, offsets, m, tiles_x, world, rank,
-                                                           keys, vals);
+    recv_unpack_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, dkey, rect_lo, rect_hi);
     return hipGetLastError();
 }
 

@@ -85,6 +85,9 @@ typedef struct gs_stats {
     /* stage times in ms (valid when options.stage_timing = 1) */
     float ms_preprocess, ms_scan, ms_duplicate, ms_sort, ms_ranges, ms_composite, ms_total;
     int64_t bytes_preprocess, bytes_scan, bytes_duplicate, bytes_sort, bytes_ranges, bytes_composite;
+    float ms_depth_sort;   /* splats by depth key (ms_sort = pairs by tile) */
+    int32_t pad0;
+    int64_t bytes_depth_sort;
 } gs_stats;
 
 typedef struct gs_handle gs_handle;

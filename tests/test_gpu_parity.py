@@ -110,8 +110,8 @@ def test_sorted_pairs_match_stable_sort(built):
                 ev.append(i)
     ek = np.array(ek, np.uint64)
     ev = np.array(ev, np.uint32)
-    order = np.argsort(ek, kind="stable")
-    np.testing.assert_array_equal(keys.astype(np.uint64), ek[order])
+    order = np.argsort(ek, kind="stable")  # (tile, dkey), ties by splat index
+    np.testing.assert_array_equal(keys.astype(np.uint64), ek[order] >> np.uint64(15))  # tile id
     np.testing.assert_array_equal(vals, ev[order])
 
 
