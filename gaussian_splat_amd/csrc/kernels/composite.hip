@@ -1,15 +1,18 @@
 // composite.hip — per-tile front-to-back alpha composite.
 //
 // One 256-lane workgroup per 16x16 tile, one pixel per lane; wave w owns the
-// 16x4 pixel strip of rows 4w..4w+3.  The tile's depth-sorted splat list is
-// streamed through LDS in batches of 256 records (each lane gathers one 48-B
-// record by splat id).  Per batch every wave compacts, with one ballot per 64
-// records, the list of splats whose conservative pixel rect overlaps its
-// strip, then walks only that list: coverage (K6 closed
+// 8x8 quadrant (w & 1, w >> 1) of the tile.  The tile's depth-sorted splat
+// list is streamed through LDS in batches of 256 records (each lane gathers
+// one 48-B record by splat id).  Per batch every wave compacts, 64 records per
+// ballot, the splats whose support can reach its quadrant: the pixel rect
+// must overlap it AND the gaussian ellipse q <= 2 ln 100 must intersect the
+// parallelogram the quadrant's pixel centres map to in (u, v) space (an exact
+// point-to-parallelogram distance with a relative safety margin, so the test
+// is conservative).  The wave then walks only that list: coverage (K6 closed
 // form), gaussian + 0.01 cutoff (F1, tile.metal:191-197) and the composite
 // (A1, tile.metal:251-266; or the live 50-layer rule, 50layer.metal:208-222).
 // The per-pixel body is branch-free (a non-covering splat contributes an
-// exact zero), a wave leaves the batch as soon as all 64 of its pixels are
+// exact zero), a wave leaves the batch once all 64 of its pixels are
 // saturated, and the workgroup stops fetching once all 256 are.
 // Tiles are dealt to workgroups XCD-aware: consecutive tiles of a row share
 // most of their splats, so they are placed on one XCD's L2.
@@ -17,6 +20,35 @@
 #include "gs_wave.h"
 
 namespace gs {
+
+// Can the support of the splat (record a = (cx, cy, ax, ay), b = (bx, by, ..))
+// reach any pixel centre of the 8x8 quadrant with top-left pixel (X0, Y0)?
+// Pixel centre p maps to (u, v) = (d.A, d.B), d = (px+0.5-cx, cy-(py+0.5));
+// the quadrant maps to the parallelogram p0 + s gu + t gv, s, t in [0, 1].
+__device__ __forceinline__ bool ellipse_reaches_quadrant(const float4& a, const float4& b, float X0, float Y0) {
+    const float dx0 = (X0 + 0.5f) - a.x, dy0 = a.y - (Y0 + 0.5f);
+    const float pu = dx0 * a.z + dy0 * a.w, pv = dx0 * b.x + dy0 * b.y;  // p0
+    const float gu_u = 7.0f * a.z, gu_v = 7.0f * b.x;                     // +7 px in x
+    const float gv_u = -7.0f * a.w, gv_v = -7.0f * b.y;                   // +7 px in y (dy decreases)
+    // origin inside the parallelogram?
+    const float det = gu_u * gv_v - gu_v * gv_u;
+    const float s = (gv_u * pv - gv_v * pu) / det;  // solves p0 + s gu + t gv = 0
+    const float t = (gu_v * pu - gu_u * pv) / det;
+    const float tol = 1e-3f;
+    bool hit = s >= -tol && s <= 1.0f + tol && t >= -tol && t <= 1.0f + tol;
+    // squared distance from the origin to each edge segment
+    auto seg = [](float px, float py, float gx, float gy) {
+        const float gg = gx * gx + gy * gy;
+        float k = -(px * gx + py * gy) / gg;
+        k = fminf(fmaxf(k, 0.0f), 1.0f);
+        const float x = px + k * gx, y = py + k * gy;
+        return x * x + y * y;
+    };
+    const float m = fminf(fminf(seg(pu, pv, gu_u, gu_v), seg(pu, pv, gv_u, gv_v)),
+                          fminf(seg(pu + gv_u, pv + gv_v, gu_u, gu_v), seg(pu + gu_u, pv + gu_v, gv_u, gv_v)));
+    hit = hit || m <= kQMax * 1.001f + 1e-3f;
+    return hit || !(det == det);  // NaN guard: keep
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_t nwg) {
@@ -26,8 +58,8 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
     // residue class a contiguous run of tiles (cdna_hip_programming.md §5, T1).
     const uint32_t orig = blockIdx.x;
-    const uint32_t xcd = orig & 7u, q = nwg >> 3, r = nwg & 7u;
-    const uint32_t wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
+    const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
 
     // Grid covers only the owned tile rows: ty = row_rem + k * row_mod.
     const int owned_row = (int)wg / a.tiles_x;
@@ -38,14 +70,14 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     const int tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
-    const int px = tx * kTile + (tid & 15);
-    const int py = ty * kTile + (tid >> 4);
+    // this wave's quadrant: pixels [qx0, qx0+7] x [qy0, qy0+7]
+    const uint32_t qx0 = (uint32_t)(tx * kTile) + (wave & 1u) * 8u;
+    const uint32_t qy0 = (uint32_t)(ty * kTile) + (wave >> 1) * 8u;
+    const int px = (int)qx0 + (int)(lane & 7u);
+    const int py = (int)qy0 + (int)(lane >> 3);
     const bool inside = px < width && py < height;
     const float fx = (float)px + 0.5f;
     const float fy = (float)py + 0.5f;
-    // this wave's strip: rows [wy0, wy0+3], tile columns [wx0, wx0+15]
-    const uint32_t wy0 = (uint32_t)(ty * kTile) + wave * 4u, wy1 = wy0 + 3u;
-    const uint32_t wx0 = (uint32_t)(tx * kTile), wx1 = wx0 + 15u;
 
     const uint2 rg = a.ranges[tile];
     float A = 0.0f;  // tile rule: accumulated alpha
@@ -53,6 +85,36 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     bool done = !inside;
     bool any = false;
+
+    auto body = [&](uint32_t k) {
+        const float4 aa = s0[k];
+        const float4 bb = s1[k];
+        const float4 cc = s2[k];
+        const float dx = fx - aa.x;
+        const float dy = aa.y - fy;
+        const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
+        const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
+        const float qq = __builtin_fmaf(v, v, u * u);
+        const bool in = !done && fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+        const float alpha = bb.z * gs_gauss(qq);
+        any |= in;
+        if constexpr (MODE == 0) {
+            // out-of-support lanes add an exact zero: bit-identical to skipping
+            const float sa = in ? alpha * (1.0f - A) : 0.0f;
+            C0 = __builtin_fmaf(bb.w, sa, C0);
+            C1 = __builtin_fmaf(cc.x, sa, C1);
+            C2 = __builtin_fmaf(cc.y, sa, C2);
+            A = A + sa;
+            done = done || A >= kSat;
+        } else {
+            const float tw = in ? T : 0.0f;
+            C0 = __builtin_fmaf(bb.w, tw, C0);
+            C1 = __builtin_fmaf(cc.x, tw, C1);
+            C2 = __builtin_fmaf(cc.y, tw, C2);
+            T = in ? T * (1.0f - alpha) : T;
+            done = done || T < kTMin;
+        }
+    };
 
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
         if (__syncthreads_count(!done) == 0) break;
@@ -66,52 +128,33 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         }
         __syncthreads();
         const uint32_t cnt = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
-        // wave-level compaction of the splats overlapping this strip (index order kept)
+        // wave-level compaction of the splats reaching this quadrant (index order kept)
         uint32_t nl = 0;
-        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            bool hit = false;
-            if (k < cnt) {
-                const float4 c = s2[k];
-                const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
-                hit = !((hi >> 16) < wy0 || (lo >> 16) > wy1 || (hi & 0xFFFFu) < wx0 || (lo & 0xFFFFu) > wx1);
+        if (__ballot(!done) != 0) {
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                bool hit = false;
+                if (k < cnt) {
+                    const float4 c = s2[k];
+                    const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+                    hit = !((hi >> 16) < qy0 || (lo >> 16) > qy0 + 7u || (hi & 0xFFFFu) < qx0 ||
+                            (lo & 0xFFFFu) > qx0 + 7u);
+                    if (hit) hit = ellipse_reaches_quadrant(s0[k], s1[k], (float)qx0, (float)qy0);
+                }
+                const uint64_t m = __ballot(hit);
+                if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
+                nl += (uint32_t)__popcll(m);
             }
-            const uint64_t m = __ballot(hit);
-            if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
-            nl += (uint32_t)__popcll(m);
         }
         // (wlist[wave] is only touched by this wave: DS ops of one wave are ordered)
-        for (uint32_t i = 0; i < nl; ++i) {
+        uint32_t i = 0;
+        for (; i + 1 < nl; i += 2) {
             if (__ballot(!done) == 0) break;
-            const uint32_t k = wlist[wave][i];
-            const float4 aa = s0[k];
-            const float4 bb = s1[k];
-            const float4 cc = s2[k];
-            const float dx = fx - aa.x;
-            const float dy = aa.y - fy;
-            const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
-            const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
-            const float qq = __builtin_fmaf(v, v, u * u);
-            const bool in = !done && fabsf(u) <= 3.0f && fabsf(v) <= 3.0f && qq <= kQMax;
-            const float alpha = bb.z * gs_exp(-0.5f * qq);
-            any |= in;
-            if constexpr (MODE == 0) {
-                // out-of-support lanes add an exact zero: bit-identical to skipping
-                const float sa = in ? alpha * (1.0f - A) : 0.0f;
-                C0 = __builtin_fmaf(bb.w, sa, C0);
-                C1 = __builtin_fmaf(cc.x, sa, C1);
-                C2 = __builtin_fmaf(cc.y, sa, C2);
-                A = A + sa;
-                done = done || A >= kSat;
-            } else {
-                const float tw = in ? T : 0.0f;
-                C0 = __builtin_fmaf(bb.w, tw, C0);
-                C1 = __builtin_fmaf(cc.x, tw, C1);
-                C2 = __builtin_fmaf(cc.y, tw, C2);
-                T = in ? T * (1.0f - alpha) : T;
-                done = done || T < kTMin;
-            }
+            const uint32_t k0 = wlist[wave][i], k1 = wlist[wave][i + 1];
+            body(k0);
+            body(k1);
         }
+        if (i < nl && __ballot(!done) != 0) body(wlist[wave][i]);
     }
     if (inside) {
         float4 o;

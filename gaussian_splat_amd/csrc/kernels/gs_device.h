@@ -53,10 +53,8 @@ __device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, fl
     return __builtin_fmaf(a2, b2, __builtin_fmaf(a1, b1, a0 * b0));
 }
 
-// exp(x), x in [-4.61, 0]: 2^(x log2 e) by rint + degree-6 fma chain + ldexp.
-// Same op sequence as oracle ora_expf.
-__device__ __forceinline__ float gs_exp(float x) {
-    float t = x * 1.44269504088896341f;
+// 2^t by rint + degree-6 fma chain + ldexp (oracle ora_exp2_poly, op for op).
+__device__ __forceinline__ float gs_exp2_poly(float t) {
     float n = __builtin_rintf(t);
     float f = t - n;
     float p = 1.5403530393381606e-4f;
@@ -68,6 +66,9 @@ __device__ __forceinline__ float gs_exp(float x) {
     p = __builtin_fmaf(p, f, 1.0f);
     return __builtin_ldexpf(p, (int)n);
 }
+
+// F1 gaussian exp(-q/2) = 2^(q * -log2(e)/2) (oracle ora_gauss).
+__device__ __forceinline__ float gs_gauss(float q) { return gs_exp2_poly(q * -0.72134752044448170f); }
 
 // IEEE half bits, round to nearest even (v_cvt_f16_f32).
 __device__ __forceinline__ uint32_t half_bits(float f) {

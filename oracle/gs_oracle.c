@@ -63,13 +63,9 @@ uint16_t ora_f32_to_f16_bits(float f) {
     return (uint16_t)(sign | h);
 }
 
-/* exp(x) for x in [-4.61, 0] by 2^(x log2 e) with a degree-6 polynomial.
- * Defined by op sequence (rint, fmaf chain, ldexp) so the GPU reproduces it
- * bit for bit; |rel err| < 4e-7 (tile.metal:191 evaluates exp in relaxed
- * math and stores alpha as half, so this is far inside the reference's own
- * precision). */
-float ora_expf(float x) {
-    float t = x * 1.44269504088896341f;
+/* 2^t for t in [-7, 0]: rint + degree-6 polynomial + ldexp.  Defined by op
+ * sequence (rint, fmaf chain, ldexp) so the GPU reproduces it bit for bit. */
+static float ora_exp2_poly(float t) {
     float n = rintf(t);
     float f = t - n;
     float p = 1.5403530393381606e-4f;
@@ -81,6 +77,15 @@ float ora_expf(float x) {
     p = fmaf(p, f, 1.0f);
     return ldexpf(p, (int)n);
 }
+
+/* exp(x) = 2^(x log2 e); |rel err| < 5e-7 on [-4.7, 0]. */
+float ora_expf(float x) { return ora_exp2_poly(x * 1.44269504088896341f); }
+
+/* The F1 gaussian exp(-q/2) (tile.metal:191) as 2^(q * (-log2(e)/2)): one
+ * rounding before the polynomial.  |rel err| < 5e-7 for q in [0, 9.22];
+ * tile.metal evaluates exp in relaxed math and stores alpha as half, so this
+ * is far inside the reference's own precision. */
+float ora_gauss(float q) { return ora_exp2_poly(q * -0.72134752044448170f); }
 
 /* ------------------------------------------------------------------------ */
 /* I1: PLY loader restatement (src/ply_loader.cpp)                           */
@@ -583,7 +588,7 @@ static float frag_alpha(const ora_record *r, int px, int py) {
     if (!(fabsf(u) <= 3.0f && fabsf(v) <= 3.0f)) return -1.0f; /* K6 quad coverage */
     float q = fmaf(v, v, u * u);
     if (!(q <= ORA_QMAX)) return -1.0f; /* g < 0.01 discard, tile.metal:193 */
-    return r->opacity * ora_expf(-0.5f * q); /* tile.metal:197 */
+    return r->opacity * ora_gauss(q); /* tile.metal:197 */
 }
 
 typedef struct {

@@ -141,6 +141,7 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
 /* Helpers exposed for tests. */
 uint16_t ora_f32_to_f16_bits(float f);
 float ora_expf(float x);
+float ora_gauss(float q); /* exp(-q/2) as used by F1 */
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,8 @@ def lib() -> C.CDLL:
         L.ora_f32_to_f16_bits.restype = C.c_uint16
         L.ora_expf.argtypes = [C.c_float]
         L.ora_expf.restype = C.c_float
+        L.ora_gauss.argtypes = [C.c_float]
+        L.ora_gauss.restype = C.c_float
         _lib = L
     return _lib
 
@@ -180,6 +182,10 @@ def f16_bits(x: float) -> int:
 
 def expf(x: float) -> float:
     return float(lib().ora_expf(float(x)))
+
+
+def gauss(q: float) -> float:
+    return float(lib().ora_gauss(float(q)))
 
 
 # ---- oracle/_ref: the reference's own loader, compiled from /root/reference ----

@@ -111,6 +111,10 @@ def test_expf_accuracy():
     rel = np.abs(got / np.exp(xs.astype(np.float64)) - 1)
     assert rel.max() < 5e-7
     assert O.expf(0.0) == 1.0
+    qs = np.linspace(0.0, 9.2104, 20001, dtype=np.float32)
+    g = np.array([O.gauss(float(q)) for q in qs], np.float64)
+    assert np.abs(g / np.exp(-0.5 * qs.astype(np.float64)) - 1).max() < 5e-7
+    assert O.gauss(0.0) == 1.0
 
 
 def test_oracle_render_invariants():
