@@ -189,8 +189,8 @@ gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
     u.campos[3] = 0.0f;
     u.width = W;
     u.height = H;
-    u.tiles_x = (W + gs::kTile - 1) / gs::kTile;
-    u.tiles_y = (H + gs::kTile - 1) / gs::kTile;
+    u.tiles_x = (W + gs::kBin - 1) / gs::kBin;  // binning granularity (32x32 bins)
+    u.tiles_y = (H + gs::kBin - 1) / gs::kBin;
     return u;
 }
 

@@ -3,11 +3,12 @@
 // Depth-first binning: splats are first sorted by their 15-bit depth key
 // (stable, so equal half depths keep index = arrival order,
 // shaders/gaussian_splat_tile.metal:244), then every splat, visited in that
-// order, emits one (tile, splat index) pair per tile of its conservative
-// pixel rect.  A stable sort of the pairs by tile id alone then yields each
-// tile's list in S1 order: 2 digit passes over P (13 tile bits at 1080p)
-// instead of 4 over a 28-bit (tile, depth) key.
-// tile_ranges: boundary detection on the tile-sorted keys -> [start, end).
+// order, emits one (bin, splat index) pair per 32x32 bin of its conservative
+// pixel rect.  A stable sort of the pairs by bin id alone then yields each
+// bin's list in S1 order: 2 digit passes over P (11 bin bits at 1080p)
+// instead of 4 over a 28-bit (tile, depth) key, and ~half the pairs of
+// 16x16 binning.
+// tile_ranges: boundary detection on the bin-sorted keys -> [start, end).
 #include "gs_kernels.h"
 
 namespace gs {
@@ -25,8 +26,8 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
     if (x1 < x0) return;  // culled
     const uint32_t i = order[j];
-    const uint32_t tx0 = x0 >> 4, ty0 = (lo >> 16) >> 4;
-    const uint32_t tx1 = x1 >> 4, ty1 = (hi >> 16) >> 4;
+    const uint32_t tx0 = x0 >> kBinShift, ty0 = (lo >> 16) >> kBinShift;
+    const uint32_t tx1 = x1 >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     uint32_t off = offsets[j];
     for (uint32_t ty = first_owned_row(ty0, world, rank); ty <= ty1; ty += world) {
         for (uint32_t tx = tx0; tx <= tx1; ++tx) {

@@ -1,21 +1,24 @@
 // composite.hip — per-tile front-to-back alpha composite.
 //
-// One 256-lane workgroup per 16x16 tile, one pixel per lane; wave w owns the
-// 8x8 quadrant (w & 1, w >> 1) of the tile.  The tile's depth-sorted splat
-// list is streamed through LDS in batches of 256 records (each lane gathers
-// one 48-B record by splat id).  Per batch every wave compacts, 64 records per
-// ballot, the splats whose support can reach its quadrant: the pixel rect
-// must overlap it AND the gaussian ellipse q <= 2 ln 100 must intersect the
-// parallelogram the quadrant's pixel centres map to in (u, v) space (an exact
-// point-to-parallelogram distance with a relative safety margin, so the test
-// is conservative).  The wave then walks only that list: coverage (K6 closed
-// form), gaussian + 0.01 cutoff (F1, tile.metal:191-197) and the composite
+// One 256-lane workgroup per 16x16 tile, one pixel per lane, each wave an
+// 8x8 quadrant.  Lists are binned per 32x32 bin (2x2 tiles: 2.35 instead of
+// 4.38 pairs per splat, so sorting is cheaper); the four tiles of a bin are
+// consecutive workgroups on one XCD and share the bin list through its L2.
+// The list is streamed through LDS in batches of 256 (each lane gathers the
+// 16-B rect word of one record, and the other 32 B only when the pixel rect
+// reaches this tile).  Per batch each wave keeps the records whose rect
+// overlaps its quadrant AND whose gaussian ellipse q <= 2 ln 100 intersects
+// the parallelogram the quadrant's pixel centres map to in (u, v) space (an
+// exact point-to-parallelogram distance with a relative safety margin, so the
+// test is conservative).
+// Every wave compacts that list, 64 records per ballot, then walks only
+// it: coverage (K6 closed form), gaussian + 0.01 cutoff (F1, tile.metal:191-197) and the composite
 // (A1, tile.metal:251-266; or the live 50-layer rule, 50layer.metal:208-222).
 // The per-pixel body is branch-free (a non-covering splat contributes an
 // exact zero), a wave leaves the batch once all 64 of its pixels are
 // saturated, and the workgroup stops fetching once all 256 are.
-// Tiles are dealt to workgroups XCD-aware: consecutive tiles of a row share
-// most of their splats, so they are placed on one XCD's L2.
+// Bins are dealt to workgroups XCD-aware: consecutive bins of a row share
+// many of their splats, so they are placed on one XCD's L2.
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -31,15 +34,17 @@ __device__ __forceinline__ bool ellipse_reaches_quadrant(const float4& a, const 
     const float gu_u = 7.0f * a.z, gu_v = 7.0f * b.x;                     // +7 px in x
     const float gv_u = -7.0f * a.w, gv_v = -7.0f * b.y;                   // +7 px in y (dy decreases)
     // origin inside the parallelogram?
+    // approximate reciprocals are fine: both decisions carry a safety margin
     const float det = gu_u * gv_v - gu_v * gv_u;
-    const float s = (gv_u * pv - gv_v * pu) / det;  // solves p0 + s gu + t gv = 0
-    const float t = (gu_v * pu - gu_u * pv) / det;
+    const float idet = __builtin_amdgcn_rcpf(det);
+    const float s = (gv_u * pv - gv_v * pu) * idet;  // solves p0 + s gu + t gv = 0
+    const float t = (gu_v * pu - gu_u * pv) * idet;
     const float tol = 1e-3f;
     bool hit = s >= -tol && s <= 1.0f + tol && t >= -tol && t <= 1.0f + tol;
     // squared distance from the origin to each edge segment
     auto seg = [](float px, float py, float gx, float gy) {
         const float gg = gx * gx + gy * gy;
-        float k = -(px * gx + py * gy) / gg;
+        float k = -(px * gx + py * gy) * __builtin_amdgcn_rcpf(gg);
         k = fminf(fmaxf(k, 0.0f), 1.0f);
         const float x = px + k * gx, y = py + k * gy;
         return x * x + y * y;
@@ -61,25 +66,29 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
     const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
 
-    // Grid covers only the owned tile rows: ty = row_rem + k * row_mod.
-    const int owned_row = (int)wg / a.tiles_x;
-    const int tx = (int)wg - owned_row * a.tiles_x;
-    const int ty = a.row_rem + owned_row * a.row_mod;
-    const int tile = ty * a.tiles_x + tx;
+    // Grid covers only the owned bin rows: by = row_rem + k * row_mod.  The
+    // four 16x16 tiles of a bin are consecutive workgroups (same XCD / L2).
+    const uint32_t per_row = 4u * (uint32_t)a.tiles_x;
+    const int owned_row = (int)(wg / per_row);
+    const uint32_t k4 = wg - (uint32_t)owned_row * per_row;
+    const int bx = (int)(k4 >> 2);
+    const int by = a.row_rem + owned_row * a.row_mod;
+    const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
     const int width = a.width, height = a.height;
     const int tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
     // this wave's quadrant: pixels [qx0, qx0+7] x [qy0, qy0+7]
-    const uint32_t qx0 = (uint32_t)(tx * kTile) + (wave & 1u) * 8u;
-    const uint32_t qy0 = (uint32_t)(ty * kTile) + (wave >> 1) * 8u;
+    const uint32_t tx0 = (uint32_t)(tx * kTile), ty0 = (uint32_t)(ty * kTile);
+    const uint32_t qx0 = tx0 + (wave & 1u) * 8u;
+    const uint32_t qy0 = ty0 + (wave >> 1) * 8u;
     const int px = (int)qx0 + (int)(lane & 7u);
     const int py = (int)qy0 + (int)(lane >> 3);
     const bool inside = px < width && py < height;
     const float fx = (float)px + 0.5f;
     const float fy = (float)py + 0.5f;
 
-    const uint2 rg = a.ranges[tile];
+    const uint2 rg = a.ranges[by * a.tiles_x + bx];
     float A = 0.0f;  // tile rule: accumulated alpha
     float T = 1.0f;  // live50 rule: transmittance
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -120,11 +129,19 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         if (__syncthreads_count(!done) == 0) break;
         const uint32_t j = b + tid;
         if (j < rg.y) {
+            // the bin list holds the splats of all four tiles: fetch the rect
+            // first and the geometry only for splats that reach this tile
             const uint32_t id = a.vals[j];
             const float4* rp = a.rec + (size_t)a.rec_stride * id;
-            s0[tid] = rp[0];
-            s1[tid] = rp[1];
-            s2[tid] = rp[2];
+            const float4 c = rp[2];
+            s2[tid] = c;
+            const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+            const bool hit = !((hi >> 16) < ty0 || (lo >> 16) > ty0 + (kTile - 1) || (hi & 0xFFFFu) < tx0 ||
+                               (lo & 0xFFFFu) > tx0 + (kTile - 1));
+            if (hit) {
+                s0[tid] = rp[0];
+                s1[tid] = rp[1];
+            }
         }
         __syncthreads();
         const uint32_t cnt = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
@@ -163,8 +180,8 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         } else {
             o = make_float4(C0, C1, C2, any ? 1.0f - T : 0.0f);
         }
-        // compact = owned tile rows stacked (multi-GPU band buffer)
-        const int orow = a.compact ? owned_row * kTile + (py - ty * kTile) : py;
+        // compact = owned bin rows stacked (multi-GPU band buffer)
+        const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
         a.out[(size_t)orow * width + px] = o;
     }
 }
@@ -172,12 +189,12 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st) {
     if (a.row_mod < 1 || a.row_rem < 0 || a.row_rem >= a.row_mod) return hipErrorInvalidValue;
     const int owned_rows = a.tiles_y > a.row_rem ? (a.tiles_y - a.row_rem + a.row_mod - 1) / a.row_mod : 0;
-    const uint32_t nwg = (uint32_t)(a.tiles_x * owned_rows);
+    const uint32_t nwg = (uint32_t)(4 * a.tiles_x * owned_rows);
     if (nwg == 0) return hipSuccess;
     if (mode == 0)
-        composite_kernel<0><<<nwg, 256, 0, st>>>(a, nwg);
+        composite_kernel<0><<<nwg, kTileThreads, 0, st>>>(a, nwg);
     else
-        composite_kernel<1><<<nwg, 256, 0, st>>>(a, nwg);
+        composite_kernel<1><<<nwg, kTileThreads, 0, st>>>(a, nwg);
     return hipGetLastError();
 }
 

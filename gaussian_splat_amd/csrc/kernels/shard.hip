@@ -1,9 +1,9 @@
 // shard.hip — multi-GPU exchange kernels.
 //
 // Scenes are sharded by splat index (rank r holds a contiguous index range).
-// Tiles are owned by rank (tile_row % world): every rank projects its shard,
-// then sends each visible splat's 64-B exchange record to the ranks owning a
-// tile row its rect touches.  Received records arrive in source-rank order,
+// 32-px bin rows are owned by rank (bin_row % world): every rank projects its
+// shard, then sends each visible splat's 64-B exchange record to the ranks
+// owning a bin row its rect touches.  Received records arrive in source-rank order,
 // i.e. in global index order, so the receiving rank's stable sort reproduces
 // the single-GPU per-tile order exactly (bit-identical composite).
 #include "gs_kernels.h"
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __rest
         uint32_t m = 0;
         if (i < n) {
             const uint32_t lo = rect_lo[i], hi = rect_hi[i];
-            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> 4, (hi >> 16) >> 4, world);
+            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> kBinShift, (hi >> 16) >> kBinShift, world);
         }
         if (i < n) dest_mask[i] = m;
         for (int d = 0; d < world; ++d) {

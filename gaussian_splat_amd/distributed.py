@@ -1,7 +1,8 @@
 """Multi-GPU rendering: splat-index shards, tile-row ownership, RCCL exchange.
 
 DESIGN.md §6.  One process per GPU.  Rank r holds a contiguous splat-index
-range of the scene and owns the 16x16 tile rows ty with ty % world == r.
+range of the scene and owns the 32-pixel bin rows by with by % world == r
+(a bin is 2x2 of the 16x16 tiles; the binning granularity of the pipeline).
 Per frame:
 
   1. gs_shard_project   project the local shard on the GPU and pack a 64-B
@@ -30,30 +31,26 @@ from . import _lib as L
 from .api import InstancedSplatRenderer, Options, Scene, _mat16
 from ._lib import check, lib
 
-TILE = 16
-
-
-def tiles(width: int, height: int) -> tuple[int, int]:
-    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+ROW = 32  # ownership unit: one 32-pixel bin row
 
 
 def band_rows(height: int, world: int) -> int:
     """Pixel rows of the (padded, equal-size) band buffer of every rank."""
-    ty = (height + TILE - 1) // TILE
-    return ((ty + world - 1) // world) * TILE
+    rows = (height + ROW - 1) // ROW
+    return ((rows + world - 1) // world) * ROW
 
 
 def assemble(bands, width: int, height: int, world: int):
-    """Interleave rank bands (tile row ty <- band[ty % world], row ty // world) into a frame."""
+    """Interleave rank bands (bin row r <- band[r % world], slot r // world) into a frame."""
     import torch
 
-    th = (height + TILE - 1) // TILE
-    frame = torch.zeros((th * TILE, width, 4), dtype=torch.float32, device=bands[0].device)
-    ft = frame.view(th, TILE, width, 4)
+    th = (height + ROW - 1) // ROW
+    frame = torch.zeros((th * ROW, width, 4), dtype=torch.float32, device=bands[0].device)
+    ft = frame.view(th, ROW, width, 4)
     for r, b in enumerate(bands):
         k = len(range(r, th, world))
         if k:
-            ft[r::world] = b.view(-1, TILE, width, 4)[:k]
+            ft[r::world] = b.view(-1, ROW, width, 4)[:k]
     return frame[:height]
 
 

@@ -17,6 +17,7 @@
 #endif
 
 #define TILE 16
+#define OWN_ROW 32 /* multi-GPU ownership unit: 32-px bin rows */
 /* 2*ln(100): exp(-q/2) < 0.01 <=> q > 2 ln 100 (tile.metal:191-195). */
 #define ORA_QMAX 9.21034037197618f
 /* 0.99 saturation (tile.metal:261), 0.01 transmittance (50layer.metal:219). */
@@ -679,7 +680,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
                  ((rec[i].rect_hi >> 16) / TILE - (rec[i].rect_lo >> 16) / TILE + 1);
         ORA_RECT(i, x0, y0, x1, y1)
         for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
-            if (ty % row_mod != row_rem) continue;
+            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) cnt[ty * TW + tx + 1]++;
         }
     }
@@ -692,7 +693,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
         if (!dkey[i] && !rec[i].rect_hi && !rec[i].opacity) continue;
         ORA_RECT(i, x0, y0, x1, y1)
         for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
-            if (ty % row_mod != row_rem) continue;
+            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) list[cur[ty * TW + tx]++] = (uint32_t)i;
         }
     }
@@ -712,7 +713,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
 #endif
         for (int t = 0; t < T; ++t) {
             int tx = t % TW, ty = t / TW;
-            if (ty % row_mod != row_rem) continue;
+            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
             int64_t b = cnt[t], e = cnt[t + 1], m = e - b;
             if ((size_t)m > kcap) {
                 kcap = (size_t)m;
@@ -728,7 +729,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
              * arrival (index) order. */
             if (cap == 0) qsort(ord, (size_t)m, sizeof(kv), kv_cmp);
             for (int py = ty * TILE; py < ty * TILE + TILE && py < H; ++py) {
-                int orow = compact ? (ty / row_mod) * TILE + (py - ty * TILE) : py;
+                int orow = compact ? ((py / OWN_ROW) / row_mod) * OWN_ROW + py % OWN_ROW : py;
                 for (int px = tx * TILE; px < tx * TILE + TILE && px < W; ++px) {
                     float *o = out + ((size_t)orow * W + px) * 4;
                     int c = 0;

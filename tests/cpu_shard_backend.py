@@ -25,8 +25,8 @@ class OracleShardBackend:
 
         rec, dk, nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
         vis = nt > 0
-        ty0 = (rec["rect_lo"] >> 16) >> 4
-        ty1 = (rec["rect_hi"] >> 16) >> 4
+        ty0 = (rec["rect_lo"] >> 16) >> 5  # 32-px bin rows
+        ty1 = (rec["rect_hi"] >> 16) >> 5
         w = self.world
         parts, counts = [], []
         for d in range(w):

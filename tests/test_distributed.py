@@ -66,14 +66,14 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode):
 def test_assemble_layout():
     import torch
     from gaussian_splat_amd.distributed import assemble, band_rows
-    w, h, world = 40, 70, 3  # 5 tile rows, uneven split 2/2/1
+    w, h, world = 40, 140, 3  # 5 bin rows of 32 px, uneven split 2/2/1
     frame = torch.arange(h * w * 4, dtype=torch.float32).view(h, w, 4)
     th = 5
     bands = []
     for r in range(world):
         b = torch.zeros(band_rows(h, world), w, 4)
         for k, ty in enumerate(range(r, th, world)):
-            rows = frame[ty * 16: min(h, ty * 16 + 16)]
-            b[k * 16: k * 16 + rows.shape[0]] = rows
+            rows = frame[ty * 32: min(h, ty * 32 + 32)]
+            b[k * 32: k * 32 + rows.shape[0]] = rows
         bands.append(b)
     torch.testing.assert_close(assemble(bands, w, h, world), frame, rtol=0, atol=0)

@@ -62,7 +62,11 @@ def test_render_config1_bitexact(built, default_cam_256):
     assert linf <= TOL
     assert nbit == 0, f"{nbit} channel values differ bitwise (L-inf {linf})"
     stats = r.last_stats()
-    assert stats["pairs"] == st["pairs"] and stats["visible"] <= stats["splats"]
+    rec, _, nt = O.project(sc, V, P, 256, 256)
+    lo, hi = rec["rect_lo"][nt > 0], rec["rect_hi"][nt > 0]
+    bins = ((((hi & 0xFFFF) >> 5) - ((lo & 0xFFFF) >> 5) + 1) * (((hi >> 16) >> 5) - ((lo >> 16) >> 5) + 1)).sum()
+    assert stats["pairs"] == bins  # (splat, 32x32 bin) pairs
+    assert st["pairs"] >= stats["pairs"]
 
 
 @pytest.mark.parametrize("sh,mode", [(0, "tile"), (3, "tile"), (0, "live50"), (3, "live50")])
@@ -100,18 +104,18 @@ def test_sorted_pairs_match_stable_sort(built):
     r.render_host(V, P, W, H)
     keys, vals = r.sorted_pairs()
     rec, dk, nt = O.project(sc, V, P, W, H)
-    tx = (W + 15) // 16
+    bx = (W + 31) // 32  # 32x32 binning bins
     ek, ev = [], []
     for i in np.nonzero(nt)[0]:
         lo, hi = int(rec["rect_lo"][i]), int(rec["rect_hi"][i])
-        for ty in range((lo >> 16) >> 4, ((hi >> 16) >> 4) + 1):
-            for t in range((lo & 0xFFFF) >> 4, ((hi & 0xFFFF) >> 4) + 1):
-                ek.append(((ty * tx + t) << 15) | int(dk[i]))
+        for by in range((lo >> 16) >> 5, ((hi >> 16) >> 5) + 1):
+            for b in range((lo & 0xFFFF) >> 5, ((hi & 0xFFFF) >> 5) + 1):
+                ek.append(((by * bx + b) << 15) | int(dk[i]))
                 ev.append(i)
     ek = np.array(ek, np.uint64)
     ev = np.array(ev, np.uint32)
-    order = np.argsort(ek, kind="stable")  # (tile, dkey), ties by splat index
-    np.testing.assert_array_equal(keys.astype(np.uint64), ek[order] >> np.uint64(15))  # tile id
+    order = np.argsort(ek, kind="stable")  # (bin, dkey), ties by splat index
+    np.testing.assert_array_equal(keys.astype(np.uint64), ek[order] >> np.uint64(15))  # bin id
     np.testing.assert_array_equal(vals, ev[order])
 
 
