@@ -226,6 +226,12 @@ gs_status ensure_frame_scratch(gs_handle* h) {
 
 void mark(gs_handle* h, int k, hipStream_t st) {
     if (h->opt.stage_timing && h->events) (void)hipEventRecord(h->ev[k], st);
+    // debugging aid: GS_DEBUG_SYNC=<bitmask of stages> finishes and reports them
+    static const long dbg = std::getenv("GS_DEBUG_SYNC") ? std::strtol(std::getenv("GS_DEBUG_SYNC"), nullptr, 0) : 0;
+    if (dbg & (1L << k)) {
+        const hipError_t e = hipStreamSynchronize(st);
+        std::fprintf(stderr, "[gsplat] stage %d done: %s\n", k, hipGetErrorString(e));
+    }
 }
 
 float elapsed(gs_handle* h, int a, int b) {

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
                 nl += (uint32_t)__popcll(m);
             }
         }
-        // (wlist[wave] is only touched by this wave: DS ops of one wave are ordered)
+        wave_lds_sync();  // wlist[wave] is only touched by this wave
         uint32_t i = 0;
         for (; i + 1 < nl; i += 2) {
             if (__ballot(!done) == 0) break;

@@ -34,7 +34,7 @@ hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* rang
                               hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
-constexpr int kSortTile = 8192;  // items per onesweep tile (512 lanes x 16)
+constexpr int kSortTile = 8192;  // items per sort tile (512 lanes x 16)
 constexpr int kSortBins = 256;   // 8-bit digits
 constexpr int kMaxSortPasses = 4;
 struct SortPlan {

@@ -1,39 +1,33 @@
 // radix_sort.hip — stable LSD radix sort of uint32 keys with NV uint32 value
-// arrays, onesweep style: one kernel per 8-bit digit pass.
+// arrays, reduce-then-scan per digit pass (no inter-workgroup waiting).
 //
 // Used twice per frame by the binning stage: splats by
 // 15-bit depth key carrying (index, rect_lo, rect_hi) — 2 passes over N — then
-// (tile, splat) pairs by tile id — 2 passes over P at 1080p.
+// (bin, splat) pairs by bin id — 2 passes over P at 1080p.
 //
-//   os_hist    one read of the keys -> per-block digit histograms of EVERY
-//              pass (LDS atomics), os_reduce sums them per digit (no global
-//              atomics), os_offsets scans each pass's 256 bins
-//   os_pass    per tile of 512 x IPT items: stable tile-local ranks (wave-private
-//              ballot match, no barrier in the ranking loop), publish the tile's
-//              digit counts, decoupled look-back for the exclusive prefix over
-//              earlier tiles, then coalesced write-out of each array staged
-//              through LDS.  (1 + NV) x 4 B read and written per item per pass.
+// Per pass (digit width <= 8 bits, D = 2^width digits):
+//   rts_count  per tile of 512 x IPT items: LDS digit histogram (wave-private
+//              copies) -> C[digit][tile]
+//   rts_scan   one workgroup per digit: exclusive scan of its row of C over the
+//              tiles (in place) + the digit's total
+//   rts_pass   per tile: digit starts = block scan of the D totals; stable
+//              tile-local ranks (wave-private ballot match); each array staged
+//              through LDS in tile-sorted order and written out as coalesced
+//              digit runs at start[d] + C[d][tile] + rank
 //
-// Inter-workgroup protocol (MI355X_MICROARCH.md §Workgroup dispatch, "R2"):
-// every look-back word is a self-describing 64-bit granule {flag:2 | count:62}
-// written by ONE agent-scope atomic store and read by agent-scope relaxed
-// atomic loads (sc1, never L1-cached); the data is the flag, so no fences are
-// needed.  Tiles are numbered by an atomic ticket (not blockIdx), so a tile
-// only ever waits on tiles already held by running workgroups; spins are
-// bounded (an error word is set instead of hanging).  All words are zeroed
-// by one hipMemsetAsync per sort.
+// Why not onesweep: a decoupled look-back reads status words written by
+// workgroups on other XCDs (agent-scope loads that miss the per-XCD L2), so
+// every look-back hop costs a trip to the fabric; measured on MI355X the
+// onesweep pass took 85-90 us where this pass takes 57-64 us plus ~20 us of
+// count+scan.  The count kernel re-reads the keys once per
+// pass (4 B/item), which is the price of having no cross-workgroup wait.
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
 namespace gs {
 
-constexpr int kOsThreads = 512;
-constexpr int kOsWaves = kOsThreads / 64;
-constexpr int kOsHistItems = 16384;
-constexpr uint64_t kFlagAgg = 1ull << 62;
-constexpr uint64_t kFlagPre = 2ull << 62;
-constexpr uint64_t kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr int kRsThreads = 512;
+constexpr int kRsWaves = kRsThreads / 64;
 
 static_assert(kSortBins == 256, "8-bit digits");
 
@@ -46,23 +40,23 @@ struct SortIO {
 };
 
 constexpr int ipt_for(int nv) { return nv == 1 ? 16 : 8; }
-constexpr uint32_t tile_items(int nv) { return (uint32_t)kOsThreads * ipt_for(nv); }
+constexpr uint32_t tile_items(int nv) { return (uint32_t)kRsThreads * ipt_for(nv); }
 
-template <typename T, int NW>
-__device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T* total) {
+// Exclusive scan over the kRsThreads-lane workgroup (LDS-only barriers).
+__device__ __forceinline__ uint32_t block512_exclusive_scan(uint32_t v, uint32_t* tmp, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    T inc = wave_inclusive_scan(v);
+    const uint32_t inc = wave_scan_dpp<false>(v);
     if (lane == 63) tmp[wave] = inc;
-    __syncthreads();
-    T base = 0, tot = 0;
+    block_lds_sync();
+    uint32_t base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        T x = tmp[w];
-        base += (uint32_t)w < wave ? x : T(0);
+    for (int w = 0; w < kRsWaves; ++w) {
+        const uint32_t x = tmp[w];
+        base += (uint32_t)w < wave ? x : 0u;
         tot += x;
     }
     *total = tot;
-    __syncthreads();
+    block_lds_sync();
     return base + inc - v;
 }
 
@@ -77,80 +71,85 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int digi
     return peers;
 }
 
-// Per-block digit histograms of every pass (plain LDS atomics, wave-private
-// copies), written as partials [block][pass*256 + digit]; os_offsets reduces
-// them.  No global atomics.
-__global__ __launch_bounds__(256) void os_hist_kernel(const uint32_t* __restrict__ keys, uint32_t n, SortPlan plan,
-                                                      uint32_t* __restrict__ partial) {
-    __shared__ uint32_t h[4][kMaxSortPasses * kSortBins];
-    for (int i = threadIdx.x; i < 4 * kMaxSortPasses * kSortBins; i += 256) (&h[0][0])[i] = 0;
+template <int NV>
+__global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                        uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles) {
+    constexpr uint32_t TILE = tile_items(NV);
+    __shared__ uint32_t h[kRsWaves][kSortBins];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t base = blockIdx.x * (uint32_t)kOsHistItems;
+    const uint32_t t0 = blockIdx.x * TILE;
 #pragma unroll 4
-    for (uint32_t k = 0; k < (uint32_t)kOsHistItems / 256; ++k) {
-        const uint32_t i = base + k * 256 + threadIdx.x;
-        if (i < n) {
-            const uint32_t key = keys[i];
-            for (int p = 0; p < plan.passes; ++p)
-                atomicAdd(&h[wave][p * kSortBins + ((key >> plan.shift[p]) & plan.mask[p])], 1u);
-        }
+    for (uint32_t k = 0; k < TILE / kRsThreads; ++k) {
+        const uint32_t idx = t0 + k * kRsThreads + tid;
+        if (idx < n) atomicAdd(&h[wave][(keys[idx] >> shift) & mask], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < plan.passes * kSortBins; i += 256)
-        partial[(size_t)i * gridDim.x + blockIdx.x] = h[0][i] + h[1][i] + h[2][i] + h[3][i];
-}
-
-// One workgroup per (pass, digit): sum its row of block partials.
-__global__ __launch_bounds__(256) void os_reduce_kernel(const uint32_t* __restrict__ partial, uint32_t nblocks,
-                                                        uint32_t* __restrict__ hist) {
-    __shared__ uint32_t tmp[4];
-    const uint32_t* row = partial + (size_t)blockIdx.x * nblocks;
-    uint32_t c = 0;
-    for (uint32_t b = threadIdx.x; b < nblocks; b += 256) c += row[b];
-    uint32_t t;
-    block256_exclusive_scan<uint32_t>(c, tmp, &t);
-    if (threadIdx.x == 0) hist[blockIdx.x] = t;
-}
-
-__global__ __launch_bounds__(256) void os_offsets_kernel(const uint32_t* __restrict__ hist, int passes,
-                                                         uint32_t* __restrict__ offs) {
-    __shared__ uint32_t tmp[4];
-    for (int p = 0; p < passes; ++p) {
-        uint32_t t;
-        offs[p * kSortBins + threadIdx.x] = block256_exclusive_scan<uint32_t>(hist[p * kSortBins + threadIdx.x], tmp, &t);
+    if (tid <= mask) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kRsWaves; ++w) c += h[w][tid];
+        C[(size_t)tid * ntiles + blockIdx.x] = c;
     }
+}
+
+__global__ __launch_bounds__(256) void rts_scan_kernel(uint32_t* __restrict__ C, uint32_t ntiles,
+                                                       uint32_t* __restrict__ totals) {
+    __shared__ uint32_t tmp[4];
+    uint32_t* row = C + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < ntiles; b0 += 256) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < ntiles ? row[i] : 0u;
+        uint32_t t;
+        const uint32_t ex = block256_exclusive_scan<uint32_t>(v, tmp, &t);
+        if (i < ntiles) row[i] = carry + ex;
+        carry += t;
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
 template <int NV>
-__global__ __launch_bounds__(512) void os_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
-                                                      int digit_bits, const uint32_t* __restrict__ offs,
-                                                      uint64_t* status, uint32_t* ctr, uint32_t* err) {
+__global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
+                                                       int digit_bits, const uint32_t* __restrict__ C,
+                                                       const uint32_t* __restrict__ totals, uint32_t ntiles) {
     constexpr int IPT = ipt_for(NV);
     constexpr uint32_t TILE = tile_items(NV);
     constexpr uint32_t WAVE_ITEMS = 64u * IPT;
-    __shared__ uint32_t wh[kOsWaves][kSortBins];  // wave-private running counts -> wave offsets
+    __shared__ uint32_t wh[kRsWaves][kSortBins];  // wave-private running counts -> wave offsets
     __shared__ uint32_t blk_start[kSortBins];     // tile-local start of each digit
     __shared__ uint32_t gbase[kSortBins];         // global start of this tile's digit run
     __shared__ uint32_t stage[TILE];
     __shared__ uint8_t sdig[TILE];                // digit of each staged slot
-    __shared__ uint32_t tmp[kOsWaves];
-    __shared__ uint32_t s_tile;
+    __shared__ uint32_t tmp[kRsWaves];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < kOsWaves * kSortBins; i += kOsThreads) (&wh[0][0])[i] = 0;
-    if (tid == 0) s_tile = atomicAdd(ctr, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = blockIdx.x;
+    for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&wh[0][0])[i] = 0;
+    // Keys and all value arrays are loaded up front so their latency hides
+    // behind the ranking.  Barriers here order LDS only: they never wait for
+    // this tile's outstanding global stores.
     const uint32_t base = tile * TILE + wave * WAVE_ITEMS;
-
-    uint32_t key[IPT], pos[IPT];
+    uint32_t key[IPT], pos[IPT], val[NV][IPT];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t idx = base + k * 64 + lane;
         key[k] = idx < n ? io.kin[idx] : 0u;
     }
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t idx = base + k * 64 + lane;
+            val[a][k] = idx < n ? (io.vin[a] ? io.vin[a][idx] : idx) : 0u;
+        }
+    }
+    // global start of every digit of this tile (independent of the ranking)
+    uint32_t all;
+    const uint32_t dstart = block512_exclusive_scan(tid <= mask ? totals[tid] : 0u, tmp, &all);
+    if (tid <= mask) gbase[tid] = dstart + C[(size_t)tid * ntiles + tile];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t idx = base + k * 64 + lane;
@@ -162,49 +161,20 @@ __global__ __launch_bounds__(512) void os_pass_kernel(SortIO<NV> io, uint32_t n,
         pos[k] = old + below;
         if (valid && below == 0) wh[wave][d] = old + (uint32_t)__popcll(peers);
     }
-    __syncthreads();
+    block_lds_sync();
     uint32_t c = 0;
     if (tid < kSortBins) {
 #pragma unroll
-        for (int w = 0; w < kOsWaves; ++w) {
+        for (int w = 0; w < kRsWaves; ++w) {
             const uint32_t x = wh[w][tid];
             wh[w][tid] = c;
             c += x;
         }
-        // publish this tile's count of digit tid as early as possible
-        __hip_atomic_store(&status[(size_t)tile * kSortBins + tid], (tile == 0 ? kFlagPre : kFlagAgg) | c,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint32_t tot;
-    const uint32_t ex = block_exclusive_scan<uint32_t, kOsWaves>(tid < kSortBins ? c : 0u, tmp, &tot);
-    if (tid < kSortBins) {
-        blk_start[tid] = ex;
-        uint64_t excl = 0;
-        if (tile > 0) {
-            int64_t t = (int64_t)tile - 1;
-            uint32_t spins = 0;
-            while (true) {
-                const uint64_t v = __hip_atomic_load(&status[(size_t)t * kSortBins + tid], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t f = v & ~kValMask;
-                if (f == 0) {
-                    if (++spins > kSpinLimit) {
-                        atomicOr(err, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += v & kValMask;
-                if (f == kFlagPre || t == 0) break;
-                --t;
-            }
-            __hip_atomic_store(&status[(size_t)tile * kSortBins + tid], kFlagPre | (excl + c), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        gbase[tid] = offs[tid] + (uint32_t)excl;
-    }
-    __syncthreads();
+    const uint32_t ex = block512_exclusive_scan(tid < kSortBins ? c : 0u, tmp, &tot);
+    if (tid < kSortBins) blk_start[tid] = ex;
+    block_lds_sync();
     const uint32_t t0 = tile * TILE;
     const uint32_t cnt = n - t0 < TILE ? n - t0 : TILE;
     // keys: stage in tile-local sorted order, remember digits, write out
@@ -218,10 +188,10 @@ __global__ __launch_bounds__(512) void os_pass_kernel(SortIO<NV> io, uint32_t n,
             sdig[pos[k]] = (uint8_t)d;
         }
     }
-    __syncthreads();
+    block_lds_sync();
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-        const uint32_t j = tid + k * kOsThreads;
+        const uint32_t j = tid + k * kRsThreads;
         if (j < cnt) {
             const uint32_t d = sdig[j];
             io.kout[gbase[d] + (j - blk_start[d])] = stage[j];
@@ -230,22 +200,16 @@ __global__ __launch_bounds__(512) void os_pass_kernel(SortIO<NV> io, uint32_t n,
     // values: same permutation
 #pragma unroll
     for (int a = 0; a < NV; ++a) {
-        uint32_t v[IPT];
+        block_lds_sync();
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t idx = base + k * 64 + lane;
-            v[k] = idx < n ? (io.vin[a] ? io.vin[a][idx] : idx) : 0u;
+            if (idx < n) stage[pos[k]] = val[a][k];
         }
-        __syncthreads();
+        block_lds_sync();
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
-            const uint32_t idx = base + k * 64 + lane;
-            if (idx < n) stage[pos[k]] = v[k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < IPT; ++k) {
-            const uint32_t j = tid + k * kOsThreads;
+            const uint32_t j = tid + k * kRsThreads;
             if (j < cnt) {
                 const uint32_t d = sdig[j];
                 io.vout[a][gbase[d] + (j - blk_start[d])] = stage[j];
@@ -270,15 +234,9 @@ SortPlan make_sort_plan(int bits) {
     return p;
 }
 
-namespace {
-constexpr size_t kHeadWords = (size_t)kMaxSortPasses * (2 * kSortBins + 2) + 8;  // hist, offs, ctr, err
-}
-
 size_t radix_sort_scratch_words(uint32_t n) {
     const size_t tiles = (n + tile_items(3) - 1) / tile_items(3);  // the smaller tile bounds both
-    const size_t hblocks = (n + kOsHistItems - 1) / kOsHistItems;
-    return kHeadWords + 2 * (size_t)kMaxSortPasses * (tiles ? tiles : 1) * kSortBins +
-           (hblocks ? hblocks : 1) * kMaxSortPasses * kSortBins + 64;
+    return (size_t)(tiles ? tiles : 1) * kSortBins + kSortBins;
 }
 
 template <int NV>
@@ -289,19 +247,8 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     const SortPlan plan = make_sort_plan(bits);
     if (n == 0 || plan.passes == 0) return hipSuccess;
     const uint32_t tiles = (n + tile_items(NV) - 1) / tile_items(NV);
-    uint32_t* hist = scratch;                            // [passes][256]
-    uint32_t* offs = hist + kMaxSortPasses * kSortBins;  // [passes][256]
-    uint32_t* ctr = offs + kMaxSortPasses * kSortBins;   // [passes]
-    uint32_t* err = ctr + kMaxSortPasses;
-    uint64_t* status = reinterpret_cast<uint64_t*>(scratch + kHeadWords);
-    const size_t status_words = (size_t)plan.passes * tiles * kSortBins;
-    hipError_t e = hipMemsetAsync(scratch, 0, kHeadWords * 4 + status_words * 8, st);
-    if (e != hipSuccess) return e;
-    const uint32_t hblocks = (n + kOsHistItems - 1) / kOsHistItems;
-    uint32_t* partial = reinterpret_cast<uint32_t*>(status + (size_t)kMaxSortPasses * tiles * kSortBins);
-    os_hist_kernel<<<hblocks, 256, 0, st>>>(keys_in, n, plan, partial);
-    os_reduce_kernel<<<plan.passes * kSortBins, 256, 0, st>>>(partial, hblocks, hist);
-    os_offsets_kernel<<<1, 256, 0, st>>>(hist, plan.passes, offs);
+    uint32_t* C = scratch;                                   // [digit][tile]
+    uint32_t* totals = scratch + (size_t)tiles * kSortBins;  // [digit]
     // Pass 0 reads the caller's arrays; later passes ping-pong between
     // (keys, vals) and (tmp_keys, tmp_vals), arranged so the last pass lands
     // in (keys, vals) unless that would make pass 0 write what it reads.
@@ -316,9 +263,10 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     for (int p = 0; p < plan.passes; ++p) {
         io.kout = to_final ? keys : tmp_keys;
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
-        os_pass_kernel<NV><<<tiles, kOsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p],
-                                                         offs + p * kSortBins, status + (size_t)p * tiles * kSortBins,
-                                                         ctr + p, err);
+        rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles);
+        rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
+        rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
+                                                          totals, tiles);
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;

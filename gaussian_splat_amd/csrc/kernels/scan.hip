@@ -48,27 +48,43 @@ __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict
     if (threadIdx.x == 0) *total = carry;
 }
 
+// Down-sweep: counts are loaded striped (coalesced), transposed through LDS
+// so each lane scans kScanIpt consecutive items, and stored striped again
+// (lane-consecutive stores would be 64 partial-line writes per instruction).
+__device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }  // LDS bank spread
+
 __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n,
                                                         const uint64_t* __restrict__ partials,
                                                         uint32_t* __restrict__ offsets) {
     __shared__ uint32_t tmp[4];
-    const uint32_t base = blockIdx.x * kScanItems + threadIdx.x * kScanIpt;
+    __shared__ uint32_t st[kScanItems + kScanItems / 32];
+    const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t i = k * 256 + tid;
+        st[pad32(i)] = blk + i < n ? count_at(src, blk + i) : 0u;
+    }
+    __syncthreads();
     uint32_t v[kScanIpt];
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
-        uint32_t idx = base + k;
-        v[k] = idx < n ? count_at(src, idx) : 0u;
+        v[k] = st[pad32(tid * kScanIpt + k)];
         s += v[k];
     }
     uint32_t t;
-    uint32_t ex = block256_exclusive_scan<uint32_t>(s, tmp, &t);
+    const uint32_t ex = block256_exclusive_scan<uint32_t>(s, tmp, &t);  // (ends with a barrier)
     uint32_t run = (uint32_t)partials[blockIdx.x] + ex;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
-        uint32_t idx = base + k;
-        if (idx < n) offsets[idx] = run;
+        st[pad32(tid * kScanIpt + k)] = run;
         run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t i = k * 256 + tid;
+        if (blk + i < n) offsets[blk + i] = st[pad32(i)];
     }
 }
 

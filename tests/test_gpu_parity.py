@@ -95,10 +95,17 @@ def test_render_device_out_matches_host(built):
     np.testing.assert_array_equal(again.view(np.uint32), host.view(np.uint32))  # deterministic
 
 
-def test_sorted_pairs_match_stable_sort(built):
+@pytest.mark.parametrize("n,huge", [(40000, 0), (4096, 0), (6001, 300), (2048 * 3 + 1, 7)])
+def test_sorted_pairs_match_stable_sort(built, n, huge):
+    """Bin lists == a stable sort of the depth-ordered pairs by bin.  Covers
+    several sizes around block boundaries and splats blown up to cover much
+    of the frame."""
     from oracle import oracle_py as O
     W, H = 512, 384
-    sc = _scene(40000, 9, 0, aspect=W / H)
+    sc = _scene(n, 9, 0, aspect=W / H)
+    if huge:
+        idx = np.random.default_rng(n).choice(n, huge, replace=False)
+        sc.scale[idx] *= 40.0
     r = _renderer(sc)
     V, P = orbit_views(W, H, 1)[0]
     r.render_host(V, P, W, H)

@@ -1,4 +1,4 @@
-// sort_bench: our onesweep LSD sort vs rocPRIM (hipcub) on the frame's shapes.
+// sort_bench: our reduce-then-scan LSD sort vs rocPRIM (hipcub) on the frame's shapes.
 // Measurement tool only (cross-check + headroom); not part of libgsplat.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
         bool in_tmp;
         for (int it = 0; it < 10; ++it) CK(gs::launch_radix_sort(k, v, k2, v2, tk, tv, n, bits, scratch, &in_tmp, 0));
         CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
-        printf("onesweep n=%u bits=%d: %.1f us/sort\n", n, bits, ms * 100);
+        printf("ours n=%u bits=%d: %.1f us/sort\n", n, bits, ms * 100);
     }
     std::vector<uint32_t> ok(n); CK(hipMemcpy(ok.data(), k2, n * 4, hipMemcpyDeviceToHost));
     printf("sorted: %d\n", (int)std::is_sorted(ok.begin(), ok.end()));
