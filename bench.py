@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Benchmark: Msplats/s of the full frame (preprocess -> scan -> duplicate ->
-radix sort -> tile ranges -> composite [-> exchange -> gather]) on
+"""Benchmark: Msplats/s of the full frame (preprocess -> depth sort -> scan ->
+duplicate -> bin sort -> ranges -> composite [-> exchange -> gather]) on
 BASELINE.json's headline workload: 6M-splat scene @ 1920x1080, SH degree 3
 (configs[2]; a seeded synthetic scene with 3DGS statistics — no garden .ply
 exists offline).  Inputs are resident in HBM before the timed region.
@@ -11,6 +11,15 @@ exists offline).  Inputs are resident in HBM before the timed region.
 Multi-GPU is weak scaling: every rank holds its own 6M-splat shard of a
 (6M x N)-splat scene and owns 1/N of the tile rows; value = all splats / frame
 time (max over ranks).  Prints one JSON line on rank 0.
+
+At N=1 the line also carries
+  roofline      the slowest stage's algorithmic bytes / its HIP-event time,
+                and `traffic`: its HBM bytes per launch from two rocprofv3
+                PMC passes (FETCH_SIZE, WRITE_SIZE) run as child processes
+                (FETCH_SIZE doubled: gfx950 tallies 128-B reads at 64 B,
+                MI355X_MICROARCH.md §HBM); null if rocprofv3 is unavailable
+  cpu_baseline  the CPU oracle (oracle/gs_oracle.c, OpenMP) on the same
+                scene and camera, repeated for >= --cpu-seconds
 """
 from __future__ import annotations
 
@@ -42,7 +51,9 @@ def parse():
     ap.add_argument("--mode", default="tile")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="splats in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="splats in the CPU baseline sample (0 = all)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU baseline duration")
+    ap.add_argument("--traffic", type=int, default=1, help="measure roofline.traffic with rocprofv3 PMC (N=1)")
     ap.add_argument("--no-stage-timing", action="store_true")
     return ap.parse_args()
 
@@ -57,19 +68,69 @@ def stage_summary(stats_list):
     return out
 
 
-def cpu_baseline(scene, view, proj, w, h, sh, sample):
+def cpu_baseline(scene, view, proj, w, h, sh, sample, seconds):
     from oracle import oracle_py as O
 
-    n = min(sample, scene.n)
-    sub = scene.subset(slice(0, n))
+    n = scene.n if sample <= 0 else min(sample, scene.n)
+    sub = scene if n == scene.n else scene.subset(slice(0, n))
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     O.render(sub.subset(slice(0, min(n, 20000))), view, proj, w, h, sh_degree=sh, nthreads=threads)  # warm
-    t0 = time.perf_counter()
-    O.render(sub, view, proj, w, h, sh_degree=sh, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt / 1e6, "unit": "Msplats/s", "cores": threads, "kind": "port",
-            "sample": f"one {w}x{h} SH{sh} frame of the first {n} splats of the same scene "
-                      f"(oracle/gs_oracle.c, OpenMP), {dt:.2f} s"}
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        O.render(sub, view, proj, w, h, sh_degree=sh, nthreads=threads)
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or frames >= 50:
+            break
+    return {"value": round(n * frames / dt / 1e6, 3), "unit": "Msplats/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} x one {w}x{h} SH{sh} frame of {n} splats of the same scene and camera "
+                      f"(oracle/gs_oracle.c, OpenMP, {threads} threads), {dt:.1f} s"}
+
+
+STAGE_KERNEL = {"preprocess": "preprocess_kernel", "depth_sort": "rts_pass_kernel<3>", "scan": "scan_down_kernel",
+                "duplicate": "duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "tile_ranges_kernel",
+                "composite": "composite_kernel"}
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel`: two rocprofv3 --pmc passes over a
+    short run of this benchmark in child processes (counters and traces are
+    never combined; each pass its own process)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    bench = [sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--cpu-baseline", "0",
+             "--traffic", "0", "--no-stage-timing", "--splats", str(args.splats), "--width", str(args.width),
+             "--height", str(args.height), "--sh", str(args.sh), "--mode", args.mode, "--seed", str(args.seed)]
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    kb = {}
+    with tempfile.TemporaryDirectory(dir=env["TMPDIR"]) as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = Path(td) / ctr
+            cmd = [exe, "--kernel-trace", "--pmc", ctr, "-d", str(out), "-o", "run", "--output-format", "csv",
+                   "--"] + bench
+            try:
+                p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300, env=env,
+                                   cwd=str(ROOT))
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 {ctr} timed out"
+            if p.returncode != 0:
+                return None, f"rocprofv3 {ctr} exited {p.returncode}"
+            vals = []
+            for f in out.rglob("*counter_collection.csv"):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"no {ctr} samples for {kernel}"
+            kb[ctr] = sum(vals) / len(vals)
+    return 1024.0 * (2.0 * kb["FETCH_SIZE"] + kb["WRITE_SIZE"]), None
 
 
 def main():
@@ -156,8 +217,14 @@ def main():
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
         }
+        if world == 1 and rl is not None and args.traffic:
+            traffic, why = pmc_traffic(args, STAGE_KERNEL[rl["kernel"]])
+            rl["traffic"] = round(traffic) if traffic is not None else None
+            if why:
+                rl["traffic_note"] = why
         if world == 1 and args.cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(scene, view, proj, W, H, args.sh, args.cpu_sample)
+            line["cpu_baseline"] = cpu_baseline(scene, view, proj, W, H, args.sh, args.cpu_sample,
+                                                args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -214,9 +214,9 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
     GS_HIP(h->offsets.reserve(n * 4));
-    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 8));
-    GS_HIP(h->total.reserve(8));
-    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 8, hipHostMallocDefault));
+    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
+    GS_HIP(h->total.reserve(16));
+    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 16, hipHostMallocDefault));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
         h->events = true;
@@ -250,7 +250,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
     for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth, &h->offsets})
         GS_HIP(b->reserve(mm * 4));
-    GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 8));
+    GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)mm) * 4));
     // 1. splats by depth (descending zF == ascending dkey), ties by index,
     //    carrying (index, rect) so everything downstream reads sequentially
@@ -267,10 +267,11 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     // 2. tile counts in depth order -> pair offsets; P sizes the pair buffers
     GS_HIP(gs::launch_tile_count_scan(slo, shi, m, world, rank, h->offsets.as<uint32_t>(), h->partials.as<uint64_t>(),
                                       h->total.as<uint64_t>(), st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 8, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));
     mark(h, 3, st);
-    const uint64_t P = *h->host_total;
+    const uint64_t P = h->host_total[0];
+    h->stats.visible = (int64_t)h->host_total[1];
     if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,tile) pairs");
     const size_t p = (size_t)std::max<uint64_t>(P, 1);
     GS_HIP(h->keys.reserve(p * 4));

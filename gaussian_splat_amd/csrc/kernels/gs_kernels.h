@@ -18,7 +18,8 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
 // Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], world, rank) into
-// offsets[n]; *total (device u64) = sum.  partials: ceil(n / kScanItems) u64.
+// offsets[n]; total[0] (device u64) = sum, total[1] = items with a nonzero
+// count.  partials: 2 * ceil(n / kScanItems) u64.
 hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
                                   int rank, uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st);
 

@@ -17,19 +17,28 @@ __device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
     return rect_tile_count(c.lo[i], c.hi[i], c.world, c.rank);
 }
 
+// Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials) {
     __shared__ uint64_t tmp[4];
     const uint32_t base = blockIdx.x * kScanItems;
-    uint64_t s = 0;
+    uint64_t s = 0, vis = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         uint32_t i = base + k * 256 + threadIdx.x;
-        if (i < n) s += count_at(src, i);
+        if (i < n) {
+            const uint32_t c = count_at(src, i);
+            s += c;
+            vis += c > 0;
+        }
     }
-    uint64_t total;
+    uint64_t total, vtotal;
     block256_exclusive_scan<uint64_t>(s, tmp, &total);
-    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+    block256_exclusive_scan<uint64_t>(vis, tmp, &vtotal);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = total;
+        partials[gridDim.x + blockIdx.x] = vtotal;
+    }
 }
 
 // One workgroup scans all partials (<= a few thousand) exclusively in place.
@@ -45,7 +54,14 @@ __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict
         if (i < nb) partials[i] = carry + ex;
         carry += t;
     }
-    if (threadIdx.x == 0) *total = carry;
+    uint64_t vis = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) vis += partials[nb + b];
+    uint64_t vt;
+    block256_exclusive_scan<uint64_t>(vis, tmp, &vt);
+    if (threadIdx.x == 0) {
+        total[0] = carry;
+        total[1] = vt;
+    }
 }
 
 // Down-sweep: counts are loaded striped (coalesced), transposed through LDS
@@ -93,7 +109,7 @@ hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_
     const CountSrc src{rect_lo, rect_hi, (uint32_t)world, (uint32_t)rank};
     uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
-        return hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+        return hipMemsetAsync(total, 0, 2 * sizeof(uint64_t), st);
     }
     scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials);
     scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total);

@@ -67,6 +67,7 @@ def test_render_config1_bitexact(built, default_cam_256):
     bins = ((((hi & 0xFFFF) >> 5) - ((lo & 0xFFFF) >> 5) + 1) * (((hi >> 16) >> 5) - ((lo >> 16) >> 5) + 1)).sum()
     assert stats["pairs"] == bins  # (splat, 32x32 bin) pairs
     assert st["pairs"] >= stats["pairs"]
+    assert stats["visible"] == int((nt > 0).sum())
 
 
 @pytest.mark.parametrize("sh,mode", [(0, "tile"), (3, "tile"), (0, "live50"), (3, "live50")])
@@ -154,6 +155,7 @@ def test_empty_and_culled(built):
     img = r.render_host(V, P, 128, 128)
     assert not img.any()
     assert r.last_stats()["pairs"] == 0
+    assert r.last_stats()["visible"] == 0
     empty = S.Scene(np.zeros((0, 3)), np.zeros((0, 4)), np.zeros((0, 3)), np.zeros(0), np.zeros((0, 3)))
     r0 = _renderer(empty)
     assert r0.getPointCount() == 0
