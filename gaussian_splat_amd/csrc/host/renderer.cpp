@@ -329,10 +329,13 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     // Algorithmic bytes: what each stage must move at minimum.
     const int64_t Pi = (int64_t)P, dpass = gs::make_sort_plan(gs::kDepthBits).passes;
     s.bytes_preprocess = N * (bin + 48 + 8);
-    s.bytes_depth_sort = N * (4 + 16 * dpass);
+    // reduce-then-scan LSD: per pass the count kernel reads the keys (4 B)
+    // and the scatter moves key + values (read + write); the depth sort's
+    // first pass generates the index values instead of reading them
+    s.bytes_depth_sort = dpass > 0 ? N * (4 * dpass + 28 + 32 * (dpass - 1)) : 0;
     s.bytes_scan = N * 20;
     s.bytes_duplicate = N * 20 + Pi * 8;
-    s.bytes_sort = Pi * (4 + 16 * (int64_t)s.sort_passes);
+    s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
     s.bytes_ranges = Pi * 4 + T * 8;
     s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
     if (h->opt.stage_timing && h->events) {
