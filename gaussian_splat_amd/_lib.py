@@ -14,7 +14,8 @@ LIB_PATH = Path(__file__).resolve().parent / "libgsplat.so"
 
 class GsOptions(C.Structure):
     _fields_ = [("mode", C.c_int32), ("sh_degree", C.c_int32), ("crop", C.c_int32),
-                ("crop_radius", C.c_float), ("stage_timing", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("crop_radius", C.c_float), ("stage_timing", C.c_int32), ("cap", C.c_int32),
+                ("reserved", C.c_int32 * 6)]
 
 
 class GsSceneSoa(C.Structure):
@@ -51,7 +52,9 @@ SIGNATURES = {
     "gs_point_count": (C.c_int64, [_P]),
     "gs_destroy": (None, [_P]),
     "gs_set_mode": (C.c_int, [_P, C.c_int32]),
+    "gs_set_cap": (C.c_int, [_P, C.c_int32]),
     "gs_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
+    "gs_render_bgra8": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_last_stats": (C.c_int, [_P, C.POINTER(GsStats)]),
     "gs_project_host": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, _P, _P]),
     "gs_sorted_pairs_host": (C.c_int, [_P, _P, _P, C.c_int64, _I64P]),

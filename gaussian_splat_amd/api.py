@@ -48,6 +48,7 @@ class Options:
     crop: bool = True
     crop_radius: float = 5.0
     stage_timing: bool = False
+    cap: int = 0  # per-pixel fragment cap by arrival order (0 = none; 32 tile shader, 50 live shader)
 
     def to_c(self) -> GsOptions:
         o = GsOptions()
@@ -59,6 +60,9 @@ class Options:
         o.crop = int(bool(self.crop))
         o.crop_radius = float(self.crop_radius)
         o.stage_timing = int(bool(self.stage_timing))
+        if int(self.cap) < 0:
+            raise ValueError("cap must be >= 0")
+        o.cap = int(self.cap)
         return o
 
 
@@ -221,6 +225,11 @@ class InstancedSplatRenderer:
         check(lib().gs_set_mode(self._h, MODES[mode]), "gs_set_mode")
         self.options.mode = mode
 
+    def set_cap(self, cap: int):
+        """Per-pixel fragment cap by arrival order (0 = none)."""
+        check(lib().gs_set_cap(self._h, int(cap)), "gs_set_cap")
+        self.options.cap = int(cap)
+
     def render(self, view, proj, width: int, height: int, out=None, stream=None):
         """Render into `out` (torch float32 CUDA tensor (H, W, 4)); returns it."""
         import torch
@@ -232,6 +241,26 @@ class InstancedSplatRenderer:
             stream = torch.cuda.current_stream(out.device).cuda_stream
         check(lib().gs_render(self._h, _mat16(view), _mat16(proj), int(width), int(height), C.c_void_p(out.data_ptr()),
                               1, C.c_void_p(stream)), "gs_render")
+        return out
+
+    def render_bgra8(self, view, proj, width: int, height: int, out=None, stream=None):
+        """Render as BGRA8Unorm (the reference's drawable format) into `out`
+        (torch uint8 CUDA tensor (H, W, 4), bytes B, G, R, A); returns it."""
+        import torch
+
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.uint8, device=f"cuda:{self.device or 0}")
+        assert out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous() and out.numel() == width * height * 4
+        if stream is None:
+            stream = torch.cuda.current_stream(out.device).cuda_stream
+        check(lib().gs_render_bgra8(self._h, _mat16(view), _mat16(proj), int(width), int(height),
+                                    C.c_void_p(out.data_ptr()), 1, C.c_void_p(stream)), "gs_render_bgra8")
+        return out
+
+    def render_bgra8_host(self, view, proj, width: int, height: int) -> np.ndarray:
+        out = np.empty((height, width, 4), np.uint8)
+        check(lib().gs_render_bgra8(self._h, _mat16(view), _mat16(proj), int(width), int(height), out.ctypes.data,
+                                    0, None), "gs_render_bgra8")
         return out
 
     def render_host(self, view, proj, width: int, height: int) -> np.ndarray:

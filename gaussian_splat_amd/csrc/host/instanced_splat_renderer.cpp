@@ -32,6 +32,14 @@ void InstancedSplatRenderer::render(void* commandBuffer, void* drawableTexture, 
                         (int32_t)viewportHeight, static_cast<float*>(drawableTexture), 1, commandBuffer);
 }
 
+void InstancedSplatRenderer::renderBGRA8(void* commandBuffer, void* drawableTexture, const simd_float4x4& viewMatrix,
+                                         const simd_float4x4& projectionMatrix, float viewportWidth,
+                                         float viewportHeight) {
+    if (!handle_ || gs_point_count(handle_) == 0 || !drawableTexture) return;
+    status_ = gs_render_bgra8(handle_, viewMatrix.data(), projectionMatrix.data(), (int32_t)viewportWidth,
+                              (int32_t)viewportHeight, static_cast<uint8_t*>(drawableTexture), 1, commandBuffer);
+}
+
 int InstancedSplatRenderer::getPointCount() const { return (int)gs_point_count(handle_); }
 
 gs_stats InstancedSplatRenderer::lastStats() const {

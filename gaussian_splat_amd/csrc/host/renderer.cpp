@@ -77,7 +77,7 @@ struct gs_handle {
     bool initialized = false;
     DevBuf p0, p1, p2, p3, sh4, sh1;
     // per-frame scratch
-    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb;
+    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
@@ -93,7 +93,7 @@ struct gs_handle {
 
     ~gs_handle() {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
-                          &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
+                          &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi})
             b->release();
         if (host_total) (void)hipHostFree(host_total);
@@ -122,6 +122,7 @@ gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& op
     if (!sc || sc->n < 0 || (sc->n > 0 && (!sc->pos || !sc->rot || !sc->scale || !sc->opacity || !sc->color)))
         return fail(GS_ERR_INVALID_ARG, "gs_scene_soa: null array");
     if (opt.sh_degree < 0 || opt.sh_degree > 3) return fail(GS_ERR_INVALID_ARG, "sh_degree must be 0..3");
+    if (opt.cap < 0) return fail(GS_ERR_INVALID_ARG, "cap must be >= 0");
     if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
     if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
     h->opt = opt;
@@ -240,18 +241,91 @@ float elapsed(gs_handle* h, int a, int b) {
     return ms;
 }
 
+// Bin lists from m splats visited in `order` (nullptr = index order) with
+// rects (rect_lo, rect_hi) in that order: ordered scan of bin counts (P and
+// the visible count to host) -> duplicate -> stable sort by bin id ->
+// ranges.  Marks 3..6 when `timed`.
+gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
+                          const uint32_t* rect_hi, const gs::FrameUniforms& U, int world, int rank, bool timed,
+                          hipStream_t st, const uint32_t** vals_out, uint64_t* pairs) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, world, rank, h->offsets.as<uint32_t>(),
+                                      h->partials.as<uint64_t>(), h->total.as<uint64_t>(), st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    if (timed) mark(h, 3, st);
+    const uint64_t P = h->host_total[0];
+    h->stats.visible = (int64_t)h->host_total[1];
+    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
+    const size_t p = (size_t)std::max<uint64_t>(P, 1);
+    GS_HIP(h->keys.reserve(p * 4));
+    GS_HIP(h->vals.reserve(p * 4));
+    GS_HIP(h->tkeys.reserve(p * 4));
+    GS_HIP(h->tvals.reserve(p * 4));
+    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
+    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
+    // pairs (bin, splat) in visiting order
+    GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, world,
+                                rank, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    if (timed) mark(h, 4, st);
+    // stable sort by bin id only
+    const int bits = bits_for(T);
+    bool in_tmp = false;
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
+                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
+                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st));
+    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+    h->last_keys = sk;
+    h->last_vals = sv;
+    if (timed) mark(h, 5, st);
+    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
+    if (timed) mark(h, 6, st);
+    h->stats.sort_bits = bits;
+    h->stats.sort_passes = gs::make_sort_plan(bits).passes;
+    *vals_out = sv;
+    *pairs = P;
+    return GS_OK;
+}
+
 // Binning + sort + composite over m items (local splats, or received
-// exchange records): depth sort -> ordered scan of tile counts (P to host) ->
-// duplicate in depth order -> stable sort by tile -> ranges -> composite.
+// exchange records): depth sort -> bin lists in depth order -> composite.
+// With a fragment cap, per-pixel thresholds come first from index-ordered
+// bin lists (counted in the depth-sort stage time).
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
-                             int world, int rank, int compact, float4* out, hipStream_t st) {
-    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+                             int world, int rank, int compact, float4* out, uint32_t* out_bgra8, hipStream_t st) {
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
     for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth, &h->offsets})
         GS_HIP(b->reserve(mm * 4));
     GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)mm) * 4));
+    gs::CompositeArgs ca{};
+    ca.rec = rec;
+    ca.rec_stride = rec_stride;
+    ca.width = U.width;
+    ca.height = U.height;
+    ca.tiles_x = U.tiles_x;
+    ca.tiles_y = U.tiles_y;
+    ca.row_mod = world;
+    ca.row_rem = rank;
+    ca.compact = compact;
+    ca.out = out;
+    ca.out_bgra8 = out_bgra8;
+    ca.cap = h->opt.cap;
+    const uint32_t* vals = nullptr;
+    uint64_t P = 0;
+    if (ca.cap > 0) {
+        // 0. per-pixel cap thresholds from the lists in arrival (index) order
+        GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, world, rank, false, st, &vals, &P);
+        if (s != GS_OK) return s;
+        ca.vals = vals;
+        ca.ranges = h->ranges.as<uint2>();
+        ca.thr_out = h->thr.as<uint32_t>();
+        GS_HIP(gs::launch_cap_threshold(ca, st));
+        ca.thr = h->thr.as<uint32_t>();
+    }
     // 1. splats by depth (descending zF == ascending dkey), ties by index,
     //    carrying (index, rect) so everything downstream reads sequentially
     bool in_tmp = false;
@@ -264,56 +338,14 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* slo = in_tmp ? vtmp[1] : vout[1];
     const uint32_t* shi = in_tmp ? vtmp[2] : vout[2];
     mark(h, 2, st);
-    // 2. tile counts in depth order -> pair offsets; P sizes the pair buffers
-    GS_HIP(gs::launch_tile_count_scan(slo, shi, m, world, rank, h->offsets.as<uint32_t>(), h->partials.as<uint64_t>(),
-                                      h->total.as<uint64_t>(), st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
-    GS_HIP(hipStreamSynchronize(st));
-    mark(h, 3, st);
-    const uint64_t P = h->host_total[0];
-    h->stats.visible = (int64_t)h->host_total[1];
-    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,tile) pairs");
-    const size_t p = (size_t)std::max<uint64_t>(P, 1);
-    GS_HIP(h->keys.reserve(p * 4));
-    GS_HIP(h->vals.reserve(p * 4));
-    GS_HIP(h->tkeys.reserve(p * 4));
-    GS_HIP(h->tvals.reserve(p * 4));
-    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
-    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
-    // 3. pairs (tile, splat) in depth order
-    GS_HIP(gs::launch_duplicate(order, slo, shi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, world, rank,
-                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
-    mark(h, 4, st);
-    // 4. stable sort by tile id only
-    const int bits = bits_for(T);
-    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
-                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
-                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st));
-    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
-    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
-    h->last_keys = sk;
-    h->last_vals = sv;
-    mark(h, 5, st);
-    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
-    mark(h, 6, st);
-    gs::CompositeArgs ca;
-    ca.vals = sv;
+    // 2. bin lists in depth order
+    gs_status s = build_bin_lists(h, m, order, slo, shi, U, world, rank, true, st, &vals, &P);
+    if (s != GS_OK) return s;
+    ca.vals = vals;
     ca.ranges = h->ranges.as<uint2>();
-    ca.rec = rec;
-    ca.rec_stride = rec_stride;
-    ca.width = U.width;
-    ca.height = U.height;
-    ca.tiles_x = U.tiles_x;
-    ca.tiles_y = U.tiles_y;
-    ca.row_mod = world;
-    ca.row_rem = rank;
-    ca.compact = compact;
-    ca.out = out;
     GS_HIP(gs::launch_composite(ca, h->opt.mode, st));
     mark(h, 7, st);
     h->stats.pairs = (int64_t)P;
-    h->stats.sort_bits = bits;
-    h->stats.sort_passes = gs::make_sort_plan(bits).passes;
     return GS_OK;
 }
 
@@ -483,21 +515,30 @@ gs_status gs_set_mode(gs_handle* h, int32_t mode) {
     return GS_OK;
 }
 
-gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, float* out_rgba,
-                    int32_t out_is_device, void* stream) {
+gs_status gs_set_cap(gs_handle* h, int32_t cap) {
+    if (!h || cap < 0) return fail(GS_ERR_INVALID_ARG, "bad cap");
+    h->opt.cap = cap;
+    return GS_OK;
+}
+
+// One frame into a caller-owned framebuffer: fp32 RGBA (16 B/pixel) or, with
+// bgra8, packed BGRA8Unorm (4 B/pixel, converted inside the composite).
+static gs_status render_frame(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
+                              void* out_user, int32_t out_is_device, bool bgra8, void* stream) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if (!view || !proj || !out_rgba || W <= 0 || H <= 0 || W > 65535 || H > 65535)
+    if (!view || !proj || !out_user || W <= 0 || H <= 0 || W > 65535 || H > 65535)
         return fail(GS_ERR_INVALID_ARG, "gs_render: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
     const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     if (T == 0 || bits_for(T) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
-    float4* out = reinterpret_cast<float4*>(out_rgba);
+    const size_t bytes = (size_t)W * H * (bgra8 ? 4 : 16);
+    void* out = out_user;
     if (!out_is_device) {
-        GS_HIP(h->fb.reserve((size_t)W * H * 16));
-        out = h->fb.as<float4>();
+        GS_HIP(h->fb.reserve(bytes));
+        out = h->fb.ptr;
     }
     std::memset(&h->stats, 0, sizeof h->stats);
     mark(h, 0, st);
@@ -505,15 +546,28 @@ gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t 
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     mark(h, 1, st);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
-                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 1, 0, 0, out, st)) != GS_OK)
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 1, 0, 0,
+                                bgra8 ? nullptr : static_cast<float4*>(out),
+                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, st)) != GS_OK)
         return s;
     const uint64_t P = (uint64_t)h->stats.pairs;
     if (!out_is_device) {
-        GS_HIP(hipMemcpyAsync(out_rgba, out, (size_t)W * H * 16, hipMemcpyDeviceToHost, st));
+        GS_HIP(hipMemcpyAsync(out_user, out, bytes, hipMemcpyDeviceToHost, st));
         GS_HIP(hipStreamSynchronize(st));
     }
     fill_stats(h, P, U);
+    if (bgra8) h->stats.bytes_composite -= (int64_t)W * H * 12;
     return GS_OK;
+}
+
+gs_status gs_render(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, float* out_rgba,
+                    int32_t out_is_device, void* stream) {
+    return render_frame(h, view, proj, W, H, out_rgba, out_is_device, false, stream);
+}
+
+gs_status gs_render_bgra8(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
+                          uint8_t* out_bgra, int32_t out_is_device, void* stream) {
+    return render_frame(h, view, proj, W, H, out_bgra, out_is_device, true, stream);
 }
 
 gs_status gs_last_stats(const gs_handle* h, gs_stats* out) {
@@ -653,7 +707,7 @@ gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, 
                                   h->rrhi.as<uint32_t>(), st));
     if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                 h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, h->world, h->rank, 1,
-                                reinterpret_cast<float4*>(out_rgba), st)) != GS_OK)
+                                reinterpret_cast<float4*>(out_rgba), nullptr, st)) != GS_OK)
         return s;
     const uint64_t P = (uint64_t)h->stats.pairs;
     h->stats.pairs = (int64_t)P;

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     const uint32_t lo = rect_lo[j], hi = rect_hi[j];
     const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
     if (x1 < x0) return;  // culled
-    const uint32_t i = order[j];
+    const uint32_t i = order ? order[j] : j;
     const uint32_t tx0 = x0 >> kBinShift, ty0 = (lo >> 16) >> kBinShift;
     const uint32_t tx1 = x1 >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     uint32_t off = offsets[j];

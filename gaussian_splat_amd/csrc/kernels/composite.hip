@@ -55,9 +55,14 @@ __device__ __forceinline__ bool ellipse_reaches_quadrant(const float4& a, const 
     return hit || !(det == det);  // NaN guard: keep
 }
 
-template <int MODE>
+// MODE 0: tile rule, 1: live50 rule, 2: cap threshold pass (index-ordered
+// lists; per pixel the id of the a.cap-th covering fragment).  CAP: composite
+// only fragments with id <= thr[pixel] (the first a.cap in arrival order).
+template <int MODE, bool CAP>
 __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_t nwg) {
+    constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
     __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
+    __shared__ uint32_t sid[kIds ? kTileThreads : 1];
     __shared__ uint8_t wlist[4][kTileThreads];
 
     // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
@@ -94,6 +99,11 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     bool done = !inside;
     bool any = false;
+    uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
+    int cnt = 0;                 // MODE 2: covering fragments seen
+    if constexpr (CAP) {
+        if (inside) thr = a.thr[(size_t)py * width + px];
+    }
 
     auto body = [&](uint32_t k) {
         const float4 aa = s0[k];
@@ -104,24 +114,35 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
         const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
         const float qq = __builtin_fmaf(v, v, u * u);
-        const bool in = !done && fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
-        const float alpha = bb.z * gs_gauss(qq);
-        any |= in;
-        if constexpr (MODE == 0) {
-            // out-of-support lanes add an exact zero: bit-identical to skipping
-            const float sa = in ? alpha * (1.0f - A) : 0.0f;
-            C0 = __builtin_fmaf(bb.w, sa, C0);
-            C1 = __builtin_fmaf(cc.x, sa, C1);
-            C2 = __builtin_fmaf(cc.y, sa, C2);
-            A = A + sa;
-            done = done || A >= kSat;
+        bool in = !done && fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+        if constexpr (MODE == 2) {
+            // arrival order: the a.cap-th covering fragment fixes the threshold
+            cnt += in ? 1 : 0;
+            if (in && cnt == a.cap) {
+                thr = sid[k];
+                done = true;
+            }
+            return;
         } else {
-            const float tw = in ? T : 0.0f;
-            C0 = __builtin_fmaf(bb.w, tw, C0);
-            C1 = __builtin_fmaf(cc.x, tw, C1);
-            C2 = __builtin_fmaf(cc.y, tw, C2);
-            T = in ? T * (1.0f - alpha) : T;
-            done = done || T < kTMin;
+            if constexpr (CAP) in = in && sid[k] <= thr;
+            const float alpha = bb.z * gs_gauss(qq);
+            any |= in;
+            if constexpr (MODE == 0) {
+                // out-of-support lanes add an exact zero: bit-identical to skipping
+                const float sa = in ? alpha * (1.0f - A) : 0.0f;
+                C0 = __builtin_fmaf(bb.w, sa, C0);
+                C1 = __builtin_fmaf(cc.x, sa, C1);
+                C2 = __builtin_fmaf(cc.y, sa, C2);
+                A = A + sa;
+                done = done || A >= kSat;
+            } else {
+                const float tw = in ? T : 0.0f;
+                C0 = __builtin_fmaf(bb.w, tw, C0);
+                C1 = __builtin_fmaf(cc.x, tw, C1);
+                C2 = __builtin_fmaf(cc.y, tw, C2);
+                T = in ? T * (1.0f - alpha) : T;
+                done = done || T < kTMin;
+            }
         }
     };
 
@@ -135,6 +156,7 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
             const float4* rp = a.rec + (size_t)a.rec_stride * id;
             const float4 c = rp[2];
             s2[tid] = c;
+            if constexpr (kIds) sid[tid] = id;
             const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
             const bool hit = !((hi >> 16) < ty0 || (lo >> 16) > ty0 + (kTile - 1) || (hi & 0xFFFFu) < tx0 ||
                                (lo & 0xFFFFu) > tx0 + (kTile - 1));
@@ -144,14 +166,14 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
             }
         }
         __syncthreads();
-        const uint32_t cnt = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
+        const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
         // wave-level compaction of the splats reaching this quadrant (index order kept)
         uint32_t nl = 0;
         if (__ballot(!done) != 0) {
-            for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 bool hit = false;
-                if (k < cnt) {
+                if (k < cnt_b) {
                     const float4 c = s2[k];
                     const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
                     hit = !((hi >> 16) < qy0 || (lo >> 16) > qy0 + 7u || (hi & 0xFFFFu) < qx0 ||
@@ -173,7 +195,10 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         }
         if (i < nl && __ballot(!done) != 0) body(wlist[wave][i]);
     }
-    if (inside) {
+    if (!inside) return;
+    if constexpr (MODE == 2) {
+        a.thr_out[(size_t)py * width + px] = thr;
+    } else {
         float4 o;
         if constexpr (MODE == 0) {
             o = make_float4(C0, C1, C2, A);
@@ -182,20 +207,33 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         }
         // compact = owned bin rows stacked (multi-GPU band buffer)
         const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
-        a.out[(size_t)orow * width + px] = o;
+        if (a.out_bgra8)
+            a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
+        else
+            a.out[(size_t)orow * width + px] = o;
     }
 }
 
-hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st) {
+template <int MODE, bool CAP>
+static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st) {
     if (a.row_mod < 1 || a.row_rem < 0 || a.row_rem >= a.row_mod) return hipErrorInvalidValue;
     const int owned_rows = a.tiles_y > a.row_rem ? (a.tiles_y - a.row_rem + a.row_mod - 1) / a.row_mod : 0;
     const uint32_t nwg = (uint32_t)(4 * a.tiles_x * owned_rows);
     if (nwg == 0) return hipSuccess;
-    if (mode == 0)
-        composite_kernel<0><<<nwg, kTileThreads, 0, st>>>(a, nwg);
-    else
-        composite_kernel<1><<<nwg, kTileThreads, 0, st>>>(a, nwg);
+    composite_kernel<MODE, CAP><<<nwg, kTileThreads, 0, st>>>(a, nwg);
     return hipGetLastError();
+}
+
+hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st) {
+    const bool cap = a.cap > 0;
+    if (cap && !a.thr) return hipErrorInvalidValue;
+    if (mode == 0) return cap ? launch_mode<0, true>(a, st) : launch_mode<0, false>(a, st);
+    return cap ? launch_mode<1, true>(a, st) : launch_mode<1, false>(a, st);
+}
+
+hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {
+    if (a.cap <= 0 || !a.thr_out) return hipErrorInvalidValue;
+    return launch_mode<2, false>(a, st);
 }
 
 }  // namespace gs

@@ -101,4 +101,15 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, ui
     return f > ty1 ? 0u : ((ty1 - f) / world + 1u) * cols;
 }
 
+// fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to
+// nearest even (the Metal/Vulkan unorm conversion rule; parity unpinned: no
+// Metal runtime here), bytes B, G, R, A from low to high address.
+__host__ __device__ inline uint32_t unorm8(float x) {
+    x = x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f;  // NaN -> 0
+    return (uint32_t)__builtin_rintf(x * 255.0f);
+}
+__host__ __device__ inline uint32_t pack_bgra8(float r, float g, float b, float a) {
+    return unorm8(b) | (unorm8(g) << 8) | (unorm8(r) << 16) | (unorm8(a) << 24);
+}
+
 }  // namespace gs

@@ -25,8 +25,9 @@ hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_
 
 // ---- binning.hip -----------------------------------------------------------
 // Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
-// rect_hi[j]) emits (tile, order[j]) for each tile of its rect whose row is
-// owned (ty % world == rank), starting at offsets[j].
+// rect_hi[j]) emits (bin, order[j]) for each bin of its rect whose row is
+// owned (by % world == rank), starting at offsets[j].  order == nullptr
+// means the identity (pairs in index order).
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                             const uint32_t* offsets, uint32_t n, uint32_t tiles_x, int world, int rank,
                             uint32_t* keys, uint32_t* vals, hipStream_t st);
@@ -62,17 +63,28 @@ hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* va
 // ---- composite.hip ---------------------------------------------------------
 struct CompositeArgs {
     const uint32_t* vals;   // sorted splat ids (index into rec)
-    const uint2* ranges;    // [tiles] -> [start, end) into vals
+    const uint2* ranges;    // [bins] -> [start, end) into vals
     const float4* rec;      // records, rec_stride float4 apart (3 local, 4 exchange)
     int rec_stride;
-    int width, height, tiles_x, tiles_y;
-    int row_mod, row_rem;   // composite tile rows ty with ty % row_mod == row_rem
-    int compact;            // 1: write owned tile rows stacked (band buffer)
-    float4* out;
+    int width, height, tiles_x, tiles_y;  // frame and 32x32 bin grid
+    int row_mod, row_rem;   // composite bin rows by with by % row_mod == row_rem
+    int compact;            // 1: write owned bin rows stacked (band buffer)
+    float4* out;            // fp32 RGBA, or (when out_bgra8 is set) unused
+    uint32_t* out_bgra8;    // packed BGRA8Unorm (metal_renderer.mm:58), converted in-kernel
+    // per-pixel fragment cap (0 = none): thr[py * width + px] = splat id of the
+    // cap-th covering fragment in index (arrival) order, UINT32_MAX if fewer
+    int cap;
+    const uint32_t* thr;    // read by the capped composite
+    uint32_t* thr_out;      // written by launch_cap_threshold
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
-// break), 1 = live50 rule (T < 0.01 break).
+// break), 1 = live50 rule (T < 0.01 break); with a.cap > 0 only fragments
+// with id <= thr[pixel] are composited.
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st);
+// Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):
+// walks each pixel's covering fragments in arrival order and records the id
+// of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).
+hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 
 // ---- shard.hip (multi-GPU tile-row ownership) ------------------------------
 constexpr int kXRecFloat4 = 4;  // 64-B exchange record: 48-B record + dkey, global index

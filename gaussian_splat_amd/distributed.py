@@ -141,12 +141,12 @@ class ShardedRenderer:
 
 
 def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,
-                          mode: str = "tile", device: int = 0) -> np.ndarray:
+                          mode: str = "tile", device: int = 0, cap: int = 0) -> np.ndarray:
     """All `world` ranks in one process on one GPU, exchange by slicing —
     the same kernels and record protocol as the multi-process path."""
     import torch
 
-    opts = Options(mode=mode, sh_degree=sh_degree, crop=False)
+    opts = Options(mode=mode, sh_degree=sh_degree, crop=False, cap=cap)
     backends = []
     for r in range(world):
         b, e = shard_bounds(scene.n, world, r)

@@ -58,7 +58,9 @@ typedef struct gs_options {
     int32_t crop;          /* 1 = keep |x|,|y|,|z| < crop_radius (instanced_splat_renderer.mm:382-386) */
     float crop_radius;     /* 5.0 in the reference */
     int32_t stage_timing;  /* 1 = record HIP events around every kernel (gs_last_stats) */
-    int32_t reserved[7];
+    int32_t cap;           /* per-pixel fragment cap by arrival order, 0 = none (contract default);
+                              32 = gaussian_splat_tile.metal:7, 50 = gaussian_splat_50layer.metal:8 */
+    int32_t reserved[6];
 } gs_options;
 
 /* Scene as SoA host arrays (all float32, n splats).  Used by
@@ -106,12 +108,21 @@ gs_status gs_initialize(gs_handle *h, int32_t device_ordinal); /* uploads the sc
 int64_t gs_point_count(const gs_handle *h);
 void gs_destroy(gs_handle *h);
 gs_status gs_set_mode(gs_handle *h, int32_t mode);
+/* Per-pixel fragment cap (0 = none): keep the first `cap` covering fragments
+ * of each pixel in arrival (= splat index) order, as the reference's
+ * fixed-size per-pixel lists do (tile.metal:199-202, 50layer.metal:170). */
+gs_status gs_set_cap(gs_handle *h, int32_t cap);
 
 /* ---- frame (InstancedSplatRenderer::render) --------------------------- */
 /* out_rgba: width*height*4 float32, row-major, y down.  out_is_device = 1:
  * HBM pointer, async on `hip_stream`; 0: host pointer, the call syncs. */
 gs_status gs_render(gs_handle *h, const float view[16], const float proj[16], int32_t width,
                     int32_t height, float *out_rgba, int32_t out_is_device, void *hip_stream);
+/* Same frame, written as packed BGRA8Unorm (4 B/pixel, bytes B,G,R,A): the
+ * drawable format of metal_renderer.mm:58 / instanced_splat_renderer.mm:269-271,
+ * converted inside the composite (clamp [0,1], x255, round to nearest even). */
+gs_status gs_render_bgra8(gs_handle *h, const float view[16], const float proj[16], int32_t width,
+                          int32_t height, uint8_t *out_bgra, int32_t out_is_device, void *hip_stream);
 gs_status gs_last_stats(const gs_handle *h, gs_stats *out);
 
 /* ---- stage-level entry points (tests, multi-GPU orchestration) --------- */

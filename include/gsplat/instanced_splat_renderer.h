@@ -37,6 +37,11 @@ public:
 
     int getPointCount() const;
 
+    // Same, into a BGRA8Unorm drawable-format device buffer (width*height*4 B),
+    // the reference's drawable pixel format (metal_renderer.mm:58).
+    void renderBGRA8(void* commandBuffer, void* drawableTexture, const simd_float4x4& viewMatrix,
+                     const simd_float4x4& projectionMatrix, float viewportWidth, float viewportHeight);
+
     // Additions (not in the reference): status of the last call, frame stats.
     gs_status lastStatus() const { return status_; }
     gs_stats lastStats() const;

@@ -88,6 +88,24 @@ float ora_expf(float x) { return ora_exp2_poly(x * 1.44269504088896341f); }
  * is far inside the reference's own precision. */
 float ora_gauss(float q) { return ora_exp2_poly(q * -0.72134752044448170f); }
 
+static uint8_t ora_unorm8(float x) {
+    if (!(x > 0.0f)) return 0; /* also NaN */
+    if (x >= 1.0f) return 255;
+    float y = x * 255.0f;
+    float f = floorf(y), d = y - f; /* round half to even, explicitly */
+    if (d > 0.5f || (d == 0.5f && fmodf(f, 2.0f) != 0.0f)) f += 1.0f;
+    return (uint8_t)f;
+}
+
+void ora_to_bgra8(const float *rgba, int64_t npix, uint8_t *bgra) {
+    for (int64_t i = 0; i < npix; ++i) {
+        bgra[4 * i + 0] = ora_unorm8(rgba[4 * i + 2]);
+        bgra[4 * i + 1] = ora_unorm8(rgba[4 * i + 1]);
+        bgra[4 * i + 2] = ora_unorm8(rgba[4 * i + 0]);
+        bgra[4 * i + 3] = ora_unorm8(rgba[4 * i + 3]);
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* I1: PLY loader restatement (src/ply_loader.cpp)                           */
 /* ------------------------------------------------------------------------ */

@@ -142,6 +142,10 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
 uint16_t ora_f32_to_f16_bits(float f);
 float ora_expf(float x);
 float ora_gauss(float q); /* exp(-q/2) as used by F1 */
+/* fp32 RGBA -> BGRA8Unorm (metal_renderer.mm:58, instanced_splat_renderer.mm:269-271):
+ * per channel clamp to [0,1], x255, round half to even; bytes B,G,R,A.
+ * Parity unpinned (Metal's conversion cannot run here). */
+void ora_to_bgra8(const float *rgba, int64_t npix, uint8_t *bgra);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,8 @@ def lib() -> C.CDLL:
         L.ora_expf.restype = C.c_float
         L.ora_gauss.argtypes = [C.c_float]
         L.ora_gauss.restype = C.c_float
+        L.ora_to_bgra8.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+        L.ora_to_bgra8.restype = None
         _lib = L
     return _lib
 
@@ -186,6 +188,14 @@ def expf(x: float) -> float:
 
 def gauss(q: float) -> float:
     return float(lib().ora_gauss(float(q)))
+
+
+def to_bgra8(rgba: np.ndarray) -> np.ndarray:
+    """(H, W, 4) fp32 RGBA -> (H, W, 4) uint8 BGRA8Unorm."""
+    f = np.ascontiguousarray(rgba, dtype=np.float32)
+    out = np.empty(f.shape[:-1] + (4,), np.uint8)
+    lib().ora_to_bgra8(f.ctypes.data, f.size // 4, out.ctypes.data)
+    return out
 
 
 # ---- oracle/_ref: the reference's own loader, compiled from /root/reference ----

@@ -16,9 +16,9 @@ assert XREC.itemsize == 64
 class OracleShardBackend:
     xbytes = 64
 
-    def __init__(self, shard, rank, world, index_base, sh_degree=0, mode="tile"):
+    def __init__(self, shard, rank, world, index_base, sh_degree=0, mode="tile", cap=0):
         self.shard, self.rank, self.world, self.base = shard, rank, world, index_base
-        self.sh, self.mode = sh_degree, mode
+        self.sh, self.mode, self.cap = sh_degree, mode, cap
 
     def project(self, view, proj, width, height):
         import torch
@@ -52,5 +52,5 @@ class OracleShardBackend:
         # received order must be global index order (tie rule); check it
         assert np.all(np.diff(raw["gidx"].astype(np.int64)) > 0)
         band = O.composite_records(rec, raw["dkey"], width, height, row_mod=self.world, row_rem=self.rank,
-                                   compact=True, mode=self.mode)
+                                   compact=True, mode=self.mode, cap=self.cap)
         return torch.from_numpy(band)

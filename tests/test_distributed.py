@@ -14,7 +14,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, w, h, sh, mode, q):
+def _worker(rank, world, port, n, w, h, sh, mode, cap, q):
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent))
@@ -29,15 +29,17 @@ def _worker(rank, world, port, n, w, h, sh, mode, q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         sc = S.synthetic_scene(n, seed=17, sh_degree=sh, aspect=w / h)
+        if cap:
+            sc.scale *= 3.0
         cam = default_camera(w, h)
         cam.orbit(0.3, 0.05)
         V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
         b, e = shard_bounds(n, world, rank)
-        be = OracleShardBackend(sc.subset(slice(b, e)), rank, world, b, sh_degree=sh, mode=mode)
+        be = OracleShardBackend(sc.subset(slice(b, e)), rank, world, b, sh_degree=sh, mode=mode, cap=cap)
         frame = ShardedRenderer(be, rank, world).render(V, P, w, h)
         if rank == 0:
             from oracle import oracle_py as O
-            ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
+            ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode, cap=cap)
             got = frame.numpy()
             q.put((got.shape == ref.shape and bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))),
                    float(np.abs(got - ref).max()) if got.shape == ref.shape else -1.0))
@@ -46,13 +48,14 @@ def _worker(rank, world, port, n, w, h, sh, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sh,mode", [(2, 0, "tile"), (3, 3, "tile"), (2, 0, "live50")])
-def test_gloo_sharded_frame_bitexact(world, sh, mode):
+@pytest.mark.parametrize("world,sh,mode,cap", [(2, 0, "tile", 0), (3, 3, "tile", 0), (2, 0, "live50", 0),
+                                               (3, 0, "tile", 32)])
+def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 30000, 320, 200, sh, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 30000, 320, 200, sh, mode, cap, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)

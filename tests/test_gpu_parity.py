@@ -83,6 +83,51 @@ def test_render_1080p_parity(built, sh, mode):
         assert nbit == 0, f"{nbit} differing values, L-inf {linf}"
 
 
+@pytest.mark.parametrize("n,w,h,sh,mode,cap,grow", [(10000, 256, 256, 0, "tile", 32, 4.0),
+                                                     (20000, 640, 360, 0, "live50", 50, 4.0),
+                                                     (150000, 1920, 1080, 3, "tile", 32, 1.0),
+                                                     (40000, 640, 360, 0, "live50", 8, 1.0)])
+def test_render_cap_parity(built, n, w, h, sh, mode, cap, grow):
+    """cap mode: first `cap` covering fragments per pixel
+    in arrival order, then S1 order and the mode's composite.  Splats are
+    grown so that per-pixel lists overflow the cap."""
+    from oracle import oracle_py as O
+    sc = _scene(n, 21 + sh, sh, aspect=w / h)
+    sc.scale *= grow
+    r = _renderer(sc, sh=sh, mode=mode)
+    r.set_cap(cap)
+    V, P = orbit_views(w, h, 1)[0]
+    img = r.render_host(V, P, w, h)
+    ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode, cap=cap)
+    linf, nbit = _compare(img, ref)
+    assert linf <= TOL
+    assert nbit == 0, f"{nbit} differing values, L-inf {linf}"
+    uncapped, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
+    assert np.count_nonzero(uncapped.view(np.uint32) != ref.view(np.uint32)) > 0  # the cap is exercised
+    r.set_cap(0)
+    again = r.render_host(V, P, w, h)
+    np.testing.assert_array_equal(again.view(np.uint32), uncapped.view(np.uint32))
+
+
+@pytest.mark.parametrize("n,w,h,sh,mode", [(10000, 256, 256, 0, "tile"), (150000, 1920, 1080, 3, "live50")])
+def test_render_bgra8(built, n, w, h, sh, mode):
+    """BGRA8Unorm output converted inside the composite == the oracle frame
+    converted by the oracle, byte for byte; device and host paths agree."""
+    import torch
+    from oracle import oracle_py as O
+    sc = _scene(n, 41 + sh, sh, aspect=w / h)
+    r = _renderer(sc, sh=sh, mode=mode)
+    V, P = orbit_views(w, h, 1)[0]
+    got = r.render_bgra8_host(V, P, w, h)
+    ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
+    np.testing.assert_array_equal(got, O.to_bgra8(ref))
+    assert got[..., 3].any() and got[..., 2].any()
+    dev = r.render_bgra8(V, P, w, h)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev.cpu().numpy(), got)
+    np.testing.assert_array_equal(O.to_bgra8(r.render_host(V, P, w, h)), got)
+
+
 def test_render_device_out_matches_host(built):
     import torch
     sc = _scene(30000, 5, 0, aspect=4 / 3)
@@ -184,15 +229,19 @@ def test_ply_dropin_path(built, tmp_path):
     assert _compare(img, ref) == (0.0, 0)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_virtual_shards_bitexact(built, world):
+@pytest.mark.parametrize("world,cap", [(2, 0), (3, 0), (3, 32)])
+def test_virtual_shards_bitexact(built, world, cap):
     """K virtual ranks on one GPU through gs_shard_project/gs_shard_render
-    reassemble the single-GPU frame bit for bit (SURVEY §8e verification)."""
+    reassemble the single-GPU frame bit for bit (SURVEY §8e verification);
+    with a fragment cap, arrival order survives the exchange."""
     from gaussian_splat_amd import distributed as D
     W, H = 640, 400
     sc = _scene(60000, 31, 3, aspect=W / H)
+    if cap:
+        sc.scale *= 3.0
     full = _renderer(sc, sh=3)
+    full.set_cap(cap)
     V, P = orbit_views(W, H, 1)[0]
     ref = full.render_host(V, P, W, H)
-    img = D.render_virtual_shards(sc, world, V, P, W, H, sh_degree=3)
+    img = D.render_virtual_shards(sc, world, V, P, W, H, sh_degree=3, cap=cap)
     assert _compare(img, ref) == (0.0, 0)

@@ -130,3 +130,19 @@ def test_oracle_render_invariants():
     assert st["visible"] == 10000 and st["pairs"] > 10000
     img2, _ = O.render(sc, V, P, 256, 256, nthreads=1)
     np.testing.assert_array_equal(img.view(np.uint32), img2.view(np.uint32))  # thread-count independent
+
+
+def test_bgra8_conversion():
+    """BGRA8Unorm output: clamp, x255, round half to even,
+    bytes B, G, R, A.  Parity unpinned (Metal's conversion cannot run here);
+    pinned to that published rule."""
+    from oracle import oracle_py as O
+    special = np.array([[1.0, 0.0, 0.0, 1.0], [0.5, -1.0, 2.0, np.nan], [0.0, 0.25, 0.75, 0.999]], np.float32)
+    got = O.to_bgra8(special.reshape(1, 3, 4))[0]
+    np.testing.assert_array_equal(got[0], [0, 0, 255, 255])          # pure red -> B=0, G=0, R=255
+    np.testing.assert_array_equal(got[1], [255, 0, 128, 0])           # 127.5 -> 128 (even), clamp, NaN -> 0
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.1, 1.1, (64, 48, 4)).astype(np.float32)
+    x[0, :, :] = (np.arange(48 * 4, dtype=np.float32).reshape(48, 4) + 0.5) / np.float32(255)  # near-ties
+    y = np.rint(np.clip(x, 0, 1) * np.float32(255)).astype(np.uint8)
+    np.testing.assert_array_equal(O.to_bgra8(x), y[..., [2, 1, 0, 3]])
