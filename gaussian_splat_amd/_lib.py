@@ -7,9 +7,11 @@ fallback anywhere in the package.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libgsplat.so"
+# GSPLAT_LIB: development aid to A/B a differently built libgsplat (tools/ab.sh)
+LIB_PATH = Path(os.environ.get("GSPLAT_LIB") or Path(__file__).resolve().parent / "libgsplat.so")
 
 
 class GsOptions(C.Structure):

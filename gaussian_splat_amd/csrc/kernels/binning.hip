@@ -29,7 +29,8 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     const uint32_t tx0 = x0 >> kBinShift, ty0 = (lo >> 16) >> kBinShift;
     const uint32_t tx1 = x1 >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     uint32_t off = offsets[j];
-    for (uint32_t ty = first_owned_row(ty0, world, rank); ty <= ty1; ty += world) {
+    for (uint32_t ty = ty0; ty <= ty1; ++ty) {
+        if (!owns_bin_row(ty, world, rank)) continue;
         for (uint32_t tx = tx0; tx <= tx1; ++tx) {
             keys[off] = ty * tiles_x + tx;
             vals[off] = i;

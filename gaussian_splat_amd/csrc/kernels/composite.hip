@@ -4,9 +4,9 @@
 // 8x8 quadrant.  Lists are binned per 32x32 bin (2x2 tiles: 2.35 instead of
 // 4.38 pairs per splat, so sorting is cheaper); the four tiles of a bin are
 // consecutive workgroups on one XCD and share the bin list through its L2.
-// The list is streamed through LDS in batches of 256 (each lane gathers the
-// 16-B rect word of one record, and the other 32 B only when the pixel rect
-// reaches this tile).  Per batch each wave keeps the records whose rect
+// The list is streamed through LDS in batches of 256 records (one 48-B record
+// gathered per lane), software-pipelined: the next batch is in flight into
+// registers while the current one is composited.  Per batch each wave keeps the records whose rect
 // overlaps its quadrant AND whose gaussian ellipse q <= 2 ln 100 intersects
 // the parallelogram the quadrant's pixel centres map to in (u, v) space (an
 // exact point-to-parallelogram distance with a relative safety margin, so the
@@ -71,13 +71,15 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
     const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
 
-    // Grid covers only the owned bin rows: by = row_rem + k * row_mod.  The
-    // four 16x16 tiles of a bin are consecutive workgroups (same XCD / L2).
+    // Grid covers only the owned bin rows: owned row o lies in band
+    // row_rem + (o / 4) * row_mod.  The four 16x16 tiles of a
+    // bin are consecutive workgroups (same XCD / L2).
     const uint32_t per_row = 4u * (uint32_t)a.tiles_x;
     const int owned_row = (int)(wg / per_row);
     const uint32_t k4 = wg - (uint32_t)owned_row * per_row;
     const int bx = (int)(k4 >> 2);
-    const int by = a.row_rem + owned_row * a.row_mod;
+    const int by = ((a.row_rem + (owned_row >> kBandShift) * a.row_mod) << kBandShift) + (owned_row & (kBandRows - 1));
+    if (by >= a.tiles_y) return;  // the last band can be partial
     const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
     const int width = a.width, height = a.height;
     const int tid = threadIdx.x;
@@ -105,6 +107,29 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         if (inside) thr = a.thr[(size_t)py * width + px];
     }
 
+    // Composite update of one fragment (covered = box test and 0.01 cutoff).
+    auto step = [&](bool covered, float alpha, float r, float g, float bl, uint32_t id) {
+        bool in = !done && covered;
+        if constexpr (CAP) in = in && id <= thr;
+        any |= in;
+        if constexpr (MODE == 0) {
+            // out-of-support lanes add an exact zero: bit-identical to skipping
+            const float sa = in ? alpha * (1.0f - A) : 0.0f;
+            C0 = __builtin_fmaf(r, sa, C0);
+            C1 = __builtin_fmaf(g, sa, C1);
+            C2 = __builtin_fmaf(bl, sa, C2);
+            A = A + sa;
+            done = done || A >= kSat;
+        } else {
+            const float tw = in ? T : 0.0f;
+            C0 = __builtin_fmaf(r, tw, C0);
+            C1 = __builtin_fmaf(g, tw, C1);
+            C2 = __builtin_fmaf(bl, tw, C2);
+            T = in ? T * (1.0f - alpha) : T;
+            done = done || T < kTMin;
+        }
+    };
+
     auto body = [&](uint32_t k) {
         const float4 aa = s0[k];
         const float4 bb = s1[k];
@@ -114,58 +139,55 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
         const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
         const float qq = __builtin_fmaf(v, v, u * u);
-        bool in = !done && fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
         if constexpr (MODE == 2) {
             // arrival order: the a.cap-th covering fragment fixes the threshold
+            const bool in = !done && covered;
             cnt += in ? 1 : 0;
             if (in && cnt == a.cap) {
                 thr = sid[k];
                 done = true;
             }
-            return;
         } else {
-            if constexpr (CAP) in = in && sid[k] <= thr;
-            const float alpha = bb.z * gs_gauss(qq);
-            any |= in;
-            if constexpr (MODE == 0) {
-                // out-of-support lanes add an exact zero: bit-identical to skipping
-                const float sa = in ? alpha * (1.0f - A) : 0.0f;
-                C0 = __builtin_fmaf(bb.w, sa, C0);
-                C1 = __builtin_fmaf(cc.x, sa, C1);
-                C2 = __builtin_fmaf(cc.y, sa, C2);
-                A = A + sa;
-                done = done || A >= kSat;
-            } else {
-                const float tw = in ? T : 0.0f;
-                C0 = __builtin_fmaf(bb.w, tw, C0);
-                C1 = __builtin_fmaf(cc.x, tw, C1);
-                C2 = __builtin_fmaf(cc.y, tw, C2);
-                T = in ? T * (1.0f - alpha) : T;
-                done = done || T < kTMin;
-            }
+            step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, kIds ? sid[k] : 0u);
         }
     };
 
+    // Software pipeline: while batch b is composited, batch b+1's records are
+    // in flight into registers and batch b+2's ids are being loaded.
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    uint32_t id_cur = 0, id_next = 0;
+    {
+        const uint32_t j = rg.x + tid;
+        if (j < rg.y) {
+            id_cur = a.vals[j];
+            const float4* rp = a.rec + (size_t)a.rec_stride * id_cur;
+            r0 = rp[0];
+            r1 = rp[1];
+            r2 = rp[2];
+        }
+        if (j + kTileThreads < rg.y) id_next = a.vals[j + kTileThreads];
+    }
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
         if (__syncthreads_count(!done) == 0) break;
-        const uint32_t j = b + tid;
-        if (j < rg.y) {
-            // the bin list holds the splats of all four tiles: fetch the rect
-            // first and the geometry only for splats that reach this tile
-            const uint32_t id = a.vals[j];
-            const float4* rp = a.rec + (size_t)a.rec_stride * id;
-            const float4 c = rp[2];
-            s2[tid] = c;
-            if constexpr (kIds) sid[tid] = id;
-            const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
-            const bool hit = !((hi >> 16) < ty0 || (lo >> 16) > ty0 + (kTile - 1) || (hi & 0xFFFFu) < tx0 ||
-                               (lo & 0xFFFFu) > tx0 + (kTile - 1));
-            if (hit) {
-                s0[tid] = rp[0];
-                s1[tid] = rp[1];
-            }
+        if (b + tid < rg.y) {
+            s0[tid] = r0;
+            s1[tid] = r1;
+            s2[tid] = r2;
+            if constexpr (kIds) sid[tid] = id_cur;
         }
         __syncthreads();
+        {
+            const uint32_t j = b + kTileThreads + tid;
+            if (j < rg.y) {
+                id_cur = id_next;
+                const float4* rp = a.rec + (size_t)a.rec_stride * id_cur;
+                r0 = rp[0];
+                r1 = rp[1];
+                r2 = rp[2];
+            }
+            if (j + kTileThreads < rg.y) id_next = a.vals[j + kTileThreads];
+        }
         const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
         // wave-level compaction of the splats reaching this quadrant (index order kept)
         uint32_t nl = 0;
@@ -217,7 +239,8 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
 template <int MODE, bool CAP>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st) {
     if (a.row_mod < 1 || a.row_rem < 0 || a.row_rem >= a.row_mod) return hipErrorInvalidValue;
-    const int owned_rows = a.tiles_y > a.row_rem ? (a.tiles_y - a.row_rem + a.row_mod - 1) / a.row_mod : 0;
+    const int bands = (a.tiles_y + kBandRows - 1) >> kBandShift;
+    const int owned_rows = bands > a.row_rem ? ((bands - a.row_rem + a.row_mod - 1) / a.row_mod) * kBandRows : 0;
     const uint32_t nwg = (uint32_t)(4 * a.tiles_x * owned_rows);
     if (nwg == 0) return hipSuccess;
     composite_kernel<MODE, CAP><<<nwg, kTileThreads, 0, st>>>(a, nwg);

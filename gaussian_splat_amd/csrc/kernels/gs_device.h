@@ -86,19 +86,32 @@ __device__ __forceinline__ uint32_t half_bits(float f) {
 // splat carries the empty rect (lo = 0xFFFFFFFF, hi = 0).
 constexpr uint32_t kEmptyRectLo = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t first_owned_row(uint32_t a, uint32_t world, uint32_t rank) {
-    return a + (rank + world - a % world) % world;
+// Multi-GPU ownership: bin row `by` belongs to band
+// by >> kBandShift (4 bin rows = 128 px), and band b to rank b % world.
+// Bands rather than single rows: a typical 16-px-tall splat straddles a
+// 128-px boundary ~4x less often than a 32-px one, which shrinks the
+// record exchange.
+constexpr int kBandShift = 2;
+constexpr int kBandRows = 1 << kBandShift;
+
+__device__ __forceinline__ bool owns_bin_row(uint32_t by, uint32_t world, uint32_t rank) {
+    return world == 1 || ((by >> kBandShift) % world) == rank;
 }
 
-// Bins of the rect whose bin row is owned by `rank` (by % world == rank).
+// Bins of the rect whose bin row is owned by `rank`.
 __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, uint32_t world, uint32_t rank) {
     const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
     if (x1 < x0) return 0u;
     const uint32_t ty0 = (lo >> 16) >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     const uint32_t cols = (x1 >> kBinShift) - (x0 >> kBinShift) + 1u;
     if (world == 1) return (ty1 - ty0 + 1u) * cols;
-    const uint32_t f = first_owned_row(ty0, world, rank);
-    return f > ty1 ? 0u : ((ty1 - f) / world + 1u) * cols;
+    uint32_t rows = 0;
+    for (uint32_t b = ty0 >> kBandShift; b <= ty1 >> kBandShift; ++b) {
+        if (b % world != rank) continue;
+        const uint32_t r0 = max(ty0, b << kBandShift), r1 = min(ty1, (b << kBandShift) + kBandRows - 1u);
+        rows += r1 - r0 + 1u;
+    }
+    return rows * cols;
 }
 
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to

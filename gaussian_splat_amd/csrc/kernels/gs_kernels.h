@@ -67,8 +67,8 @@ struct CompositeArgs {
     const float4* rec;      // records, rec_stride float4 apart (3 local, 4 exchange)
     int rec_stride;
     int width, height, tiles_x, tiles_y;  // frame and 32x32 bin grid
-    int row_mod, row_rem;   // composite bin rows by with by % row_mod == row_rem
-    int compact;            // 1: write owned bin rows stacked (band buffer)
+    int row_mod, row_rem;   // composite bin rows in bands (by >> kBandShift) % row_mod == row_rem
+    int compact;            // 1: write owned bands stacked (band buffer)
     float4* out;            // fp32 RGBA, or (when out_bgra8 is set) unused
     uint32_t* out_bgra8;    // packed BGRA8Unorm (metal_renderer.mm:58), converted in-kernel
     // per-pixel fragment cap (0 = none): thr[py * width + px] = splat id of the

@@ -15,10 +15,12 @@ constexpr int kShWaves = 4;
 constexpr int kShIpt = kScanItems / 256;  // 16 rounds of 64 per wave
 constexpr int kShWaveItems = 64 * kShIpt;
 
+// Ranks owning any of the bin rows ty0..ty1 (band b -> rank b % world).
 __device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, int world) {
-    if (ty1 - ty0 + 1 >= (uint32_t)world) return world >= 32 ? 0xFFFFFFFFu : ((1u << world) - 1u);
+    const uint32_t b0 = ty0 >> kBandShift, b1 = ty1 >> kBandShift;
+    if (b1 - b0 + 1 >= (uint32_t)world) return world >= 32 ? 0xFFFFFFFFu : ((1u << world) - 1u);
     uint32_t m = 0;
-    for (uint32_t t = ty0; t <= ty1; ++t) m |= 1u << (t % (uint32_t)world);
+    for (uint32_t b = b0; b <= b1; ++b) m |= 1u << (b % (uint32_t)world);
     return m;
 }
 

@@ -1,8 +1,8 @@
-"""Multi-GPU rendering: splat-index shards, tile-row ownership, RCCL exchange.
+"""Multi-GPU rendering: splat-index shards, band ownership, RCCL exchange.
 
 DESIGN.md §6.  One process per GPU.  Rank r holds a contiguous splat-index
-range of the scene and owns the 32-pixel bin rows by with by % world == r
-(a bin is 2x2 of the 16x16 tiles; the binning granularity of the pipeline).
+range of the scene and owns the 128-pixel bands b (4 rows of 32x32 bins)
+with b % world == r.
 Per frame:
 
   1. gs_shard_project   project the local shard on the GPU and pack a 64-B
@@ -10,7 +10,7 @@ Per frame:
                         rank) pair, grouped by destination, index order inside
   2. all_to_all         exchange counts, then records (RCCL over xGMI)
   3. gs_shard_render    bin/sort/composite the received records into the
-                        owned tile rows (a compact band buffer)
+                        owned bands (a compact band buffer)
   4. gather             bands -> rank 0, interleaved back into the frame
 
 Records arrive in source-rank order = global splat-index order, so each
@@ -31,7 +31,7 @@ from . import _lib as L
 from .api import InstancedSplatRenderer, Options, Scene, _mat16
 from ._lib import check, lib
 
-ROW = 32  # ownership unit: one 32-pixel bin row
+ROW = 128  # ownership unit: one 128-pixel band (4 bin rows)
 
 
 def band_rows(height: int, world: int) -> int:
@@ -41,7 +41,7 @@ def band_rows(height: int, world: int) -> int:
 
 
 def assemble(bands, width: int, height: int, world: int):
-    """Interleave rank bands (bin row r <- band[r % world], slot r // world) into a frame."""
+    """Interleave rank bands (band r <- bands[r % world], slot r // world) into a frame."""
     import torch
 
     th = (height + ROW - 1) // ROW

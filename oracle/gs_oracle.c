@@ -17,7 +17,7 @@
 #endif
 
 #define TILE 16
-#define OWN_ROW 32 /* multi-GPU ownership unit: 32-px bin rows */
+#define OWN_ROW 128 /* multi-GPU ownership unit: 128-px bands of 4 bin rows */
 /* 2*ln(100): exp(-q/2) < 0.01 <=> q > 2 ln 100 (tile.metal:191-195). */
 #define ORA_QMAX 9.21034037197618f
 /* 0.99 saturation (tile.metal:261), 0.01 transmittance (50layer.metal:219). */

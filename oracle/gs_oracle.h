@@ -125,7 +125,7 @@ int ora_render(const ora_scene *s, const float view[16], const float proj[16], i
                int height, const ora_options *opt, float *out_rgba, ora_stats *stats);
 
 /* Bin, sort (S1) and composite an explicit record list (index = arrival
- * order) into the 32-px pixel-row bands b = py / 32 with b % row_mod ==
+ * order) into the 128-px pixel-row bands b = py / 128 with b % row_mod ==
  * row_rem; compact = 1 writes those bands stacked (the multi-GPU layout).  Culled records are
  * all-zero (dkey 0, rect_hi 0, opacity 0). */
 int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int width, int height,

@@ -160,8 +160,8 @@ def composite_records(rec, dkey, width, height, row_mod=1, row_rem=0, compact=Fa
     """Bin/sort/composite an explicit record list (index = arrival order)."""
     rec = np.ascontiguousarray(rec, RECORD_DTYPE)
     dkey = np.ascontiguousarray(dkey, np.uint32)
-    th = (height + 31) // 32
-    rows = ((th + row_mod - 1) // row_mod) * 32 if compact else height
+    nb = (height + 127) // 128  # 128-px ownership bands
+    rows = ((nb + row_mod - 1) // row_mod) * 128 if compact else height
     out = np.zeros((rows, width, 4), np.float32)
     o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
     st = OraStats()

@@ -1,7 +1,7 @@
 """CPU stand-in for HipShardBackend (test infrastructure).
 
 Per-rank compute by the oracle; the 64-B exchange record format, the
-destination rule (tile row % world) and the band layout are the product's,
+destination rule (128-px band % world) and the band layout are the product's,
 so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer exercise the
 real exchange / gather / assembly protocol on CPU.
 """
@@ -25,8 +25,8 @@ class OracleShardBackend:
 
         rec, dk, nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
         vis = nt > 0
-        ty0 = (rec["rect_lo"] >> 16) >> 5  # 32-px bin rows
-        ty1 = (rec["rect_hi"] >> 16) >> 5
+        ty0 = (rec["rect_lo"] >> 16) >> 7  # 128-px ownership bands
+        ty1 = (rec["rect_hi"] >> 16) >> 7
         w = self.world
         parts, counts = [], []
         for d in range(w):

@@ -1,4 +1,4 @@
-"""Multi-rank protocol on CPU with gloo: splat-index shards, tile-row
+"""Multi-rank protocol on CPU with gloo: splat-index shards, band
 ownership, all_to_all record exchange, band gather + assembly.  The
 assembled frame must equal the single-process oracle frame bit for bit."""
 import os
@@ -55,7 +55,7 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 30000, 320, 200, sh, mode, cap, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 30000, 320, 400, sh, mode, cap, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
@@ -69,14 +69,14 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
 def test_assemble_layout():
     import torch
     from gaussian_splat_amd.distributed import assemble, band_rows
-    w, h, world = 40, 140, 3  # 5 bin rows of 32 px, uneven split 2/2/1
+    w, h, world = 40, 560, 3  # 5 bands of 128 px (last one partial), uneven split 2/2/1
     frame = torch.arange(h * w * 4, dtype=torch.float32).view(h, w, 4)
     th = 5
     bands = []
     for r in range(world):
         b = torch.zeros(band_rows(h, world), w, 4)
         for k, ty in enumerate(range(r, th, world)):
-            rows = frame[ty * 32: min(h, ty * 32 + 32)]
-            b[k * 32: k * 32 + rows.shape[0]] = rows
+            rows = frame[ty * 128: min(h, ty * 128 + 128)]
+            b[k * 128: k * 128 + rows.shape[0]] = rows
         bands.append(b)
     torch.testing.assert_close(assemble(bands, w, h, world), frame, rtol=0, atol=0)
