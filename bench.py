@@ -65,6 +65,9 @@ def stage_summary(stats_list):
         ms = float(np.mean([s[f"ms_{k}"] for s in stats_list]))
         by = float(np.mean([s[f"bytes_{k}"] for s in stats_list]))
         out[k] = {"ms": ms, "bytes": by, "gbs": by / (ms * 1e6) if ms > 0 else 0.0}
+    ex = float(np.mean([s["ms_exchange"] for s in stats_list]))
+    if ex > 0:  # multi-GPU: count + pack + all_to_all (not a kernel roofline)
+        out["exchange"] = {"ms": ex, "bytes": 0.0, "gbs": 0.0}
     return out
 
 
@@ -141,9 +144,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
+    # device 0, collectives over gloo staged through host memory.
+    backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+    if os.environ.get("GS_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
 
     from gaussian_splat_amd import scene as S
@@ -199,7 +210,7 @@ def main():
         s0 = stats[-1]
         rl = None
         if st:
-            dom = max(st, key=lambda k: st[k]["ms"])
+            dom = max((k for k in st if k != "exchange"), key=lambda k: st[k]["ms"])
             d = st[dom]
             rl = {"bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": round(d["gbs"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
@@ -212,7 +223,8 @@ def main():
             "data": "synthetic (seeded 3DGS-statistics scene; no garden .ply offline)",
             "config": {"workload": f"{args.splats} splats/GPU @ {W}x{H}, SH{args.sh}, {args.mode} contract",
                        "global_splats": total_splats, "width": W, "height": H, "sh_degree": args.sh,
-                       "parallelism": f"splat-shard x{world}, tile-row ownership" if world > 1 else "single GPU",
+                       "parallelism": f"splat-shard x{world}, 128-px band ownership, {backend}" if world > 1
+                       else "single GPU",
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},

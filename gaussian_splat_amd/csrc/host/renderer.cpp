@@ -82,7 +82,8 @@ struct gs_handle {
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
     uint64_t* host_total = nullptr;  // pinned
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[9] = {};  // stage boundaries 0..7; 8 = exchange done (shard frames)
+    bool shard_frame = false;
     bool events = false;
     uint32_t* last_keys = nullptr;  // sorted pair arrays of the last frame
     uint32_t* last_vals = nullptr;
@@ -373,7 +374,8 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     if (h->opt.stage_timing && h->events) {
         (void)hipEventSynchronize(h->ev[7]);
         s.ms_preprocess = elapsed(h, 0, 1);
-        s.ms_depth_sort = elapsed(h, 1, 2);
+        s.ms_exchange = h->shard_frame ? elapsed(h, 1, 8) : 0.0f;
+        s.ms_depth_sort = elapsed(h, h->shard_frame ? 8 : 1, 2);
         s.ms_scan = elapsed(h, 2, 3);
         s.ms_duplicate = elapsed(h, 3, 4);
         s.ms_sort = elapsed(h, 4, 5);
@@ -541,6 +543,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         out = h->fb.ptr;
     }
     std::memset(&h->stats, 0, sizeof h->stats);
+    h->shard_frame = false;
     mark(h, 0, st);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
@@ -663,8 +666,12 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
     GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
     GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
     if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
+    std::memset(&h->stats, 0, sizeof h->stats);
+    h->shard_frame = true;
+    mark(h, 0, st);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
+    mark(h, 1, st);
     GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
     GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
@@ -703,14 +710,16 @@ gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, 
     GS_HIP(h->rrlo.reserve(mm * 4));
     GS_HIP(h->rrhi.reserve(mm * 4));
     const float4* rv = static_cast<const float4*>(recv);
+    mark(h, 8, st);
     GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));
     if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                 h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, h->world, h->rank, 1,
                                 reinterpret_cast<float4*>(out_rgba), nullptr, st)) != GS_OK)
         return s;
-    const uint64_t P = (uint64_t)h->stats.pairs;
-    h->stats.pairs = (int64_t)P;
+    // stage times span both calls: preprocess (gs_shard_project) ... composite;
+    // the exchange between them falls inside the depth-sort interval
+    fill_stats(h, (uint64_t)h->stats.pairs, U);
     h->stats.tiles = T;
     return GS_OK;
 }

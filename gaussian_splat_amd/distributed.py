@@ -99,22 +99,32 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return b, e
 
 
+def _host_staged(group) -> bool:
+    """gloo moves host tensors only: stage device buffers through host memory
+    (a rehearsal path; RCCL/nccl exchanges device memory directly)."""
+    import torch.distributed as dist
+
+    return dist.get_backend(group) == "gloo"
+
+
 def exchange(send, counts, xbytes, world, group=None):
     """all_to_all of counts then of records (bytes); returns (recv, nrec)."""
     import torch
     import torch.distributed as dist
 
     dev = send.device
-    sc = torch.tensor(counts, dtype=torch.int64, device=dev)
-    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    cdev = torch.device("cpu") if _host_staged(group) else dev
+    sc = torch.tensor(counts, dtype=torch.int64, device=cdev)
+    rc = torch.empty(world, dtype=torch.int64, device=cdev)
     dist.all_to_all_single(rc, sc, group=group)
     rcounts = [int(x) for x in rc.cpu().tolist()]
     total = sum(rcounts)
-    recv = torch.empty(max(1, total * xbytes), dtype=torch.uint8, device=dev)
     ssz = sum(counts) * xbytes
-    dist.all_to_all_single(recv[: total * xbytes], send[:ssz], [c * xbytes for c in rcounts],
+    recv = torch.empty(max(1, total * xbytes), dtype=torch.uint8, device=cdev)
+    src = send[:ssz] if cdev == dev else send[:ssz].cpu()
+    dist.all_to_all_single(recv[: total * xbytes], src, [c * xbytes for c in rcounts],
                            [c * xbytes for c in counts], group=group)
-    return recv, total
+    return (recv if cdev == dev else recv.to(dev)), total
 
 
 class ShardedRenderer:
@@ -135,8 +145,14 @@ class ShardedRenderer:
             return band
         if self.world == 1:
             return assemble([band], width, height, 1)
-        bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
-        dist.gather(band, bands, dst=0, group=self.group)
+        if _host_staged(self.group):
+            hb = band.cpu()
+            bands = [hb.new_empty(hb.shape) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(hb, bands, dst=0, group=self.group)
+            bands = [b.to(band.device) for b in bands] if self.rank == 0 else None
+        else:
+            bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(band, bands, dst=0, group=self.group)
         return assemble(bands, width, height, self.world) if self.rank == 0 else None
 
 

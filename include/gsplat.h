@@ -88,7 +88,7 @@ typedef struct gs_stats {
     float ms_preprocess, ms_scan, ms_duplicate, ms_sort, ms_ranges, ms_composite, ms_total;
     int64_t bytes_preprocess, bytes_scan, bytes_duplicate, bytes_sort, bytes_ranges, bytes_composite;
     float ms_depth_sort;   /* splats by depth key (ms_sort = pairs by tile) */
-    int32_t pad0;
+    float ms_exchange;     /* multi-GPU: destination count + pack + exchange (between the shard calls) */
     int64_t bytes_depth_sort;
 } gs_stats;
 

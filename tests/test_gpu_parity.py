@@ -245,3 +245,57 @@ def test_virtual_shards_bitexact(built, world, cap):
     ref = full.render_host(V, P, W, H)
     img = D.render_virtual_shards(sc, world, V, P, W, H, sh_degree=3, cap=cap)
     assert _compare(img, ref) == (0.0, 0)
+
+
+def _rank_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import torch
+    import torch.distributed as dist
+    from gaussian_splat_amd import Options, scene as S
+    from gaussian_splat_amd.distributed import HipShardBackend, ShardedRenderer, shard_bounds
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    from conftest import orbit_views
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        W, H = 800, 600
+        sc = S.activate(S.synthetic_raw(60000, seed=51, aspect=W / H), 3)
+        b, e = shard_bounds(sc.n, world, rank)
+        be = HipShardBackend(sc.subset(slice(b, e)), rank, world, b, Options(sh_degree=3, crop=False), 0)
+        V, P = orbit_views(W, H, 1)[0]
+        frame = ShardedRenderer(be, rank, world).render(V, P, W, H)
+        if rank == 0:
+            torch.cuda.synchronize()
+            q.put(frame.cpu().numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multiprocess_ranks_bitexact(built):
+    """Two rank processes on the GPU through the product multi-GPU path
+    (gs_shard_project -> all_to_all -> gs_shard_render -> gather), collectives
+    over gloo staged through host memory (one GPU here); the gathered frame
+    equals the single-GPU render bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from gaussian_splat_amd import scene as S
+    W, H = 800, 600
+    sc = S.activate(S.synthetic_raw(60000, seed=51, aspect=W / H), 3)
+    r = _renderer(sc, sh=3, crop=False)
+    V, P = orbit_views(W, H, 1)[0]
+    ref = r.render_host(V, P, W, H)
+    assert _compare(got, ref) == (0.0, 0)
