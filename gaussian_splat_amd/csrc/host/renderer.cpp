@@ -90,12 +90,16 @@ struct gs_handle {
     gs_stats stats{};
     // multi-GPU shard config
     int32_t rank = 0, world = 1;
+    std::vector<uint8_t> custom_owner;  // gs_shard_set_rows (empty: default ranges)
+    std::vector<uint8_t> owner_host;    // table currently on the device
+    std::vector<uint16_t> rows_host;    // this rank's owned bin rows
+    DevBuf owner_dev, rows_dev;
     int64_t index_base = 0;
 
     ~gs_handle() {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
-                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi})
+                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev})
             b->release();
         if (host_total) (void)hipHostFree(host_total);
         if (host_xtotal) (void)hipHostFree(host_xtotal);
@@ -242,15 +246,60 @@ float elapsed(gs_handle* h, int a, int b) {
     return ms;
 }
 
+// Bin-row ownership of the frame as the kernels see it.
+struct Ownership {
+    gs::RowOwnership dev{nullptr, 0};  // owner table (nullptr: single GPU)
+    const uint16_t* rows = nullptr;    // owned bin rows (nullptr: all)
+    int nrows = 0;
+};
+
+// Default table: rank r owns the contiguous bin rows [r*R/world, (r+1)*R/world).
+std::vector<uint8_t> default_row_owner(int R, int world) {
+    std::vector<uint8_t> o((size_t)R);
+    for (int r = 0; r < world; ++r)
+        for (int by = (int)((int64_t)r * R / world); by < (int)((int64_t)(r + 1) * R / world); ++by) o[by] = (uint8_t)r;
+    return o;
+}
+
+gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* out) {
+    *out = Ownership{};
+    if (h->world == 1) {
+        out->nrows = tiles_y;
+        return GS_OK;
+    }
+    std::vector<uint8_t> o = (int)h->custom_owner.size() == tiles_y ? h->custom_owner
+                                                                    : default_row_owner(tiles_y, h->world);
+    if (!h->custom_owner.empty() && (int)h->custom_owner.size() != tiles_y)
+        return fail(GS_ERR_INVALID_ARG, "gs_shard_set_rows: table has " + std::to_string(h->custom_owner.size()) +
+                                            " rows, the frame has " + std::to_string(tiles_y));
+    if (o != h->owner_host) {
+        std::vector<uint16_t> rows;
+        for (int by = 0; by < tiles_y; ++by)
+            if (o[by] == h->rank) rows.push_back((uint16_t)by);
+        GS_HIP(h->owner_dev.reserve(o.size()));
+        GS_HIP(h->rows_dev.reserve(std::max<size_t>(rows.size(), 1) * 2));
+        GS_HIP(hipMemcpyAsync(h->owner_dev.ptr, o.data(), o.size(), hipMemcpyHostToDevice, st));
+        if (!rows.empty())
+            GS_HIP(hipMemcpyAsync(h->rows_dev.ptr, rows.data(), rows.size() * 2, hipMemcpyHostToDevice, st));
+        GS_HIP(hipStreamSynchronize(st));  // the host vectors are the staging copies
+        h->owner_host = std::move(o);
+        h->rows_host = std::move(rows);
+    }
+    out->dev = gs::RowOwnership{h->owner_dev.as<uint8_t>(), (uint32_t)h->rank};
+    out->rows = h->rows_dev.as<uint16_t>();
+    out->nrows = (int)h->rows_host.size();
+    return GS_OK;
+}
+
 // Bin lists from m splats visited in `order` (nullptr = index order) with
 // rects (rect_lo, rect_hi) in that order: ordered scan of bin counts (P and
 // the visible count to host) -> duplicate -> stable sort by bin id ->
 // ranges.  Marks 3..6 when `timed`.
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
-                          const uint32_t* rect_hi, const gs::FrameUniforms& U, int world, int rank, bool timed,
+                          const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, world, rank, h->offsets.as<uint32_t>(),
+    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, own.dev, h->offsets.as<uint32_t>(),
                                       h->partials.as<uint64_t>(), h->total.as<uint64_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));
@@ -266,8 +315,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     // pairs (bin, splat) in visiting order
-    GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, world,
-                                rank, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, own.dev,
+                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
     if (timed) mark(h, 4, st);
     // stable sort by bin id only
     const int bits = bits_for(T);
@@ -295,7 +344,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 // bin lists (counted in the depth-sort stage time).
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
-                             int world, int rank, int compact, float4* out, uint32_t* out_bgra8, hipStream_t st) {
+                             int compact, float4* out, uint32_t* out_bgra8, hipStream_t st) {
+    Ownership own;
+    gs_status so = frame_ownership(h, U.tiles_y, st, &own);
+    if (so != GS_OK) return so;
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
     for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth, &h->offsets})
         GS_HIP(b->reserve(mm * 4));
@@ -308,8 +360,8 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     ca.height = U.height;
     ca.tiles_x = U.tiles_x;
     ca.tiles_y = U.tiles_y;
-    ca.row_mod = world;
-    ca.row_rem = rank;
+    ca.rows = own.rows;
+    ca.nrows = own.nrows;
     ca.compact = compact;
     ca.out = out;
     ca.out_bgra8 = out_bgra8;
@@ -319,7 +371,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, world, rank, false, st, &vals, &P);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, false, st, &vals, &P);
         if (s != GS_OK) return s;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
@@ -340,7 +392,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* shi = in_tmp ? vtmp[2] : vout[2];
     mark(h, 2, st);
     // 2. bin lists in depth order
-    gs_status s = build_bin_lists(h, m, order, slo, shi, U, world, rank, true, st, &vals, &P);
+    gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P);
     if (s != GS_OK) return s;
     ca.vals = vals;
     ca.ranges = h->ranges.as<uint2>();
@@ -549,7 +601,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     mark(h, 1, st);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
-                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 1, 0, 0,
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
                                 bgra8 ? static_cast<uint32_t*>(out) : nullptr, st)) != GS_OK)
         return s;
@@ -648,6 +700,16 @@ gs_status gs_shard_configure(gs_handle* h, int32_t rank, int32_t world, int64_t 
     h->rank = rank;
     h->world = world;
     h->index_base = index_base;
+    h->custom_owner.clear();
+    h->owner_host.clear();
+    return GS_OK;
+}
+
+gs_status gs_shard_set_rows(gs_handle* h, const uint8_t* owner, int32_t nrows) {
+    if (!h || nrows < 0 || (nrows > 0 && !owner)) return fail(GS_ERR_INVALID_ARG, "gs_shard_set_rows: bad arguments");
+    for (int32_t i = 0; i < nrows; ++i)
+        if (owner[i] >= h->world) return fail(GS_ERR_INVALID_ARG, "gs_shard_set_rows: owner >= world");
+    h->custom_owner.assign(owner, owner + nrows);
     return GS_OK;
 }
 
@@ -673,7 +735,10 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     mark(h, 1, st);
     GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
-    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world,
+    Ownership own;
+    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+    if (!own.dev.owner) return fail(GS_ERR_STATE, "gs_shard_project: world size 1");
+    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, own.dev.owner,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
@@ -714,7 +779,7 @@ gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, 
     GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));
     if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
-                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, h->world, h->rank, 1,
+                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, 1,
                                 reinterpret_cast<float4*>(out_rgba), nullptr, st)) != GS_OK)
         return s;
     // stage times span both calls: preprocess (gs_shard_project) ... composite;

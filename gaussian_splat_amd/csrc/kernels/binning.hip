@@ -17,7 +17,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
                                                         const uint32_t* __restrict__ rect_lo,
                                                         const uint32_t* __restrict__ rect_hi,
                                                         const uint32_t* __restrict__ offsets, uint32_t n,
-                                                        uint32_t tiles_x, uint32_t world, uint32_t rank,
+                                                        uint32_t tiles_x, RowOwnership own,
                                                         uint32_t* __restrict__ keys,
                                                         uint32_t* __restrict__ vals) {
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     const uint32_t tx1 = x1 >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     uint32_t off = offsets[j];
     for (uint32_t ty = ty0; ty <= ty1; ++ty) {
-        if (!owns_bin_row(ty, world, rank)) continue;
+        if (!owns_bin_row(ty, own)) continue;
         for (uint32_t tx = tx0; tx <= tx1; ++tx) {
             keys[off] = ty * tiles_x + tx;
             vals[off] = i;
@@ -57,11 +57,10 @@ __global__ __launch_bounds__(256) void tile_ranges_kernel(const uint32_t* __rest
 }
 
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, int world, int rank,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
                             uint32_t* keys, uint32_t* vals, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(order, rect_lo, rect_hi, offsets, n, tiles_x, (uint32_t)world,
-                                                      (uint32_t)rank, keys, vals);
+    duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(order, rect_lo, rect_hi, offsets, n, tiles_x, own, keys, vals);
     return hipGetLastError();
 }
 

@@ -71,15 +71,13 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
     const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
 
-    // Grid covers only the owned bin rows: owned row o lies in band
-    // row_rem + (o / 4) * row_mod.  The four 16x16 tiles of a
-    // bin are consecutive workgroups (same XCD / L2).
+    // Grid covers only the owned bin rows.  The four 16x16
+    // tiles of a bin are consecutive workgroups (same XCD / L2).
     const uint32_t per_row = 4u * (uint32_t)a.tiles_x;
     const int owned_row = (int)(wg / per_row);
     const uint32_t k4 = wg - (uint32_t)owned_row * per_row;
     const int bx = (int)(k4 >> 2);
-    const int by = ((a.row_rem + (owned_row >> kBandShift) * a.row_mod) << kBandShift) + (owned_row & (kBandRows - 1));
-    if (by >= a.tiles_y) return;  // the last band can be partial
+    const int by = a.rows ? (int)a.rows[owned_row] : owned_row;
     const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
     const int width = a.width, height = a.height;
     const int tid = threadIdx.x;
@@ -238,10 +236,8 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
 
 template <int MODE, bool CAP>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st) {
-    if (a.row_mod < 1 || a.row_rem < 0 || a.row_rem >= a.row_mod) return hipErrorInvalidValue;
-    const int bands = (a.tiles_y + kBandRows - 1) >> kBandShift;
-    const int owned_rows = bands > a.row_rem ? ((bands - a.row_rem + a.row_mod - 1) / a.row_mod) * kBandRows : 0;
-    const uint32_t nwg = (uint32_t)(4 * a.tiles_x * owned_rows);
+    if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
+    const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
     if (nwg == 0) return hipSuccess;
     composite_kernel<MODE, CAP><<<nwg, kTileThreads, 0, st>>>(a, nwg);
     return hipGetLastError();

@@ -86,31 +86,29 @@ __device__ __forceinline__ uint32_t half_bits(float f) {
 // splat carries the empty rect (lo = 0xFFFFFFFF, hi = 0).
 constexpr uint32_t kEmptyRectLo = 0xFFFFFFFFu;
 
-// Multi-GPU ownership: bin row `by` belongs to band
-// by >> kBandShift (4 bin rows = 128 px), and band b to rank b % world.
-// Bands rather than single rows: a typical 16-px-tall splat straddles a
-// 128-px boundary ~4x less often than a 32-px one, which shrinks the
-// record exchange.
-constexpr int kBandShift = 2;
-constexpr int kBandRows = 1 << kBandShift;
+// Multi-GPU ownership: every 32-px bin row has one owning
+// rank, owner[by].  The default table gives each rank a contiguous, balanced
+// range of bin rows (few splats straddle a boundary, so the record exchange
+// stays small); callers may install their own (gs_shard_set_rows).  A null
+// table means a single GPU: the rank owns every row.
+struct RowOwnership {
+    const uint8_t* owner;
+    uint32_t rank;
+};
 
-__device__ __forceinline__ bool owns_bin_row(uint32_t by, uint32_t world, uint32_t rank) {
-    return world == 1 || ((by >> kBandShift) % world) == rank;
+__device__ __forceinline__ bool owns_bin_row(uint32_t by, const RowOwnership& o) {
+    return !o.owner || o.owner[by] == o.rank;
 }
 
-// Bins of the rect whose bin row is owned by `rank`.
-__device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, uint32_t world, uint32_t rank) {
+// Bins of the rect whose bin row is owned by this rank.
+__device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, const RowOwnership& o) {
     const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
     if (x1 < x0) return 0u;
     const uint32_t ty0 = (lo >> 16) >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     const uint32_t cols = (x1 >> kBinShift) - (x0 >> kBinShift) + 1u;
-    if (world == 1) return (ty1 - ty0 + 1u) * cols;
+    if (!o.owner) return (ty1 - ty0 + 1u) * cols;
     uint32_t rows = 0;
-    for (uint32_t b = ty0 >> kBandShift; b <= ty1 >> kBandShift; ++b) {
-        if (b % world != rank) continue;
-        const uint32_t r0 = max(ty0, b << kBandShift), r1 = min(ty1, (b << kBandShift) + kBandRows - 1u);
-        rows += r1 - r0 + 1u;
-    }
+    for (uint32_t by = ty0; by <= ty1; ++by) rows += o.owner[by] == o.rank ? 1u : 0u;
     return rows * cols;
 }
 

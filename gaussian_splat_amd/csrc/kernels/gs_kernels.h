@@ -17,19 +17,19 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
-// Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], world, rank) into
+// Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], own) into
 // offsets[n]; total[0] (device u64) = sum, total[1] = items with a nonzero
 // count.  partials: 2 * ceil(n / kScanItems) u64.
-hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
-                                  int rank, uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st);
+hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
+                                  uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st);
 
 // ---- binning.hip -----------------------------------------------------------
 // Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
 // rect_hi[j]) emits (bin, order[j]) for each bin of its rect whose row is
-// owned (by % world == rank), starting at offsets[j].  order == nullptr
+// owned by this rank, starting at offsets[j].  order == nullptr
 // means the identity (pairs in index order).
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, int world, int rank,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
                             uint32_t* keys, uint32_t* vals, hipStream_t st);
 // ranges[tile] = [start, end) in the tile-sorted pair array (zeroed here).
 hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* ranges, uint32_t ntiles_total,
@@ -67,8 +67,9 @@ struct CompositeArgs {
     const float4* rec;      // records, rec_stride float4 apart (3 local, 4 exchange)
     int rec_stride;
     int width, height, tiles_x, tiles_y;  // frame and 32x32 bin grid
-    int row_mod, row_rem;   // composite bin rows in bands (by >> kBandShift) % row_mod == row_rem
-    int compact;            // 1: write owned bands stacked (band buffer)
+    const uint16_t* rows;   // owned bin rows, ascending (nullptr: every row)
+    int nrows;              // number of owned bin rows
+    int compact;            // 1: write the owned bin rows stacked (band buffer)
     float4* out;            // fp32 RGBA, or (when out_bgra8 is set) unused
     uint32_t* out_bgra8;    // packed BGRA8Unorm (metal_renderer.mm:58), converted in-kernel
     // per-pixel fragment cap (0 = none): thr[py * width + px] = splat id of the
@@ -89,9 +90,10 @@ hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 // ---- shard.hip (multi-GPU tile-row ownership) ------------------------------
 constexpr int kXRecFloat4 = 4;  // 64-B exchange record: 48-B record + dkey, global index
 constexpr int kMaxWorld = 32;
-// dest_mask[i]: bit r set iff splat i touches a tile row owned by rank r.
+// dest_mask[i]: bit r set iff splat i touches a bin row owned by rank r (owner[by]).
 // counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
+                              const uint8_t* owner,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);
 // Exclusive scan of each destination row; dest_total[world].
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);

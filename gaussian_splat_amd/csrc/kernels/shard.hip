@@ -1,9 +1,9 @@
 // shard.hip — multi-GPU exchange kernels.
 //
 // Scenes are sharded by splat index (rank r holds a contiguous index range).
-// 32-px bin rows are owned by rank (bin_row % world): every rank projects its
-// shard, then sends each visible splat's 64-B exchange record to the ranks
-// owning a bin row its rect touches.  Received records arrive in source-rank order,
+// Every 32-px bin row has an owning rank (owner[by]): every
+// rank projects its shard, then sends each visible splat's 64-B exchange
+// record to the ranks owning a bin row its rect touches.  Received records arrive in source-rank order,
 // i.e. in global index order, so the receiving rank's stable sort reproduces
 // the single-GPU per-tile order exactly (bit-identical composite).
 #include "gs_kernels.h"
@@ -15,18 +15,17 @@ constexpr int kShWaves = 4;
 constexpr int kShIpt = kScanItems / 256;  // 16 rounds of 64 per wave
 constexpr int kShWaveItems = 64 * kShIpt;
 
-// Ranks owning any of the bin rows ty0..ty1 (band b -> rank b % world).
-__device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, int world) {
-    const uint32_t b0 = ty0 >> kBandShift, b1 = ty1 >> kBandShift;
-    if (b1 - b0 + 1 >= (uint32_t)world) return world >= 32 ? 0xFFFFFFFFu : ((1u << world) - 1u);
+// Ranks owning any of the bin rows ty0..ty1.
+__device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const uint8_t* __restrict__ owner) {
     uint32_t m = 0;
-    for (uint32_t b = b0; b <= b1; ++b) m |= 1u << (b % (uint32_t)world);
+    for (uint32_t by = ty0; by <= ty1; ++by) m |= 1u << owner[by];
     return m;
 }
 
 __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __restrict__ rect_lo,
                                                           const uint32_t* __restrict__ rect_hi, uint32_t n,
-                                                          int world, uint32_t* __restrict__ dest_mask,
+                                                          int world, const uint8_t* __restrict__ owner,
+                                                          uint32_t* __restrict__ dest_mask,
                                                           uint32_t* __restrict__ counts, uint32_t nblocks) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -37,7 +36,7 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __rest
         uint32_t m = 0;
         if (i < n) {
             const uint32_t lo = rect_lo[i], hi = rect_hi[i];
-            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> kBinShift, (hi >> 16) >> kBinShift, world);
+            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> kBinShift, (hi >> 16) >> kBinShift, owner);
         }
         if (i < n) dest_mask[i] = m;
         for (int d = 0; d < world; ++d) {
@@ -138,10 +137,12 @@ __global__ __launch_bounds__(256) void recv_unpack_kernel(const float4* __restri
 }
 
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
+                              const uint8_t* owner,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st) {
     if (world < 1 || world > kMaxWorld) return hipErrorInvalidValue;
     if (nblocks == 0) return hipSuccess;
-    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, dest_mask, counts, nblocks);
+    if (!owner) return hipErrorInvalidValue;
+    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, owner, dest_mask, counts, nblocks);
     return hipGetLastError();
 }
 

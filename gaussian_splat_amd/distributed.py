@@ -1,20 +1,20 @@
-"""Multi-GPU rendering: splat-index shards, band ownership, RCCL exchange.
+"""Multi-GPU rendering: splat-index shards, bin-row ownership, RCCL exchange.
 
 DESIGN.md §6.  One process per GPU.  Rank r holds a contiguous splat-index
-range of the scene and owns the 128-pixel bands b (4 rows of 32x32 bins)
-with b % world == r.
-Per frame:
+range of the scene.  Every 32-pixel bin row has one owning rank; by default
+(`row_owner`) rank r owns a contiguous, balanced range of rows, so few splats
+straddle an ownership boundary.  Per frame:
 
-  1. gs_shard_project   project the local shard on the GPU and pack a 64-B
-                        exchange record for every (visible splat, owning
-                        rank) pair, grouped by destination, index order inside
+  1. gs_shard_project   project the local shard and pack a 64-B exchange
+                        record for every (visible splat, owning rank) pair,
+                        grouped by destination, index order inside
   2. all_to_all         exchange counts, then records (RCCL over xGMI)
   3. gs_shard_render    bin/sort/composite the received records into the
-                        owned bands (a compact band buffer)
-  4. gather             bands -> rank 0, interleaved back into the frame
+                        owned bin rows (a compact band buffer)
+  4. gather             bands -> rank 0, scattered back into the frame
 
 Records arrive in source-rank order = global splat-index order, so each
-owned tile sees exactly the single-GPU list order: the assembled frame is
+owned bin sees exactly the single-GPU list order: the assembled frame is
 bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
 tests/test_distributed.py).  The backend object does the per-rank compute:
 `HipShardBackend` (libgsplat.so) in production; the gloo tests plug in a
@@ -31,38 +31,63 @@ from . import _lib as L
 from .api import InstancedSplatRenderer, Options, Scene, _mat16
 from ._lib import check, lib
 
-ROW = 128  # ownership unit: one 128-pixel band (4 bin rows)
+ROW = 32  # ownership unit: one 32-pixel bin row
 
 
-def band_rows(height: int, world: int) -> int:
+def row_owner(height: int, world: int) -> np.ndarray:
+    """Default owner table (the C-ABI's, gs_shard_set_rows): rank r owns the
+    contiguous bin rows [r*R/world, (r+1)*R/world), R = ceil(height/32)."""
+    R = (height + ROW - 1) // ROW
+    o = np.zeros(R, np.uint8)
+    for r in range(world):
+        o[r * R // world:(r + 1) * R // world] = r
+    return o
+
+
+def band_rows(height: int, world: int, owner=None) -> int:
     """Pixel rows of the (padded, equal-size) band buffer of every rank."""
-    rows = (height + ROW - 1) // ROW
-    return ((rows + world - 1) // world) * ROW
+    o = row_owner(height, world) if owner is None else np.asarray(owner)
+    return int(max((o == r).sum() for r in range(world))) * ROW
 
 
-def assemble(bands, width: int, height: int, world: int):
-    """Interleave rank bands (band r <- bands[r % world], slot r // world) into a frame."""
+def assemble(bands, width: int, height: int, world: int, owner=None):
+    """Scatter the rank bands (owned rows stacked in ascending order) into a frame."""
     import torch
 
-    th = (height + ROW - 1) // ROW
-    frame = torch.zeros((th * ROW, width, 4), dtype=torch.float32, device=bands[0].device)
-    ft = frame.view(th, ROW, width, 4)
+    o = row_owner(height, world) if owner is None else np.asarray(owner)
+    R = len(o)
+    frame = torch.zeros((R * ROW, width, 4), dtype=torch.float32, device=bands[0].device)
     for r, b in enumerate(bands):
-        k = len(range(r, th, world))
-        if k:
-            ft[r::world] = b.view(-1, ROW, width, 4)[:k]
+        rows = np.nonzero(o == r)[0]
+        if len(rows) == 0:
+            continue
+        src = b.view(-1, ROW, width, 4)[: len(rows)]
+        starts = rows.tolist()
+        # contiguous runs of owned rows copy as one block
+        k = 0
+        while k < len(starts):
+            e = k
+            while e + 1 < len(starts) and starts[e + 1] == starts[e] + 1:
+                e += 1
+            frame[starts[k] * ROW:(starts[e] + 1) * ROW] = src[k:e + 1].reshape(-1, width, 4)
+            k = e + 1
     return frame[:height]
 
 
 class HipShardBackend:
     """Per-rank compute through libgsplat.so (device buffers are torch tensors)."""
 
-    def __init__(self, shard: Scene, rank: int, world: int, index_base: int, options: Options, device: int):
+    def __init__(self, shard: Scene, rank: int, world: int, index_base: int, options: Options, device: int,
+                 owner=None):
         import torch
 
         self.r = InstancedSplatRenderer(shard, options)
         self.r.initialize(device)
         check(lib().gs_shard_configure(self.r._h, rank, world, index_base), "gs_shard_configure")
+        self.owner = None if owner is None else np.ascontiguousarray(owner, np.uint8)
+        if self.owner is not None:  # same table on every rank (default: contiguous ranges)
+            check(lib().gs_shard_set_rows(self.r._h, self.owner.ctypes.data, len(self.owner)),
+                  "gs_shard_set_rows")
         self.world, self.rank, self.device = world, rank, torch.device(f"cuda:{device}")
         self.xbytes = int(lib().gs_exchange_record_bytes())
         self.send = torch.empty(max(1, shard.n * world * self.xbytes), dtype=torch.uint8, device=self.device)
@@ -85,7 +110,8 @@ class HipShardBackend:
     def render(self, recv, nrec, width, height):
         import torch
 
-        band = torch.empty((band_rows(height, self.world), width, 4), dtype=torch.float32, device=self.device)
+        band = torch.empty((band_rows(height, self.world, self.owner), width, 4), dtype=torch.float32,
+                           device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         check(lib().gs_shard_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
                                     C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_shard_render")
@@ -153,11 +179,11 @@ class ShardedRenderer:
         else:
             bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
             dist.gather(band, bands, dst=0, group=self.group)
-        return assemble(bands, width, height, self.world) if self.rank == 0 else None
+        return assemble(bands, width, height, self.world, getattr(self.b, "owner", None)) if self.rank == 0 else None
 
 
 def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,
-                          mode: str = "tile", device: int = 0, cap: int = 0) -> np.ndarray:
+                          mode: str = "tile", device: int = 0, cap: int = 0, owner=None) -> np.ndarray:
     """All `world` ranks in one process on one GPU, exchange by slicing —
     the same kernels and record protocol as the multi-process path."""
     import torch
@@ -166,7 +192,7 @@ def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, heig
     backends = []
     for r in range(world):
         b, e = shard_bounds(scene.n, world, r)
-        backends.append(HipShardBackend(scene.subset(slice(b, e)), r, world, b, opts, device))
+        backends.append(HipShardBackend(scene.subset(slice(b, e)), r, world, b, opts, device, owner))
     sends = [be.project(view, proj, width, height) for be in backends]
     xb = backends[0].xbytes
     bands = []
@@ -179,6 +205,6 @@ def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, heig
         recv = torch.cat(parts) if parts else backends[dst].empty(0)
         nrec = recv.numel() // xb
         bands.append(backends[dst].render(recv if recv.numel() else backends[dst].empty(xb), nrec, width, height))
-    frame = assemble(bands, width, height, world)
+    frame = assemble(bands, width, height, world, owner)
     torch.cuda.synchronize()
     return frame.cpu().numpy()

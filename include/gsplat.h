@@ -137,19 +137,29 @@ gs_status gs_sorted_pairs_host(gs_handle *h, uint32_t *keys, uint32_t *vals, int
 gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals,
                               int64_t n, int32_t bits, void *hip_stream);
 
-/* ---- multi-GPU: tile-band ownership across ranks --- */
-/* Shard = contiguous splat-index range [index_base, index_base + n) of the
- * global scene.  Tiles are owned by rank r iff (tile_row % world) == r. */
+/* ---- multi-GPU: bin-row ownership across ranks ----- */
+/* No reference counterpart (the reference is single-GPU Metal).
+ * Shard = contiguous splat-index range [index_base, index_base + n) of the
+ * global scene.  Every 32-px bin row of the frame has one owning rank. */
 gs_status gs_shard_configure(gs_handle *h, int32_t rank, int32_t world, int64_t index_base);
-/* Project the local shard and pack per-destination records into `send`
- * (device memory, capacity `send_cap_bytes`).  Writes world send counts
- * (in records) to host `send_counts`.  Record size: gs_exchange_record_bytes(). */
+/* Bin-row ownership: owner[by] = rank owning 32-px bin row by, for every
+ * bin row of the frame (ceil(height/32) entries).  Default (no table, or
+ * nrows = 0): rank r owns the contiguous rows [r*R/world, (r+1)*R/world).
+ * Every rank must install the same table (e.g. rebalanced from the last
+ * frame's per-row cost). */
+gs_status gs_shard_set_rows(gs_handle *h, const uint8_t *owner, int32_t nrows);
+/* Project the local shard and pack, for every visible splat and every rank
+ * owning a bin row its rect touches, one exchange record into `send`
+ * (device memory, capacity `send_cap_bytes`), grouped by destination, index
+ * order inside.  Writes world send counts (in records) to host `send_counts`.
+ * Record size: gs_exchange_record_bytes(). */
 gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[16], int32_t width,
                            int32_t height, void *send, int64_t send_cap_bytes, int64_t *send_counts,
                            void *hip_stream);
 /* Bin, sort and composite the received records (concatenated in source-rank
- * order) into the owned tiles of out_rgba (device, width*height*4; tiles not
- * owned are left untouched). */
+ * order, i.e. global index order) into this rank's band buffer `out_rgba`
+ * (device): the owned bin rows stacked in ascending order, 32 pixel rows
+ * each, width pixels wide, fp32 RGBA. */
 gs_status gs_shard_render(gs_handle *h, const void *recv, int64_t recv_count, int32_t width, int32_t height,
                           float *out_rgba, void *hip_stream);
 int32_t gs_exchange_record_bytes(void);

@@ -17,7 +17,7 @@
 #endif
 
 #define TILE 16
-#define OWN_ROW 128 /* multi-GPU ownership unit: 128-px bands of 4 bin rows */
+#define OWN_ROW 32 /* multi-GPU ownership unit: 32-px bin rows, owner[by] */
 /* 2*ln(100): exp(-q/2) < 0.01 <=> q > 2 ln 100 (tile.metal:191-195). */
 #define ORA_QMAX 9.21034037197618f
 /* 0.99 saturation (tile.metal:261), 0.01 transmittance (50layer.metal:219). */
@@ -669,7 +669,7 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
 }
 
 int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
-                          const ora_options *opt, int row_mod, int row_rem, int compact, float *out,
+                          const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
                           ora_stats *st) {
     int mode = opt ? opt->mode : ORA_MODE_TILE;
     int cap = opt ? opt->cap : 0;
@@ -677,8 +677,12 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
 #ifdef _OPENMP
     if (nth > 0) omp_set_num_threads(nth);
 #endif
-    if (row_mod < 1) row_mod = 1;
     int TW = (W + TILE - 1) / TILE, TH = (H + TILE - 1) / TILE, T = TW * TH;
+    /* ownership of 32-px rows; slot[r] = position of owned row r in the band buffer */
+    int NR = (H + OWN_ROW - 1) / OWN_ROW;
+    int *slot = (int *)malloc(sizeof(int) * (size_t)(NR > 0 ? NR : 1));
+    for (int r = 0, k = 0; r < NR; ++r) slot[r] = (!owner || owner[r] == rank) ? k++ : -1;
+#define ORA_OWNED(ty) (slot[((ty) * TILE) / OWN_ROW] >= 0)
     /* Oracle binning uses the record rect widened by 2 px, so a too-tight
      * product rect shows up as a framebuffer mismatch.  Records with a zero
      * rect (rect_hi == 0 && rect_lo == 0 && opacity == 0) are culled. */
@@ -698,7 +702,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
                  ((rec[i].rect_hi >> 16) / TILE - (rec[i].rect_lo >> 16) / TILE + 1);
         ORA_RECT(i, x0, y0, x1, y1)
         for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
-            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
+            if (!ORA_OWNED(ty)) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) cnt[ty * TW + tx + 1]++;
         }
     }
@@ -711,7 +715,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
         if (!dkey[i] && !rec[i].rect_hi && !rec[i].opacity) continue;
         ORA_RECT(i, x0, y0, x1, y1)
         for (int ty = y0 / TILE; ty <= y1 / TILE; ++ty) {
-            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
+            if (!ORA_OWNED(ty)) continue;
             for (int tx = x0 / TILE; tx <= x1 / TILE; ++tx) list[cur[ty * TW + tx]++] = (uint32_t)i;
         }
     }
@@ -731,7 +735,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
 #endif
         for (int t = 0; t < T; ++t) {
             int tx = t % TW, ty = t / TW;
-            if ((ty * TILE / OWN_ROW) % row_mod != row_rem) continue;
+            if (!ORA_OWNED(ty)) continue;
             int64_t b = cnt[t], e = cnt[t + 1], m = e - b;
             if ((size_t)m > kcap) {
                 kcap = (size_t)m;
@@ -747,7 +751,7 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
              * arrival (index) order. */
             if (cap == 0) qsort(ord, (size_t)m, sizeof(kv), kv_cmp);
             for (int py = ty * TILE; py < ty * TILE + TILE && py < H; ++py) {
-                int orow = compact ? ((py / OWN_ROW) / row_mod) * OWN_ROW + py % OWN_ROW : py;
+                int orow = compact ? slot[py / OWN_ROW] * OWN_ROW + py % OWN_ROW : py;
                 for (int px = tx * TILE; px < tx * TILE + TILE && px < W; ++px) {
                     float *o = out + ((size_t)orow * W + px) * 4;
                     int c = 0;
@@ -807,6 +811,8 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
         st->pairs = pairs;
         st->tiles = T;
     }
+#undef ORA_OWNED
+    free(slot);
     free(list);
     free(cnt);
     return 1;
@@ -819,7 +825,7 @@ int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, 
     uint32_t *dkey = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
     uint32_t *nt = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
     ora_project_all(s, V, P, W, H, rec, dkey, nt, opt ? opt->nthreads : 0);
-    int ok = ora_composite_records(rec, dkey, n, W, H, opt, 1, 0, 0, out, st);
+    int ok = ora_composite_records(rec, dkey, n, W, H, opt, NULL, 0, 0, out, st);
     free(rec);
     free(dkey);
     free(nt);

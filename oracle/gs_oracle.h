@@ -125,11 +125,12 @@ int ora_render(const ora_scene *s, const float view[16], const float proj[16], i
                int height, const ora_options *opt, float *out_rgba, ora_stats *stats);
 
 /* Bin, sort (S1) and composite an explicit record list (index = arrival
- * order) into the 128-px pixel-row bands b = py / 128 with b % row_mod ==
- * row_rem; compact = 1 writes those bands stacked (the multi-GPU layout).  Culled records are
- * all-zero (dkey 0, rect_hi 0, opacity 0). */
+ * order) into the 32-px pixel rows r (r = py / 32) with owner[r] == rank
+ * (owner == NULL: every row); compact = 1 writes the owned rows stacked in
+ * ascending order (the multi-GPU band layout).  Culled records are all-zero
+ * (dkey 0, rect_hi 0, opacity 0). */
 int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int width, int height,
-                          const ora_options *opt, int row_mod, int row_rem, int compact, float *out,
+                          const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
                           ora_stats *stats);
 
 /* Composite a single synthetic fragment list (depth, rgb, alpha) with the S1

@@ -59,7 +59,7 @@ def lib() -> C.CDLL:
                                  C.POINTER(OraOptions), C.c_void_p, C.POINTER(OraStats)]
         L.ora_render.restype = C.c_int
         L.ora_composite_records.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int,
-                                            C.POINTER(OraOptions), C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.POINTER(OraOptions), C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                             C.POINTER(OraStats)]
         L.ora_composite_records.restype = C.c_int
         L.ora_composite_list.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -155,19 +155,20 @@ def render(scene, view, proj, width, height, sh_degree=0, mode="tile", cap=0, nt
     return out, {"visible": st.visible, "pairs": st.pairs, "tiles": st.tiles}
 
 
-def composite_records(rec, dkey, width, height, row_mod=1, row_rem=0, compact=False, mode="tile", cap=0,
+def composite_records(rec, dkey, width, height, owner=None, rank=0, compact=False, mode="tile", cap=0,
                       nthreads=0):
-    """Bin/sort/composite an explicit record list (index = arrival order)."""
+    """Bin/sort/composite an explicit record list (index = arrival order).
+    owner: uint8 per 32-px row (None = all rows owned)."""
     rec = np.ascontiguousarray(rec, RECORD_DTYPE)
     dkey = np.ascontiguousarray(dkey, np.uint32)
-    nb = (height + 127) // 128  # 128-px ownership bands
-    rows = ((nb + row_mod - 1) // row_mod) * 128 if compact else height
+    own = None if owner is None else np.ascontiguousarray(owner, np.uint8)
+    rows = int((own == rank).sum()) * 32 if (compact and own is not None) else height
     out = np.zeros((rows, width, 4), np.float32)
     o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
     st = OraStats()
     lib().ora_composite_records(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
-                                C.byref(o), int(row_mod), int(row_rem), int(bool(compact)), out.ctypes.data,
-                                C.byref(st))
+                                C.byref(o), None if own is None else own.ctypes.data, int(rank),
+                                int(bool(compact)), out.ctypes.data, C.byref(st))
     return out
 
 

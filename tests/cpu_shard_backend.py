@@ -1,7 +1,7 @@
 """CPU stand-in for HipShardBackend (test infrastructure).
 
 Per-rank compute by the oracle; the 64-B exchange record format, the
-destination rule (128-px band % world) and the band layout are the product's,
+destination rule (bin-row owner table) and the band layout are the product's,
 so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer exercise the
 real exchange / gather / assembly protocol on CPU.
 """
@@ -23,15 +23,21 @@ class OracleShardBackend:
     def project(self, view, proj, width, height):
         import torch
 
+        from gaussian_splat_amd.distributed import row_owner
+
         rec, dk, nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
         vis = nt > 0
-        ty0 = (rec["rect_lo"] >> 16) >> 7  # 128-px ownership bands
-        ty1 = (rec["rect_hi"] >> 16) >> 7
+        owner = row_owner(height, self.world)
+        ty0 = (rec["rect_lo"] >> 16) >> 5  # 32-px bin rows
+        ty1 = (rec["rect_hi"] >> 16) >> 5
         w = self.world
         parts, counts = [], []
         for d in range(w):
-            first = ty0 + (d + w - ty0 % w) % w
-            idx = np.nonzero(vis & (first <= ty1))[0]
+            rows = np.nonzero(owner == d)[0]
+            touch = np.zeros(len(nt), bool)
+            if len(rows):  # a rank owns a contiguous range [rows[0], rows[-1]]
+                touch = (ty0 <= rows[-1]) & (ty1 >= rows[0])
+            idx = np.nonzero(vis & touch)[0]
             x = np.zeros(len(idx), XREC)
             for f in O.RECORD_DTYPE.names:
                 x[f] = rec[f][idx]
@@ -51,6 +57,10 @@ class OracleShardBackend:
             rec[f] = raw[f]
         # received order must be global index order (tie rule); check it
         assert np.all(np.diff(raw["gidx"].astype(np.int64)) > 0)
-        band = O.composite_records(rec, raw["dkey"], width, height, row_mod=self.world, row_rem=self.rank,
-                                   compact=True, mode=self.mode, cap=self.cap)
+        from gaussian_splat_amd.distributed import band_rows, row_owner
+
+        band = np.zeros((band_rows(height, self.world), width, 4), np.float32)
+        out = O.composite_records(rec, raw["dkey"], width, height, owner=row_owner(height, self.world),
+                                  rank=self.rank, compact=True, mode=self.mode, cap=self.cap)
+        band[: out.shape[0]] = out
         return torch.from_numpy(band)

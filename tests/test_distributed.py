@@ -1,4 +1,4 @@
-"""Multi-rank protocol on CPU with gloo: splat-index shards, band
+"""Multi-rank protocol on CPU with gloo: splat-index shards, bin-row
 ownership, all_to_all record exchange, band gather + assembly.  The
 assembled frame must equal the single-process oracle frame bit for bit."""
 import os
@@ -67,16 +67,27 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
 
 
 def test_assemble_layout():
+    import numpy as np
     import torch
-    from gaussian_splat_amd.distributed import assemble, band_rows
-    w, h, world = 40, 560, 3  # 5 bands of 128 px (last one partial), uneven split 2/2/1
+    from gaussian_splat_amd.distributed import assemble, band_rows, row_owner
+    w, h, world = 40, 140, 3  # 5 bin rows of 32 px (the last partial), owners 0,1,1,2,2
+    owner = row_owner(h, world)
+    assert owner.tolist() == [0, 1, 1, 2, 2]
     frame = torch.arange(h * w * 4, dtype=torch.float32).view(h, w, 4)
-    th = 5
     bands = []
     for r in range(world):
         b = torch.zeros(band_rows(h, world), w, 4)
-        for k, ty in enumerate(range(r, th, world)):
-            rows = frame[ty * 128: min(h, ty * 128 + 128)]
-            b[k * 128: k * 128 + rows.shape[0]] = rows
+        for k, ty in enumerate(np.nonzero(owner == r)[0]):
+            rows = frame[ty * 32: min(h, ty * 32 + 32)]
+            b[k * 32: k * 32 + rows.shape[0]] = rows
         bands.append(b)
     torch.testing.assert_close(assemble(bands, w, h, world), frame, rtol=0, atol=0)
+    custom = np.array([2, 1, 0, 1, 2], np.uint8)  # any table works
+    bands = []
+    for r in range(world):
+        b = torch.zeros(band_rows(h, world, custom), w, 4)
+        for k, ty in enumerate(np.nonzero(custom == r)[0]):
+            rows = frame[ty * 32: min(h, ty * 32 + 32)]
+            b[k * 32: k * 32 + rows.shape[0]] = rows
+        bands.append(b)
+    torch.testing.assert_close(assemble(bands, w, h, world, custom), frame, rtol=0, atol=0)

@@ -229,8 +229,8 @@ def test_ply_dropin_path(built, tmp_path):
     assert _compare(img, ref) == (0.0, 0)
 
 
-@pytest.mark.parametrize("world,cap", [(2, 0), (3, 0), (3, 32)])
-def test_virtual_shards_bitexact(built, world, cap):
+@pytest.mark.parametrize("world,cap,table", [(2, 0, None), (3, 0, None), (3, 32, None), (4, 0, "interleaved")])
+def test_virtual_shards_bitexact(built, world, cap, table):
     """K virtual ranks on one GPU through gs_shard_project/gs_shard_render
     reassemble the single-GPU frame bit for bit (SURVEY §8e verification);
     with a fragment cap, arrival order survives the exchange."""
@@ -243,7 +243,10 @@ def test_virtual_shards_bitexact(built, world, cap):
     full.set_cap(cap)
     V, P = orbit_views(W, H, 1)[0]
     ref = full.render_host(V, P, W, H)
-    img = D.render_virtual_shards(sc, world, V, P, W, H, sh_degree=3, cap=cap)
+    owner = None
+    if table == "interleaved":  # a custom gs_shard_set_rows table
+        owner = (np.arange((H + 31) // 32) % world).astype(np.uint8)[::-1].copy()
+    img = D.render_virtual_shards(sc, world, V, P, W, H, sh_degree=3, cap=cap, owner=owner)
     assert _compare(img, ref) == (0.0, 0)
 
 
