@@ -717,8 +717,10 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
                            int64_t send_cap_bytes, int64_t* send_counts, void* stream) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if (!view || !proj || !send_counts || W <= 0 || H <= 0 || W > 65535 || H > 65535)
+    if (!view || !proj || !send_counts || W <= 0 || H <= 0)
         return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
+    if (W > gs::kXMaxDim || H > gs::kXMaxDim)
+        return fail(GS_ERR_UNSUPPORTED, "multi-GPU frames are limited to 4096 x 4096 (packed exchange record)");
     hipStream_t st = static_cast<hipStream_t>(stream);
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
@@ -753,17 +755,17 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
                                     std::to_string(total * gs_exchange_record_bytes()) + " bytes needed)");
     if (total > 0 && !send) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: null send buffer");
     GS_HIP(gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
-                                 (uint32_t)h->index_base, h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
+                                 h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
                                  static_cast<float4*>(send), st));
     return GS_OK;
 }
 
-gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
+gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
                           void* stream) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !out_rgba || W <= 0 || H <= 0 || W > 65535 ||
-        H > 65535)
+    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !out_rgba || W <= 0 || H <= 0 ||
+        W > gs::kXMaxDim || H > gs::kXMaxDim)
         return fail(GS_ERR_INVALID_ARG, "gs_shard_render: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
@@ -774,7 +776,7 @@ gs_status gs_shard_render(gs_handle* h, const void* recv, int64_t m, int32_t W, 
     GS_HIP(h->rdkey.reserve(mm * 4));
     GS_HIP(h->rrlo.reserve(mm * 4));
     GS_HIP(h->rrhi.reserve(mm * 4));
-    const float4* rv = static_cast<const float4*>(recv);
+    float4* rv = static_cast<float4*>(recv);
     mark(h, 8, st);
     GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));

@@ -88,7 +88,8 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st);
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 
 // ---- shard.hip (multi-GPU tile-row ownership) ------------------------------
-constexpr int kXRecFloat4 = 4;  // 64-B exchange record: 48-B record + dkey, global index
+constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the record, depth key packed into the rect words
+constexpr int kXMaxDim = 4096;  // frame limit of the packed rect (12-bit coordinates)
 constexpr int kMaxWorld = 32;
 // dest_mask[i]: bit r set iff splat i touches a bin row owned by rank r (owner[by]).
 // counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
@@ -99,9 +100,9 @@ hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, 
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);
 // Pack exchange records grouped by destination, splat-index order inside.
 hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
-                             int world, uint32_t index_base, const uint32_t* counts, const uint32_t* dest_total,
+                             int world, const uint32_t* counts, const uint32_t* dest_total,
                              uint32_t nblocks, float4* send, hipStream_t st);
 // Unpack dkey and packed rect of every received exchange record.
-hipError_t launch_recv_unpack(const float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+hipError_t launch_recv_unpack(float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
                               uint32_t* rect_hi, hipStream_t st);
 }  // namespace gs

@@ -2,7 +2,7 @@
 //
 // Scenes are sharded by splat index (rank r holds a contiguous index range).
 // Every 32-px bin row has an owning rank (owner[by]): every
-// rank projects its shard, then sends each visible splat's 64-B exchange
+// rank projects its shard, then sends each visible splat's 48-B exchange
 // record to the ranks owning a bin row its rect touches.  Received records arrive in source-rank order,
 // i.e. in global index order, so the receiving rank's stable sort reproduces
 // the single-GPU per-tile order exactly (bit-identical composite).
@@ -10,6 +10,15 @@
 #include "gs_wave.h"
 
 namespace gs {
+
+// 48-B exchange record = the 48-B record with its rect words repacked as
+// x (12 bits) | y (12 bits) << 12 | 8 bits of the 15-bit depth key << 24
+// (low byte in the lo word, high 7 bits in the hi word).  Frames up to
+// kXMaxDim x kXMaxDim (4K UHD included).
+__device__ __forceinline__ uint32_t xrect_pack(uint32_t xy, uint32_t key8) {
+    return (xy & 0xFFFu) | (((xy >> 16) & 0xFFFu) << 12) | (key8 << 24);
+}
+__device__ __forceinline__ uint32_t xrect_unpack(uint32_t p) { return (p & 0xFFFu) | (((p >> 12) & 0xFFFu) << 16); }
 
 constexpr int kShWaves = 4;
 constexpr int kShIpt = kScanItems / 256;  // 16 rounds of 64 per wave
@@ -71,8 +80,7 @@ __global__ __launch_bounds__(256) void rows_scan_kernel(uint32_t* __restrict__ c
 __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restrict__ rec,
                                                          const uint32_t* __restrict__ dkey,
                                                          const uint32_t* __restrict__ dest_mask, uint32_t n,
-                                                         int world, uint32_t index_base,
-                                                         const uint32_t* __restrict__ counts,
+                                                         int world, const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ dest_total,
                                                          uint32_t nblocks, float4* __restrict__ send) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];   // per-wave counts -> per-wave offsets
@@ -114,26 +122,35 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
                 uint32_t pos = base_d[d] + run + mbcnt(b);
                 const float4* src = rec + 3 * (size_t)i;
                 float4* dst = send + (size_t)kXRecFloat4 * pos;
+                const float4 c = src[2];
+                const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w), dk = dkey[i];
                 dst[0] = src[0];
                 dst[1] = src[1];
-                dst[2] = src[2];
-                dst[3] = make_float4(__uint_as_float(dkey[i]), __uint_as_float(index_base + i), 0.0f, 0.0f);
+                dst[2] = make_float4(c.x, c.y, __uint_as_float(xrect_pack(lo, dk & 0xFFu)),
+                                     __uint_as_float(xrect_pack(hi, dk >> 8)));
             }
             if (lane == 0) wc[wave][d] = run + (uint32_t)__popcll(b);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void recv_unpack_kernel(const float4* __restrict__ recv, uint32_t m,
+// Decode the received records in place: the packed rect words become the
+// standard (x | y << 16) ones, so the composite reads them like local records.
+__global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ recv, uint32_t m,
                                                           uint32_t* __restrict__ dkey, uint32_t* __restrict__ rect_lo,
                                                           uint32_t* __restrict__ rect_hi) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= m) return;
-    const float4* r = recv + (size_t)kXRecFloat4 * i;
-    const float4 c = r[2];
-    dkey[i] = __float_as_uint(r[3].x);
-    rect_lo[i] = __float_as_uint(c.z);
-    rect_hi[i] = __float_as_uint(c.w);
+    float4* r = recv + (size_t)kXRecFloat4 * i;
+    float4 c = r[2];
+    const uint32_t plo = __float_as_uint(c.z), phi = __float_as_uint(c.w);
+    const uint32_t lo = xrect_unpack(plo), hi = xrect_unpack(phi);
+    dkey[i] = (plo >> 24) | ((phi >> 24) << 8);
+    rect_lo[i] = lo;
+    rect_hi[i] = hi;
+    c.z = __uint_as_float(lo);
+    c.w = __uint_as_float(hi);
+    r[2] = c;
 }
 
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
@@ -153,15 +170,14 @@ hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32
 }
 
 hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
-                             int world, uint32_t index_base, const uint32_t* counts, const uint32_t* dest_total,
+                             int world, const uint32_t* counts, const uint32_t* dest_total,
                              uint32_t nblocks, float4* send, hipStream_t st) {
     if (nblocks == 0) return hipSuccess;
-    shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, dkey, dest_mask, n, world, index_base, counts, dest_total,
-                                               nblocks, send);
+    shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, dkey, dest_mask, n, world, counts, dest_total, nblocks, send);
     return hipGetLastError();
 }
 
-hipError_t launch_recv_unpack(const float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+hipError_t launch_recv_unpack(float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
                               uint32_t* rect_hi, hipStream_t st) {
     if (m == 0) return hipSuccess;
     recv_unpack_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, dkey, rect_lo, rect_hi);

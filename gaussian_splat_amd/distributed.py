@@ -5,7 +5,7 @@ range of the scene.  Every 32-pixel bin row has one owning rank; by default
 (`row_owner`) rank r owns a contiguous, balanced range of rows, so few splats
 straddle an ownership boundary.  Per frame:
 
-  1. gs_shard_project   project the local shard and pack a 64-B exchange
+  1. gs_shard_project   project the local shard and pack a 48-B exchange
                         record for every (visible splat, owning rank) pair,
                         grouped by destination, index order inside
   2. all_to_all         exchange counts, then records (RCCL over xGMI)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 1
+#define GSPLAT_ABI_VERSION 2
 
 typedef enum {
     GS_OK = 0,
@@ -159,8 +159,10 @@ gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[
 /* Bin, sort and composite the received records (concatenated in source-rank
  * order, i.e. global index order) into this rank's band buffer `out_rgba`
  * (device): the owned bin rows stacked in ascending order, 32 pixel rows
- * each, width pixels wide, fp32 RGBA. */
-gs_status gs_shard_render(gs_handle *h, const void *recv, int64_t recv_count, int32_t width, int32_t height,
+ * each, width pixels wide, fp32 RGBA.  `recv` (device) is decoded in place.
+ * Multi-GPU frames are limited to 4096 x 4096 (the exchange record packs
+ * 12-bit rect coordinates with the depth key). */
+gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height,
                           float *out_rgba, void *hip_stream);
 int32_t gs_exchange_record_bytes(void);
 

@@ -1,6 +1,6 @@
 """CPU stand-in for HipShardBackend (test infrastructure).
 
-Per-rank compute by the oracle; the 64-B exchange record format, the
+Per-rank compute by the oracle; the 48-B exchange record format, the
 destination rule (bin-row owner table) and the band layout are the product's,
 so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer exercise the
 real exchange / gather / assembly protocol on CPU.
@@ -9,12 +9,20 @@ import numpy as np
 
 from oracle import oracle_py as O
 
-XREC = np.dtype(O.RECORD_DTYPE.descr + [("dkey", "<u4"), ("gidx", "<u4"), ("pad0", "<u4"), ("pad1", "<u4")])
-assert XREC.itemsize == 64
+XREC = O.RECORD_DTYPE  # 48-B exchange record: rect words repacked with the depth key
+assert XREC.itemsize == 48
+
+
+def _xpack(xy, key8):
+    return (xy & 0xFFF) | (((xy >> 16) & 0xFFF) << 12) | (key8.astype(np.uint32) << 24)
+
+
+def _xunpack(p):
+    return (p & 0xFFF) | (((p >> 12) & 0xFFF) << 16)
 
 
 class OracleShardBackend:
-    xbytes = 64
+    xbytes = 48
 
     def __init__(self, shard, rank, world, index_base, sh_degree=0, mode="tile", cap=0):
         self.shard, self.rank, self.world, self.base = shard, rank, world, index_base
@@ -38,11 +46,9 @@ class OracleShardBackend:
             if len(rows):  # a rank owns a contiguous range [rows[0], rows[-1]]
                 touch = (ty0 <= rows[-1]) & (ty1 >= rows[0])
             idx = np.nonzero(vis & touch)[0]
-            x = np.zeros(len(idx), XREC)
-            for f in O.RECORD_DTYPE.names:
-                x[f] = rec[f][idx]
-            x["dkey"] = dk[idx]
-            x["gidx"] = idx + self.base
+            x = rec[idx].copy()
+            x["rect_lo"] = _xpack(rec["rect_lo"][idx], dk[idx] & 0xFF)
+            x["rect_hi"] = _xpack(rec["rect_hi"][idx], dk[idx] >> 8)
             parts.append(x)
             counts.append(len(idx))
         buf = np.concatenate(parts).view(np.uint8) if parts else np.zeros(0, np.uint8)
@@ -51,16 +57,15 @@ class OracleShardBackend:
     def render(self, recv, nrec, width, height):
         import torch
 
-        raw = recv.numpy()[: nrec * 64].copy().view(XREC)
-        rec = np.zeros(nrec, O.RECORD_DTYPE)
-        for f in O.RECORD_DTYPE.names:
-            rec[f] = raw[f]
-        # received order must be global index order (tie rule); check it
-        assert np.all(np.diff(raw["gidx"].astype(np.int64)) > 0)
+        raw = recv.numpy()[: nrec * 48].copy().view(XREC)
+        rec = raw.copy()
+        dkey = (raw["rect_lo"] >> 24) | ((raw["rect_hi"] >> 24) << 8)
+        rec["rect_lo"] = _xunpack(raw["rect_lo"])
+        rec["rect_hi"] = _xunpack(raw["rect_hi"])
         from gaussian_splat_amd.distributed import band_rows, row_owner
 
         band = np.zeros((band_rows(height, self.world), width, 4), np.float32)
-        out = O.composite_records(rec, raw["dkey"], width, height, owner=row_owner(height, self.world),
+        out = O.composite_records(rec, dkey, width, height, owner=row_owner(height, self.world),
                                   rank=self.rank, compact=True, mode=self.mode, cap=self.cap)
         band[: out.shape[0]] = out
         return torch.from_numpy(band)

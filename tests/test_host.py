@@ -23,8 +23,8 @@ def test_library_exports_every_declared_symbol(built):
     for name in sorted(declared):
         assert hasattr(L, name), name
     assert set(_lib.SIGNATURES) == declared
-    assert L.gs_abi_version() == 1
-    assert L.gs_exchange_record_bytes() == 64
+    assert L.gs_abi_version() == 2
+    assert L.gs_exchange_record_bytes() == 48
 
 
 def test_errors_are_reported_not_thrown(built):
