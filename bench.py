@@ -91,7 +91,7 @@ def cpu_baseline(scene, view, proj, w, h, sh, sample, seconds):
 
 
 STAGE_KERNEL = {"preprocess": "preprocess_kernel", "depth_sort": "rts_pass_kernel<3>", "scan": "scan_down_kernel",
-                "duplicate": "duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "tile_ranges_kernel",
+                "duplicate": "duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "rts_pass_kernel<1>",
                 "composite": "composite_kernel"}
 
 

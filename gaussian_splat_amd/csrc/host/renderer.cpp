@@ -318,19 +318,19 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, own.dev,
                                 h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
     if (timed) mark(h, 4, st);
-    // stable sort by bin id only
+    // stable sort by bin id only; the last pass also writes the bin ranges
     const int bits = bits_for(T);
     bool in_tmp = false;
+    GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), st));
     GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
                                  h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
-                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st));
+                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>()));
     uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
     uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
     h->last_keys = sk;
     h->last_vals = sv;
     if (timed) mark(h, 5, st);
-    GS_HIP(gs::launch_tile_ranges(sk, (uint32_t)P, h->ranges.as<uint2>(), T, st));
-    if (timed) mark(h, 6, st);
+    if (timed) mark(h, 6, st);  // (ranges come out of the last sort pass)
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
     *vals_out = sv;

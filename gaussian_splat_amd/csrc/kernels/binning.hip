@@ -8,7 +8,7 @@
 // bin's list in S1 order: 2 digit passes over P (11 bin bits at 1080p)
 // instead of 4 over a 28-bit (tile, depth) key, and ~half the pairs of
 // 16x16 binning.
-// tile_ranges: boundary detection on the bin-sorted keys -> [start, end).
+// The bin ranges [start, end) come out of the last sort pass (radix_sort.hip).
 #include "gs_kernels.h"
 
 namespace gs {
@@ -39,36 +39,11 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void tile_ranges_kernel(const uint32_t* __restrict__ keys, uint32_t npairs,
-                                                          uint2* __restrict__ ranges) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= npairs) return;
-    const uint32_t t = keys[i];
-    if (i == 0) {
-        ranges[t].x = 0;
-    } else {
-        const uint32_t p = keys[i - 1];
-        if (p != t) {
-            ranges[p].y = i;
-            ranges[t].x = i;
-        }
-    }
-    if (i == npairs - 1) ranges[t].y = npairs;
-}
-
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                             const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
                             uint32_t* keys, uint32_t* vals, hipStream_t st) {
     if (n == 0) return hipSuccess;
     duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(order, rect_lo, rect_hi, offsets, n, tiles_x, own, keys, vals);
-    return hipGetLastError();
-}
-
-hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* ranges, uint32_t ntiles_total,
-                              hipStream_t st) {
-    hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles_total, st);
-    if (e != hipSuccess || npairs == 0) return e;
-    tile_ranges_kernel<<<(npairs + 255) / 256, 256, 0, st>>>(keys, npairs, ranges);
     return hipGetLastError();
 }
 

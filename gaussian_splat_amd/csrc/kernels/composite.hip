@@ -6,14 +6,13 @@
 // consecutive workgroups on one XCD and share the bin list through its L2.
 // The list is streamed through LDS in batches of 256 records (one 48-B record
 // gathered per lane), software-pipelined: the next batch is in flight into
-// registers while the current one is composited.  Per batch each wave keeps the records whose rect
-// overlaps its quadrant AND whose gaussian ellipse q <= 2 ln 100 intersects
-// the parallelogram the quadrant's pixel centres map to in (u, v) space (an
-// exact point-to-parallelogram distance with a relative safety margin, so the
-// test is conservative).
-// Every wave compacts that list, 64 records per ballot, then walks only
-// it: coverage (K6 closed form), gaussian + 0.01 cutoff (F1, tile.metal:191-197) and the composite
-// (A1, tile.metal:251-266; or the live 50-layer rule, 50layer.metal:208-222).
+// registers while the current one is composited.  Per batch every wave
+// compacts the records whose pixel rect overlaps its quadrant (64 per
+// ballot) and walks only those, two at a time with both records' LDS reads
+// issued first: coverage (K6 closed form), gaussian + 0.01 cutoff (F1,
+// tile.metal:191-197) and the composite (A1, tile.metal:251-266; or the live
+// 50-layer rule, 50layer.metal:208-222).  A finer per-quadrant ellipse test
+// was measured and removed: it cost more VALU than the bodies it skipped.
 // The per-pixel body is branch-free (a non-covering splat contributes an
 // exact zero), a wave leaves the batch once all 64 of its pixels are
 // saturated, and the workgroup stops fetching once all 256 are.
@@ -24,42 +23,11 @@
 
 namespace gs {
 
-// Can the support of the splat (record a = (cx, cy, ax, ay), b = (bx, by, ..))
-// reach any pixel centre of the 8x8 quadrant with top-left pixel (X0, Y0)?
-// Pixel centre p maps to (u, v) = (d.A, d.B), d = (px+0.5-cx, cy-(py+0.5));
-// the quadrant maps to the parallelogram p0 + s gu + t gv, s, t in [0, 1].
-__device__ __forceinline__ bool ellipse_reaches_quadrant(const float4& a, const float4& b, float X0, float Y0) {
-    const float dx0 = (X0 + 0.5f) - a.x, dy0 = a.y - (Y0 + 0.5f);
-    const float pu = dx0 * a.z + dy0 * a.w, pv = dx0 * b.x + dy0 * b.y;  // p0
-    const float gu_u = 7.0f * a.z, gu_v = 7.0f * b.x;                     // +7 px in x
-    const float gv_u = -7.0f * a.w, gv_v = -7.0f * b.y;                   // +7 px in y (dy decreases)
-    // origin inside the parallelogram?
-    // approximate reciprocals are fine: both decisions carry a safety margin
-    const float det = gu_u * gv_v - gu_v * gv_u;
-    const float idet = __builtin_amdgcn_rcpf(det);
-    const float s = (gv_u * pv - gv_v * pu) * idet;  // solves p0 + s gu + t gv = 0
-    const float t = (gu_v * pu - gu_u * pv) * idet;
-    const float tol = 1e-3f;
-    bool hit = s >= -tol && s <= 1.0f + tol && t >= -tol && t <= 1.0f + tol;
-    // squared distance from the origin to each edge segment
-    auto seg = [](float px, float py, float gx, float gy) {
-        const float gg = gx * gx + gy * gy;
-        float k = -(px * gx + py * gy) * __builtin_amdgcn_rcpf(gg);
-        k = fminf(fmaxf(k, 0.0f), 1.0f);
-        const float x = px + k * gx, y = py + k * gy;
-        return x * x + y * y;
-    };
-    const float m = fminf(fminf(seg(pu, pv, gu_u, gu_v), seg(pu, pv, gv_u, gv_v)),
-                          fminf(seg(pu + gv_u, pv + gv_v, gu_u, gu_v), seg(pu + gu_u, pv + gu_v, gv_u, gv_v)));
-    hit = hit || m <= kQMax * 1.001f + 1e-3f;
-    return hit || !(det == det);  // NaN guard: keep
-}
-
 // MODE 0: tile rule, 1: live50 rule, 2: cap threshold pass (index-ordered
 // lists; per pixel the id of the a.cap-th covering fragment).  CAP: composite
 // only fragments with id <= thr[pixel] (the first a.cap in arrival order).
 template <int MODE, bool CAP>
-__global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_t nwg) {
+__global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
     __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
     __shared__ uint32_t sid[kIds ? kTileThreads : 1];
@@ -93,7 +61,7 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
     const float fx = (float)px + 0.5f;
     const float fy = (float)py + 0.5f;
 
-    const uint2 rg = a.ranges[by * a.tiles_x + bx];
+    const uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
     float A = 0.0f;  // tile rule: accumulated alpha
     float T = 1.0f;  // live50 rule: transmittance
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -126,6 +94,16 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
             T = in ? T * (1.0f - alpha) : T;
             done = done || T < kTMin;
         }
+    };
+
+    auto body_v = [&](const float4 aa, const float4 bb, const float4 cc, uint32_t id) {
+        const float dx = fx - aa.x;
+        const float dy = aa.y - fy;
+        const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
+        const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
+        const float qq = __builtin_fmaf(v, v, u * u);
+        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+        step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, id);
     };
 
     auto body = [&](uint32_t k) {
@@ -198,7 +176,6 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
                     const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
                     hit = !((hi >> 16) < qy0 || (lo >> 16) > qy0 + 7u || (hi & 0xFFFFu) < qx0 ||
                             (lo & 0xFFFFu) > qx0 + 7u);
-                    if (hit) hit = ellipse_reaches_quadrant(s0[k], s1[k], (float)qx0, (float)qy0);
                 }
                 const uint64_t m = __ballot(hit);
                 if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
@@ -210,8 +187,17 @@ __global__ __launch_bounds__(256) void composite_kernel(CompositeArgs a, uint32_
         for (; i + 1 < nl; i += 2) {
             if (__ballot(!done) == 0) break;
             const uint32_t k0 = wlist[wave][i], k1 = wlist[wave][i + 1];
-            body(k0);
-            body(k1);
+            if constexpr (MODE == 2) {
+                body(k0);
+                body(k1);
+            } else {
+                // both records' LDS reads issue before either update
+                const float4 a0 = s0[k0], b0 = s1[k0], c0 = s2[k0];
+                const float4 a1 = s0[k1], b1 = s1[k1], c1 = s2[k1];
+                const uint32_t i0 = kIds ? sid[k0] : 0u, i1 = kIds ? sid[k1] : 0u;
+                body_v(a0, b0, c0, i0);
+                body_v(a1, b1, c1, i1);
+            }
         }
         if (i < nl && __ballot(!done) != 0) body(wlist[wave][i]);
     }

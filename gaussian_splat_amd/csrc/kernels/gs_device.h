@@ -86,6 +86,9 @@ __device__ __forceinline__ uint32_t half_bits(float f) {
 // splat carries the empty rect (lo = 0xFFFFFFFF, hi = 0).
 constexpr uint32_t kEmptyRectLo = 0xFFFFFFFFu;
 
+// Bin ranges as written by the last bin-sort pass: {start, ~end}.
+__device__ __forceinline__ uint2 decode_range(uint2 r) { return make_uint2(r.x, ~r.y); }
+
 // Multi-GPU ownership: every 32-px bin row has one owning
 // rank, owner[by].  The default table gives each rank a contiguous, balanced
 // range of bin rows (few splats straddle a boundary, so the record exchange

@@ -31,9 +31,6 @@ hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                             const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
                             uint32_t* keys, uint32_t* vals, hipStream_t st);
-// ranges[tile] = [start, end) in the tile-sorted pair array (zeroed here).
-hipError_t launch_tile_ranges(const uint32_t* keys, uint32_t npairs, uint2* ranges, uint32_t ntiles_total,
-                              hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
 constexpr int kSortTile = 8192;  // items per sort tile (512 lanes x 16)
@@ -52,9 +49,12 @@ size_t radix_sort_scratch_words(uint32_t n);
 // may be null (value = index) — and leaves the result in (keys, vals), or in
 // (tmp_keys, tmp_vals) when *result_in_tmp (only if the inputs alias the
 // outputs and the pass count is odd).
+// ranges (optional): key-value extents of the sorted output, stored as
+// {start, ~end} (fill with 0xFF before; empty key = {~0, ~0}); see
+// decode_range.
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
-                             bool* result_in_tmp, hipStream_t st);
+                             bool* result_in_tmp, hipStream_t st, uint2* ranges = nullptr);
 // Same with three value arrays (vals_in[0] may be null: value = index).
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,

@@ -110,10 +110,15 @@ __global__ __launch_bounds__(256) void rts_scan_kernel(uint32_t* __restrict__ C,
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
+// ranges (last pass only, may be null): per key value k, the global extent
+// [x, ~y) of k's run in the sorted output, stored as {x, ~end} and merged
+// with atomicMin over tiles (order-independent, so deterministic); the
+// caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
 template <int NV>
 __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        int digit_bits, const uint32_t* __restrict__ C,
-                                                       const uint32_t* __restrict__ totals, uint32_t ntiles) {
+                                                       const uint32_t* __restrict__ totals, uint32_t ntiles,
+                                                       uint2* __restrict__ ranges) {
     constexpr int IPT = ipt_for(NV);
     constexpr uint32_t TILE = tile_items(NV);
     constexpr uint32_t WAVE_ITEMS = 64u * IPT;
@@ -194,7 +199,15 @@ __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n
         const uint32_t j = tid + k * kRsThreads;
         if (j < cnt) {
             const uint32_t d = sdig[j];
-            io.kout[gbase[d] + (j - blk_start[d])] = stage[j];
+            const uint32_t g = gbase[d] + (j - blk_start[d]);
+            const uint32_t key = stage[j];
+            io.kout[g] = key;
+            if (ranges) {
+                // run ends of this key inside the tile (the tile's output is a
+                // contiguous, fully sorted slice of the final order per digit)
+                if (j == 0 || stage[j - 1] != key) atomicMin(&ranges[key].x, g);
+                if (j + 1 == cnt || stage[j + 1] != key) atomicMin(&ranges[key].y, ~(g + 1u));
+            }
         }
     }
     // values: same permutation
@@ -242,7 +255,7 @@ size_t radix_sort_scratch_words(uint32_t n) {
 template <int NV>
 static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
-                                  int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
+                                  int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st) {
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -266,7 +279,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles);
         rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
         rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
-                                                          totals, tiles);
+                                                          totals, tiles, p + 1 == plan.passes ? ranges : nullptr);
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;
@@ -276,17 +289,18 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
 
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
-                             bool* result_in_tmp, hipStream_t st) {
+                             bool* result_in_tmp, hipStream_t st, uint2* ranges) {
     const uint32_t* vi[1] = {vals_in};
     uint32_t* vo[1] = {vals};
     uint32_t* vt[1] = {tmp_vals};
-    return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, st);
+    return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, ranges, st);
 }
 
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                               int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
-    return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp, st);
+    return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp,
+                              nullptr, st);
 }
 
 }  // namespace gs
