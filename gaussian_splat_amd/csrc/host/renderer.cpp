@@ -197,6 +197,7 @@ gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
     u.height = H;
     u.tiles_x = (W + gs::kBin - 1) / gs::kBin;  // binning granularity (32x32 bins)
     u.tiles_y = (H + gs::kBin - 1) / gs::kBin;
+    u.cell_mask = (W <= gs::kCellMaskDim && H <= gs::kCellMaskDim) ? 1 : 0;
     return u;
 }
 
@@ -363,6 +364,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     ca.rows = own.rows;
     ca.nrows = own.nrows;
     ca.compact = compact;
+    ca.cell_mask = U.cell_mask;
     ca.out = out;
     ca.out_bgra8 = out_bgra8;
     ca.cap = h->opt.cap;
@@ -643,7 +645,16 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     GS_HIP(hipStreamSynchronize(st));
     const size_t n = (size_t)h->n;
-    if (records) GS_HIP(hipMemcpy(records, h->rec.ptr, n * sizeof(gs::Record3), hipMemcpyDeviceToHost));
+    if (records) {
+        GS_HIP(hipMemcpy(records, h->rec.ptr, n * sizeof(gs::Record3), hipMemcpyDeviceToHost));
+        if (U.cell_mask) {  // the cell-exclusion mask is internal: export the reference record
+            uint32_t* w = static_cast<uint32_t*>(records);
+            for (size_t i = 0; i < n; ++i) {
+                w[12 * i + 10] &= 0x0FFF0FFFu;
+                w[12 * i + 11] &= 0x0FFF0FFFu;
+            }
+        }
+    }
     if (dkeys) GS_HIP(hipMemcpy(dkeys, h->dkey.ptr, n * 4, hipMemcpyDeviceToHost));
     if (ntiles) {
         std::vector<uint32_t> lo(n), hi(n);

@@ -173,9 +173,15 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
                 bool hit = false;
                 if (k < cnt_b) {
                     const float4 c = s2[k];
-                    const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w);
+                    const uint32_t wlo = __float_as_uint(c.z), whi = __float_as_uint(c.w);
+                    const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
                     hit = !((hi >> 16) < qy0 || (lo >> 16) > qy0 + 7u || (hi & 0xFFFFu) < qx0 ||
                             (lo & 0xFFFFu) > qx0 + 7u);
+                    if (hit && a.cell_mask) {
+                        // skip the quadrant when the ellipse provably misses it
+                        const uint32_t dcx = (qx0 >> 3) - ((lo & 0xFFFFu) >> 3), dcy = (qy0 >> 3) - ((lo >> 16) >> 3);
+                        if (dcx < 4u && dcy < 4u) hit = !((rect_cell_mask(wlo, whi) >> (dcy * 4u + dcx)) & 1u);
+                    }
                 }
                 const uint64_t m = __ballot(hit);
                 if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;

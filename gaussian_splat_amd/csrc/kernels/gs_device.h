@@ -33,7 +33,22 @@ struct FrameUniforms {
     float campos[4];  // eye position for SH view directions
     int32_t width, height;
     int32_t tiles_x, tiles_y;  // 32x32 bins (see kBin)
+    int32_t cell_mask;         // 1: records carry the 8x8-cell exclusion mask (frames <= 4096 px)
 };
+
+// Record rect words (record float4 #2 .zw).  With cell masks (frames up to
+// kCellMaskDim px) each word is x (12 bits) | 4 mask bits | y (12 bits) | 4
+// mask bits; the 16-bit mask marks the 8x8 pixel cells (global 8-px grid,
+// first 4x4 cells of the rect, row-major) that the splat's q <= 2 ln 100
+// ellipse provably misses.  A zero mask excludes nothing (always safe).
+constexpr int kCellMaskDim = 4096;
+__device__ __forceinline__ uint32_t rect_coords(uint32_t w, bool masked) { return masked ? w & 0x0FFF0FFFu : w; }
+__device__ __forceinline__ uint32_t rect_cell_mask(uint32_t lo, uint32_t hi) {
+    return ((lo >> 12) & 0xFu) | ((lo >> 28) << 4) | (((hi >> 12) & 0xFu) << 8) | ((hi >> 28) << 12);
+}
+__device__ __forceinline__ uint32_t rect_with_mask(uint32_t w, uint32_t m4lo, uint32_t m4hi) {
+    return w | (m4lo << 12) | (m4hi << 28);
+}
 
 // Scene SoA resident in HBM: coalesced 16-B loads per lane.
 struct SceneDev {

@@ -70,6 +70,7 @@ struct CompositeArgs {
     const uint16_t* rows;   // owned bin rows, ascending (nullptr: every row)
     int nrows;              // number of owned bin rows
     int compact;            // 1: write the owned bin rows stacked (band buffer)
+    int cell_mask;          // 1: record rect words carry the cell-exclusion mask (FrameUniforms)
     float4* out;            // fp32 RGBA, or (when out_bgra8 is set) unused
     uint32_t* out_bgra8;    // packed BGRA8Unorm (metal_renderer.mm:58), converted in-kernel
     // per-pixel fragment cap (0 = none): thr[py * width + px] = splat id of the

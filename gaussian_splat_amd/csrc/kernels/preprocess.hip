@@ -81,6 +81,55 @@ __device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px
     }
 }
 
+// Cell-exclusion mask (gs_device.h): which 8x8 pixel cells of the rect's
+// first 4x4 the q <= 2 ln 100 ellipse provably misses.  In pixel offsets
+// X = px + 0.5 - cx, Y = cy - (py + 0.5) the record gives u = X ax + Y ay,
+// v = X bx + Y by, so q = aX^2 + 2bXY + cY^2 with a = ax^2 + bx^2,
+// b = ax ay + bx by, c = ay^2 + by^2, det = ac - b^2.  For each 8-px row
+// band [Ya, Yb] the ellipse's X extent is closed form: X(Y) =
+// (-bY +- sqrt(Qa - det Y^2)) / a, extremal at the band ends or at the
+// ellipse's own x-extreme points Y = -+b sqrt(Q/(c det)).  Q and the X range
+// carry a margin, so a cell is excluded only when no pixel centre of it can
+// be covered (the composite then skips a record that would add exact zeros).
+__device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, float ax, float ay, float bx, float by,
+                                                        uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    const uint32_t cx0 = x0 >> 3, cy0 = y0 >> 3, cx1 = x1 >> 3, cy1 = y1 >> 3;
+    if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
+    const float a = ax * ax + bx * bx, b = ax * ay + bx * by, c = ay * ay + by * by;
+    // det = ac - b^2 = (ax by - ay bx)^2: the record's axes are orthogonal, so
+    // the cross product does not cancel (ac - b^2 would, for thin ellipses)
+    const float cr = ax * by - ay * bx;
+    const float det = cr * cr;
+    if (!(det > 0.0f) || !(a > 0.0f) || !(c > 0.0f) || !(det < 3.0e38f)) return 0u;  // degenerate: no claim
+    const float Q = kQMax * 1.002f + 1e-3f;
+    const float ia = 1.0f / a;
+    const float ymax = sqrtf(Q * a / det);          // |Y| reach of the ellipse
+    const float xs = sqrtf(Q * c / det);            // X of the x-extreme points
+    const float ys = b * xs / c;                    // max-X point at Y = -ys, min-X point at Y = +ys
+    uint32_t excl = 0;
+    for (uint32_t r = 0; r <= cy1 - cy0; ++r) {
+        const float pyA = (float)((cy0 + r) * 8u);  // band's pixel rows pyA .. pyA+7
+        float yl = cy - (pyA + 7.5f), yh = cy - (pyA + 0.5f);
+        yl = fmaxf(yl, -ymax);
+        yh = fminf(yh, ymax);
+        float xmin = 1e30f, xmax = -1e30f;  // (empty unless the band meets the ellipse)
+        if (yl <= yh) {
+            auto xhi = [&](float y) { return (-b * y + sqrtf(fmaxf(Q * a - det * y * y, 0.0f))) * ia; };
+            auto xlo = [&](float y) { return (-b * y - sqrtf(fmaxf(Q * a - det * y * y, 0.0f))) * ia; };
+            xmax = (-ys >= yl && -ys <= yh) ? xs : fmaxf(xhi(yl), xhi(yh));
+            xmin = (ys >= yl && ys <= yh) ? -xs : fminf(xlo(yl), xlo(yh));
+            const float pad = 0.01f + 1e-4f * fabsf(xs);
+            xmax += pad;
+            xmin -= pad;
+        }
+        for (uint32_t q = 0; q <= cx1 - cx0; ++q) {
+            const float px0 = (float)((cx0 + q) * 8u) + 0.5f - cx;  // cell's X range
+            if (px0 + 7.0f < xmin || px0 > xmax) excl |= 1u << (r * 4u + q);
+        }
+    }
+    return excl;
+}
+
 template <int DEG>
 __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
@@ -225,9 +274,17 @@ __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const Frame
                     float2 a3 = s.p3[i];
                     sh_color<DEG>(s, i, px, py, pz, U.campos, a2.w, a3.x, a3.y, cr, cg, cbl);
                     float4* o = rec + 3 * (size_t)i;
-                    o[0] = make_float4(cx, cy, e1x * k1, e1y * k1);
-                    o[1] = make_float4(e2x * k2, e2y * k2, a0.w, cr);
-                    o[2] = make_float4(cg, cbl, __uint_as_float(x0 | (y0 << 16)), __uint_as_float(x1 | (y1 << 16)));
+                    const float4 ra = make_float4(cx, cy, e1x * k1, e1y * k1);
+                    const float4 rb = make_float4(e2x * k2, e2y * k2, a0.w, cr);
+                    // 8x8 cells of the rect the ellipse provably misses (the
+                    // composite skips them; frames up to kCellMaskDim px)
+                    const uint32_t excl =
+                        U.cell_mask ? cell_exclusion_mask(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1) : 0u;
+                    o[0] = ra;
+                    o[1] = rb;
+                    o[2] = make_float4(cg, cbl,
+                                       __uint_as_float(rect_with_mask(x0 | (y0 << 16), excl & 0xFu, (excl >> 4) & 0xFu)),
+                                       __uint_as_float(rect_with_mask(x1 | (y1 << 16), (excl >> 8) & 0xFu, excl >> 12)));
                     key = kDepthInf - half_bits(zf);
                     rlo = x0 | (y0 << 16);
                     rhi = x1 | (y1 << 16);
