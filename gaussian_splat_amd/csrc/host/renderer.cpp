@@ -300,7 +300,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, own.dev, h->offsets.as<uint32_t>(),
+    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->offsets.as<uint32_t>(),
                                       h->partials.as<uint64_t>(), h->total.as<uint64_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));
@@ -317,6 +317,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     // pairs (bin, splat) in visiting order
     GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, own.dev,
+                                U.cell_mask != 0,
                                 h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
     if (timed) mark(h, 4, st);
     // stable sort by bin id only; the last pass also writes the bin ranges
@@ -660,8 +661,10 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
         std::vector<uint32_t> lo(n), hi(n);
         GS_HIP(hipMemcpy(lo.data(), h->rlo.ptr, n * 4, hipMemcpyDeviceToHost));
         GS_HIP(hipMemcpy(hi.data(), h->rhi.ptr, n * 4, hipMemcpyDeviceToHost));
+        const uint32_t cm = U.cell_mask ? 0x0FFF0FFFu : 0xFFFFFFFFu;  // strip the bin-exclusion mask
         for (size_t i = 0; i < n; ++i) {
-            const uint32_t x0 = lo[i] & 0xFFFF, x1 = hi[i] & 0xFFFF, y0 = lo[i] >> 16, y1 = hi[i] >> 16;
+            const uint32_t l = lo[i] & cm, u = hi[i] & cm;
+            const uint32_t x0 = l & 0xFFFF, x1 = u & 0xFFFF, y0 = l >> 16, y1 = u >> 16;
             ntiles[i] = x1 < x0 ? 0u : ((x1 >> 4) - (x0 >> 4) + 1) * ((y1 >> 4) - (y0 >> 4) + 1);
         }
     }
@@ -752,6 +755,7 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
     if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
     if (!own.dev.owner) return fail(GS_ERR_STATE, "gs_shard_project: world size 1");
     GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, own.dev.owner,
+                                  U.cell_mask != 0,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));

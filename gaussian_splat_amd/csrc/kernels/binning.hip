@@ -17,22 +17,20 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
                                                         const uint32_t* __restrict__ rect_lo,
                                                         const uint32_t* __restrict__ rect_hi,
                                                         const uint32_t* __restrict__ offsets, uint32_t n,
-                                                        uint32_t tiles_x, RowOwnership own,
+                                                        uint32_t tiles_x, RowOwnership own, bool masked,
                                                         uint32_t* __restrict__ keys,
                                                         uint32_t* __restrict__ vals) {
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
     if (j >= n) return;
-    const uint32_t lo = rect_lo[j], hi = rect_hi[j];
-    const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
-    if (x1 < x0) return;  // culled
+    const BinRect r = bin_rect(rect_lo[j], rect_hi[j], masked);
+    if (r.empty) return;  // culled
     const uint32_t i = order ? order[j] : j;
-    const uint32_t tx0 = x0 >> kBinShift, ty0 = (lo >> 16) >> kBinShift;
-    const uint32_t tx1 = x1 >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
     uint32_t off = offsets[j];
-    for (uint32_t ty = ty0; ty <= ty1; ++ty) {
-        if (!owns_bin_row(ty, own)) continue;
-        for (uint32_t tx = tx0; tx <= tx1; ++tx) {
-            keys[off] = ty * tiles_x + tx;
+    for (uint32_t by = r.by0; by <= r.by1; ++by) {
+        if (!owns_bin_row(by, own)) continue;
+        for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx) {
+            if (bin_excluded(r, by, bx)) continue;  // the ellipse misses this bin
+            keys[off] = by * tiles_x + bx;
             vals[off] = i;
             ++off;
         }
@@ -40,10 +38,11 @@ __global__ __launch_bounds__(256) void duplicate_kernel(const uint32_t* __restri
 }
 
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                             uint32_t* keys, uint32_t* vals, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(order, rect_lo, rect_hi, offsets, n, tiles_x, own, keys, vals);
+    duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(order, rect_lo, rect_hi, offsets, n, tiles_x, own, masked,
+                                                      keys, vals);
     return hipGetLastError();
 }
 

@@ -118,16 +118,46 @@ __device__ __forceinline__ bool owns_bin_row(uint32_t by, const RowOwnership& o)
     return !o.owner || o.owner[by] == o.rank;
 }
 
-// Bins of the rect whose bin row is owned by this rank.
-__device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, const RowOwnership& o) {
-    const uint32_t x0 = lo & 0xFFFFu, x1 = hi & 0xFFFFu;
-    if (x1 < x0) return 0u;
-    const uint32_t ty0 = (lo >> 16) >> kBinShift, ty1 = (hi >> 16) >> kBinShift;
-    const uint32_t cols = (x1 >> kBinShift) - (x0 >> kBinShift) + 1u;
-    if (!o.owner) return (ty1 - ty0 + 1u) * cols;
-    uint32_t rows = 0;
-    for (uint32_t by = ty0; by <= ty1; ++by) rows += o.owner[by] == o.rank ? 1u : 0u;
-    return rows * cols;
+// Bin rect of a splat from its packed pixel rect words.  With `masked`
+// (frames up to kCellMaskDim px, FrameUniforms::cell_mask) the words also
+// carry a 16-bit bin-exclusion mask over the first 4x4 bins of the rect
+// (same packing as the record's cell mask): bins the splat's ellipse
+// provably misses, which get no (splat, bin) pair.
+struct BinRect {
+    uint32_t bx0, by0, bx1, by1;
+    uint32_t excl;  // bit (by - by0) * 4 + (bx - bx0)
+    bool empty;
+};
+__device__ __forceinline__ BinRect bin_rect(uint32_t lo, uint32_t hi, bool masked) {
+    const uint32_t l = rect_coords(lo, masked), h = rect_coords(hi, masked);
+    const uint32_t x0 = l & 0xFFFFu, x1 = h & 0xFFFFu;
+    BinRect r;
+    r.empty = x1 < x0;  // culled (the empty rect survives masking: x0 = 0xFFF > x1 = 0)
+    r.bx0 = x0 >> kBinShift;
+    r.bx1 = x1 >> kBinShift;
+    r.by0 = (l >> 16) >> kBinShift;
+    r.by1 = (h >> 16) >> kBinShift;
+    r.excl = masked ? rect_cell_mask(lo, hi) : 0u;
+    return r;
+}
+__device__ __forceinline__ bool bin_excluded(const BinRect& r, uint32_t by, uint32_t bx) {
+    const uint32_t dy = by - r.by0, dx = bx - r.bx0;
+    return dy < 4u && dx < 4u && ((r.excl >> (dy * 4u + dx)) & 1u);
+}
+
+// (splat, bin) pairs of the rect: owned bin rows, minus excluded bins.
+__device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, const RowOwnership& o, bool masked) {
+    const BinRect r = bin_rect(lo, hi, masked);
+    if (r.empty) return 0u;
+    const uint32_t cols = r.bx1 - r.bx0 + 1u;
+    if (!o.owner && !r.excl) return (r.by1 - r.by0 + 1u) * cols;
+    uint32_t n = 0;
+    for (uint32_t by = r.by0; by <= r.by1; ++by) {
+        if (o.owner && o.owner[by] != o.rank) continue;
+        const uint32_t dy = by - r.by0;
+        n += cols - (dy < 4u ? (uint32_t)__builtin_popcount((r.excl >> (dy * 4u)) & 0xFu) : 0u);
+    }
+    return n;
 }
 
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to

@@ -21,7 +21,8 @@ constexpr int kScanItems = 4096;  // per block
 // offsets[n]; total[0] (device u64) = sum, total[1] = items with a nonzero
 // count.  partials: 2 * ceil(n / kScanItems) u64.
 hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
-                                  uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st);
+                                  bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
+                                  hipStream_t st);
 
 // ---- binning.hip -----------------------------------------------------------
 // Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
@@ -29,7 +30,7 @@ hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_
 // owned by this rank, starting at offsets[j].  order == nullptr
 // means the identity (pairs in index order).
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own,
+                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                             uint32_t* keys, uint32_t* vals, hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
@@ -95,7 +96,7 @@ constexpr int kMaxWorld = 32;
 // dest_mask[i]: bit r set iff splat i touches a bin row owned by rank r (owner[by]).
 // counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
-                              const uint8_t* owner,
+                              const uint8_t* owner, bool masked,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);
 // Exclusive scan of each destination row; dest_total[world].
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);

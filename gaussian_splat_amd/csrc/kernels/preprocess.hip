@@ -91,9 +91,11 @@ __device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px
 // ellipse's own x-extreme points Y = -+b sqrt(Q/(c det)).  Q and the X range
 // carry a margin, so a cell is excluded only when no pixel centre of it can
 // be covered (the composite then skips a record that would add exact zeros).
+template <int SHIFT>  // cell size 1 << SHIFT px: 3 = the composite's 8x8 cells, 5 = 32x32 bins
 __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, float ax, float ay, float bx, float by,
                                                         uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
-    const uint32_t cx0 = x0 >> 3, cy0 = y0 >> 3, cx1 = x1 >> 3, cy1 = y1 >> 3;
+    constexpr uint32_t CS = 1u << SHIFT;
+    const uint32_t cx0 = x0 >> SHIFT, cy0 = y0 >> SHIFT, cx1 = x1 >> SHIFT, cy1 = y1 >> SHIFT;
     if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
     const float a = ax * ax + bx * bx, b = ax * ay + bx * by, c = ay * ay + by * by;
     // det = ac - b^2 = (ax by - ay bx)^2: the record's axes are orthogonal, so
@@ -108,8 +110,8 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
     const float ys = b * xs / c;                    // max-X point at Y = -ys, min-X point at Y = +ys
     uint32_t excl = 0;
     for (uint32_t r = 0; r <= cy1 - cy0; ++r) {
-        const float pyA = (float)((cy0 + r) * 8u);  // band's pixel rows pyA .. pyA+7
-        float yl = cy - (pyA + 7.5f), yh = cy - (pyA + 0.5f);
+        const float pyA = (float)((cy0 + r) * CS);  // band's pixel rows pyA .. pyA+CS-1
+        float yl = cy - (pyA + ((float)CS - 0.5f)), yh = cy - (pyA + 0.5f);
         yl = fmaxf(yl, -ymax);
         yh = fminf(yh, ymax);
         float xmin = 1e30f, xmax = -1e30f;  // (empty unless the band meets the ellipse)
@@ -123,8 +125,8 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
             xmin -= pad;
         }
         for (uint32_t q = 0; q <= cx1 - cx0; ++q) {
-            const float px0 = (float)((cx0 + q) * 8u) + 0.5f - cx;  // cell's X range
-            if (px0 + 7.0f < xmin || px0 > xmax) excl |= 1u << (r * 4u + q);
+            const float px0 = (float)((cx0 + q) * CS) + 0.5f - cx;  // cell's X range
+            if (px0 + (float)(CS - 1u) < xmin || px0 > xmax) excl |= 1u << (r * 4u + q);
         }
     }
     return excl;
@@ -279,15 +281,19 @@ __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const Frame
                     // 8x8 cells of the rect the ellipse provably misses (the
                     // composite skips them; frames up to kCellMaskDim px)
                     const uint32_t excl =
-                        U.cell_mask ? cell_exclusion_mask(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1) : 0u;
+                        U.cell_mask ? cell_exclusion_mask<3>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1) : 0u;
+                    const uint32_t bexcl =
+                        U.cell_mask ? cell_exclusion_mask<kBinShift>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1)
+                                    : 0u;
                     o[0] = ra;
                     o[1] = rb;
                     o[2] = make_float4(cg, cbl,
                                        __uint_as_float(rect_with_mask(x0 | (y0 << 16), excl & 0xFu, (excl >> 4) & 0xFu)),
                                        __uint_as_float(rect_with_mask(x1 | (y1 << 16), (excl >> 8) & 0xFu, excl >> 12)));
                     key = kDepthInf - half_bits(zf);
-                    rlo = x0 | (y0 << 16);
-                    rhi = x1 | (y1 << 16);
+                    // binning rect: the same words plus the bin-exclusion mask
+                    rlo = rect_with_mask(x0 | (y0 << 16), bexcl & 0xFu, (bexcl >> 4) & 0xFu);
+                    rhi = rect_with_mask(x1 | (y1 << 16), (bexcl >> 8) & 0xFu, bexcl >> 12);
                 }
             }
         }

@@ -11,10 +11,11 @@ struct CountSrc {
     const uint32_t* lo;
     const uint32_t* hi;
     RowOwnership own;
+    bool masked;  // rect words carry the bin-exclusion mask
 };
 
 __device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
-    return rect_tile_count(c.lo[i], c.hi[i], c.own);
+    return rect_tile_count(c.lo[i], c.hi[i], c.own, c.masked);
 }
 
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
@@ -105,8 +106,9 @@ __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n
 }
 
 hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
-                                  uint32_t* offsets, uint64_t* partials, uint64_t* total, hipStream_t st) {
-    const CountSrc src{rect_lo, rect_hi, own};
+                                  bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
+                                  hipStream_t st) {
+    const CountSrc src{rect_lo, rect_hi, own, masked};
     uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
         return hipMemsetAsync(total, 0, 2 * sizeof(uint64_t), st);

@@ -33,7 +33,7 @@ __device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const u
 
 __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __restrict__ rect_lo,
                                                           const uint32_t* __restrict__ rect_hi, uint32_t n,
-                                                          int world, const uint8_t* __restrict__ owner,
+                                                          int world, const uint8_t* __restrict__ owner, bool masked,
                                                           uint32_t* __restrict__ dest_mask,
                                                           uint32_t* __restrict__ counts, uint32_t nblocks) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];
@@ -44,8 +44,8 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __rest
         uint32_t i = base + k * 64 + lane;
         uint32_t m = 0;
         if (i < n) {
-            const uint32_t lo = rect_lo[i], hi = rect_hi[i];
-            if ((hi & 0xFFFFu) >= (lo & 0xFFFFu)) m = row_mask((lo >> 16) >> kBinShift, (hi >> 16) >> kBinShift, owner);
+            const BinRect r = bin_rect(rect_lo[i], rect_hi[i], masked);
+            if (!r.empty) m = row_mask(r.by0, r.by1, owner);
         }
         if (i < n) dest_mask[i] = m;
         for (int d = 0; d < world; ++d) {
@@ -154,12 +154,13 @@ __global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ r
 }
 
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
-                              const uint8_t* owner,
+                              const uint8_t* owner, bool masked,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st) {
     if (world < 1 || world > kMaxWorld) return hipErrorInvalidValue;
     if (nblocks == 0) return hipSuccess;
     if (!owner) return hipErrorInvalidValue;
-    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, owner, dest_mask, counts, nblocks);
+    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, owner, masked, dest_mask, counts,
+                                                nblocks);
     return hipGetLastError();
 }
 

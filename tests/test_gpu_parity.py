@@ -35,6 +35,33 @@ def _compare(img, ref):
     return linf, nbit
 
 
+def _rect_bin_pairs(rec, dk, nt, W):
+    """(bin, dkey, splat) for every 32x32 bin of every visible splat's rect
+    (the superset the bin lists are drawn from), and the set of (bin, splat)
+    pairs whose splat surely covers a pixel centre of the bin (float64,
+    threshold shrunk by 1e-4: must be present)."""
+    bx = (W + 31) // 32
+    qmax = 9.21034037197618 * (1.0 - 1e-4)
+    pairs, must = [], set()
+    for i in np.nonzero(nt)[0]:
+        lo, hi = int(rec["rect_lo"][i]), int(rec["rect_hi"][i])
+        x0, y0, x1, y1 = lo & 0xFFFF, lo >> 16, hi & 0xFFFF, hi >> 16
+        r = rec[i]
+        for by in range(y0 >> 5, (y1 >> 5) + 1):
+            for b in range(x0 >> 5, (x1 >> 5) + 1):
+                key = by * bx + b
+                pairs.append((key, int(dk[i]), int(i)))
+                px = np.arange(max(b * 32, x0), min(b * 32 + 31, x1) + 1) + 0.5
+                py = np.arange(max(by * 32, y0), min(by * 32 + 31, y1) + 1) + 0.5
+                dx = px[None, :] - float(r["cx"])
+                dy = float(r["cy"]) - py[:, None]
+                u = dy * float(r["ay"]) + dx * float(r["ax"])
+                v = dy * float(r["by"]) + dx * float(r["bx"])
+                if np.any((u * u + v * v <= qmax) & (np.maximum(np.abs(u), np.abs(v)) <= 3.0 * (1 - 1e-5))):
+                    must.add((key, int(i)))
+    return pairs, must
+
+
 @pytest.mark.parametrize("sh", [0, 1, 2, 3])
 def test_records_bitexact(built, sh):
     from oracle import oracle_py as O
@@ -62,10 +89,10 @@ def test_render_config1_bitexact(built, default_cam_256):
     assert linf <= TOL
     assert nbit == 0, f"{nbit} channel values differ bitwise (L-inf {linf})"
     stats = r.last_stats()
-    rec, _, nt = O.project(sc, V, P, 256, 256)
-    lo, hi = rec["rect_lo"][nt > 0], rec["rect_hi"][nt > 0]
-    bins = ((((hi & 0xFFFF) >> 5) - ((lo & 0xFFFF) >> 5) + 1) * (((hi >> 16) >> 5) - ((lo >> 16) >> 5) + 1)).sum()
-    assert stats["pairs"] == bins  # (splat, 32x32 bin) pairs
+    rec, dk, nt = O.project(sc, V, P, 256, 256)
+    pairs, must = _rect_bin_pairs(rec, dk, nt, 256)
+    # (splat, 32x32 bin) pairs: the rect's bins minus those the ellipse misses
+    assert len(must) <= stats["pairs"] <= len(pairs)
     assert st["pairs"] >= stats["pairs"]
     assert stats["visible"] == int((nt > 0).sum())
 
@@ -164,9 +191,11 @@ def test_render_device_out_matches_host(built):
 
 @pytest.mark.parametrize("n,huge", [(40000, 0), (4096, 0), (6001, 300), (2048 * 3 + 1, 7)])
 def test_sorted_pairs_match_stable_sort(built, n, huge):
-    """Bin lists == a stable sort of the depth-ordered pairs by bin.  Covers
-    several sizes around block boundaries and splats blown up to cover much
-    of the frame."""
+    """Bin lists == a stable sort of the depth-ordered pairs by bin, over the
+    rect's bins minus those the splat's ellipse misses (bin-exclusion mask):
+    never a bin outside the rect, always every bin with a covered pixel
+    centre.  Covers sizes around block boundaries and splats blown up to
+    cover much of the frame."""
     from oracle import oracle_py as O
     W, H = 512, 384
     sc = _scene(n, 9, 0, aspect=W / H)
@@ -178,16 +207,13 @@ def test_sorted_pairs_match_stable_sort(built, n, huge):
     r.render_host(V, P, W, H)
     keys, vals = r.sorted_pairs()
     rec, dk, nt = O.project(sc, V, P, W, H)
-    bx = (W + 31) // 32  # 32x32 binning bins
-    ek, ev = [], []
-    for i in np.nonzero(nt)[0]:
-        lo, hi = int(rec["rect_lo"][i]), int(rec["rect_hi"][i])
-        for by in range((lo >> 16) >> 5, ((hi >> 16) >> 5) + 1):
-            for b in range((lo & 0xFFFF) >> 5, ((hi & 0xFFFF) >> 5) + 1):
-                ek.append(((by * bx + b) << 15) | int(dk[i]))
-                ev.append(i)
-    ek = np.array(ek, np.uint64)
-    ev = np.array(ev, np.uint32)
+    pairs, must = _rect_bin_pairs(rec, dk, nt, W)
+    got = set(zip(keys.tolist(), vals.tolist()))
+    assert len(got) == len(keys)                                  # no duplicates
+    assert got <= {(k, i) for k, _, i in pairs}                   # only bins of the rect
+    assert must <= got                                            # every surely covered bin
+    ek = np.array([(k << 15) | d for k, d, i in pairs if (k, i) in got], np.uint64)
+    ev = np.array([i for k, d, i in pairs if (k, i) in got], np.uint32)
     order = np.argsort(ek, kind="stable")  # (bin, dkey), ties by splat index
     np.testing.assert_array_equal(keys.astype(np.uint64), ek[order] >> np.uint64(15))  # bin id
     np.testing.assert_array_equal(vals, ev[order])
