@@ -424,7 +424,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_scan = N * 20;
     s.bytes_duplicate = N * 20 + Pi * 8;
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
-    s.bytes_ranges = Pi * 4 + T * 8;
+    s.bytes_ranges = T * 8;  // the fill only: ranges come out of the last sort pass
     s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
     if (h->opt.stage_timing && h->events) {
         (void)hipEventSynchronize(h->ev[7]);
