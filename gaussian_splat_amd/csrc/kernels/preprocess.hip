@@ -97,17 +97,20 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
     constexpr uint32_t CS = 1u << SHIFT;
     const uint32_t cx0 = x0 >> SHIFT, cy0 = y0 >> SHIFT, cx1 = x1 >> SHIFT, cy1 = y1 >> SHIFT;
     if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
+    if (cx1 == cx0 && cy1 == cy0) return 0u;  // one cell: the rect itself decides
     const float a = ax * ax + bx * bx, b = ax * ay + bx * by, c = ay * ay + by * by;
     // det = ac - b^2 = (ax by - ay bx)^2: the record's axes are orthogonal, so
     // the cross product does not cancel (ac - b^2 would, for thin ellipses)
     const float cr = ax * by - ay * bx;
     const float det = cr * cr;
     if (!(det > 0.0f) || !(a > 0.0f) || !(c > 0.0f) || !(det < 3.0e38f)) return 0u;  // degenerate: no claim
+    // hardware approximations (v_rcp_f32, v_sqrt_f32: ~1 ulp) are well inside
+    // the 0.2 % margin on Q and the padding on X
     const float Q = kQMax * 1.002f + 1e-3f;
-    const float ia = 1.0f / a;
-    const float ymax = sqrtf(Q * a / det);          // |Y| reach of the ellipse
-    const float xs = sqrtf(Q * c / det);            // X of the x-extreme points
-    const float ys = b * xs / c;                    // max-X point at Y = -ys, min-X point at Y = +ys
+    const float ia = __builtin_amdgcn_rcpf(a), idet = __builtin_amdgcn_rcpf(det);
+    const float ymax = __builtin_amdgcn_sqrtf(Q * a * idet);          // |Y| reach of the ellipse
+    const float xs = __builtin_amdgcn_sqrtf(Q * c * idet);            // X of the x-extreme points
+    const float ys = b * xs * __builtin_amdgcn_rcpf(c);               // max-X point at Y = -ys, min-X at +ys
     uint32_t excl = 0;
     for (uint32_t r = 0; r <= cy1 - cy0; ++r) {
         const float pyA = (float)((cy0 + r) * CS);  // band's pixel rows pyA .. pyA+CS-1
@@ -116,11 +119,12 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
         yh = fminf(yh, ymax);
         float xmin = 1e30f, xmax = -1e30f;  // (empty unless the band meets the ellipse)
         if (yl <= yh) {
-            auto xhi = [&](float y) { return (-b * y + sqrtf(fmaxf(Q * a - det * y * y, 0.0f))) * ia; };
-            auto xlo = [&](float y) { return (-b * y - sqrtf(fmaxf(Q * a - det * y * y, 0.0f))) * ia; };
+            auto root = [&](float y) { return __builtin_amdgcn_sqrtf(fmaxf(Q * a - det * y * y, 0.0f)); };
+            auto xhi = [&](float y) { return (-b * y + root(y)) * ia; };
+            auto xlo = [&](float y) { return (-b * y - root(y)) * ia; };
             xmax = (-ys >= yl && -ys <= yh) ? xs : fmaxf(xhi(yl), xhi(yh));
             xmin = (ys >= yl && ys <= yh) ? -xs : fminf(xlo(yl), xlo(yh));
-            const float pad = 0.01f + 1e-4f * fabsf(xs);
+            const float pad = 0.01f + 1e-3f * fabsf(xs);
             xmax += pad;
             xmin -= pad;
         }
