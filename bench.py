@@ -13,7 +13,12 @@ Multi-GPU is weak scaling: every rank holds its own 6M-splat shard of a
 time (max over ranks).  Prints one JSON line on rank 0.
 
 At N=1 the line also carries
-  roofline      the slowest stage's algorithmic bytes / its HIP-event time,
+  roofline      the slowest stage's algorithmic bytes / its average kernel
+                time; for preprocess / composite that time comes from HIP
+                events carried in the kernels' own dispatch packets over the
+                K timed frames (stage_timing 2: no extra packets, no syncs);
+                the full per-stage table ("stages") comes from a few extra
+                untimed frames with an event between every stage
                 and `traffic`: its HBM bytes per launch from two rocprofv3
                 PMC passes (FETCH_SIZE, WRITE_SIZE) run as child processes
                 (FETCH_SIZE doubled: gfx950 tallies 128-B reads at 64 B,
@@ -165,21 +170,22 @@ def main():
     scene = S.synthetic_scene(args.splats, seed=args.seed + 1000 * rank, sh_degree=args.sh, aspect=W / H)
     cam = default_camera(W, H)
     view, proj = cam.getViewMatrix(), cam.getProjectionMatrix()
-    opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=not args.no_stage_timing)
+    timing = 0 if args.no_stage_timing else 2  # timed frames: dispatch-packet events only
+    opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=timing)
 
     if world == 1:
         r = InstancedSplatRenderer(scene, opts)
         r.initialize(local)
         out = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
         step = lambda: r.render(view, proj, W, H, out=out)
-        stats_of = r.last_stats
+        rh = r
     else:
         from gaussian_splat_amd.distributed import HipShardBackend, ShardedRenderer
 
         be = HipShardBackend(scene, rank, world, rank * args.splats, opts, local)
         sr = ShardedRenderer(be, rank, world)
         step = lambda: sr.render(view, proj, W, H, gather=True)
-        stats_of = be.r.last_stats
+        rh = be.r
 
     for _ in range(args.warmup):
         step()
@@ -187,11 +193,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stats = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        stats.append(stats_of())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -204,17 +208,34 @@ def main():
     total_splats = args.splats * world
     value = total_splats / (ms * 1e-3) / 1e6
 
+    s0 = rh.last_stats()
+    timed = {}
+    if timing == 2:  # kernel times of the timed frames (last <= 64)
+        pre, comp = rh.kernel_times(args.steps)
+        timed = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
+    # full stage breakdown: extra untimed frames, an event between every stage
+    st = {}
+    if not args.no_stage_timing:
+        rh.set_stage_timing(1)
+        stats = []
+        for _ in range(min(max(args.steps, 3), 10)):
+            step()
+            stats.append(rh.last_stats())
+        st = stage_summary(stats)
+
     line = None
     if rank == 0:
-        st = stage_summary(stats) if not args.no_stage_timing else {}
-        s0 = stats[-1]
         rl = None
         if st:
             dom = max((k for k in st if k != "exchange"), key=lambda k: st[k]["ms"])
             d = st[dom]
-            rl = {"bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(d["gbs"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                  "kernel_ms": round(d["ms"], 4)}
+            kms, src = d["ms"], "stage events, extra untimed frames"
+            if dom in timed:
+                kms, src = timed[dom], f"dispatch-packet events, {min(args.steps, 64)} timed frames"
+            gbs = d["bytes"] / (kms * 1e6)
+            rl = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                  "kernel_ms": round(kms, 4), "bytes": int(d["bytes"]), "timing": src}
         line = {
             "metric": "Msplats/sec (6M-splat scene @1080p, SH3, full frame)",
             "value": round(value, 2), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
@@ -228,6 +249,7 @@ def main():
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
+            "timed_kernel_ms": {k: round(v, 4) for k, v in timed.items()},
         }
         if world == 1 and rl is not None and args.traffic:
             traffic, why = pmc_traffic(args, STAGE_KERNEL[rl["kernel"]])

@@ -55,9 +55,11 @@ SIGNATURES = {
     "gs_destroy": (None, [_P]),
     "gs_set_mode": (C.c_int, [_P, C.c_int32]),
     "gs_set_cap": (C.c_int, [_P, C.c_int32]),
+    "gs_set_stage_timing": (C.c_int, [_P, C.c_int32]),
     "gs_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_render_bgra8": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_last_stats": (C.c_int, [_P, C.POINTER(GsStats)]),
+    "gs_kernel_times": (C.c_int, [_P, C.c_int32, _FP, _FP, C.POINTER(C.c_int32)]),
     "gs_project_host": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, _P, _P]),
     "gs_sorted_pairs_host": (C.c_int, [_P, _P, _P, C.c_int64, _I64P]),
     "gs_radix_sort_pairs": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32, _P]),

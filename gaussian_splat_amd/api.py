@@ -47,7 +47,7 @@ class Options:
     sh_degree: int = 0
     crop: bool = True
     crop_radius: float = 5.0
-    stage_timing: bool = False
+    stage_timing: int = 0  # 0 off, 1 every stage (adds event gaps), 2 preprocess + composite only
     cap: int = 0  # per-pixel fragment cap by arrival order (0 = none; 32 tile shader, 50 live shader)
 
     def to_c(self) -> GsOptions:
@@ -59,7 +59,7 @@ class Options:
         o.sh_degree = int(self.sh_degree)
         o.crop = int(bool(self.crop))
         o.crop_radius = float(self.crop_radius)
-        o.stage_timing = int(bool(self.stage_timing))
+        o.stage_timing = int(self.stage_timing)
         if int(self.cap) < 0:
             raise ValueError("cap must be >= 0")
         o.cap = int(self.cap)
@@ -225,6 +225,11 @@ class InstancedSplatRenderer:
         check(lib().gs_set_mode(self._h, MODES[mode]), "gs_set_mode")
         self.options.mode = mode
 
+    def set_stage_timing(self, mode: int):
+        """0 off, 1 every stage, 2 preprocess + composite via their own dispatch packets."""
+        check(lib().gs_set_stage_timing(self._h, int(mode)), "gs_set_stage_timing")
+        self.options.stage_timing = int(mode)
+
     def set_cap(self, cap: int):
         """Per-pixel fragment cap by arrival order (0 = none)."""
         check(lib().gs_set_cap(self._h, int(cap)), "gs_set_cap")
@@ -273,6 +278,16 @@ class InstancedSplatRenderer:
         s = GsStats()
         check(lib().gs_last_stats(self._h, C.byref(s)), "gs_last_stats")
         return s.as_dict()
+
+    def kernel_times(self, max_frames: int = 64):
+        """stage_timing 2: (ms_preprocess, ms_composite) arrays of the last
+        frames (<= 64, oldest first) from the events in the kernels' dispatch packets."""
+        pre = np.zeros(max_frames, np.float32)
+        comp = np.zeros(max_frames, np.float32)
+        cnt = C.c_int32(0)
+        check(lib().gs_kernel_times(self._h, int(max_frames), pre.ctypes.data_as(C.POINTER(C.c_float)),
+                                    comp.ctypes.data_as(C.POINTER(C.c_float)), C.byref(cnt)), "gs_kernel_times")
+        return pre[:cnt.value], comp[:cnt.value]
 
     def project_host(self, view, proj, width: int, height: int):
         n = self.getPointCount()

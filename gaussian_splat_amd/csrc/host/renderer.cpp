@@ -82,7 +82,14 @@ struct gs_handle {
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
     uint64_t* host_total = nullptr;  // pinned
-    hipEvent_t ev[9] = {};  // stage boundaries 0..7; 8 = exchange done (shard frames)
+    hipEvent_t ev[9] = {};   // stage boundaries 0..7; 8 = exchange done (shard frames)
+    // stage_timing 2: packet events (preprocess start/stop, composite start/stop)
+    // in a ring of per-frame slots, read without stalling the frames
+    static constexpr int kKevRing = 64;
+    hipEvent_t kev[kKevRing][4] = {};
+    int64_t kev_frames = 0;    // frames recorded since stage timing was (re)set
+    int kev_slot = 0;          // slot of the frame being enqueued
+    bool kev_pending = false;  // last frame's kernel times not yet copied into stats
     bool shard_frame = false;
     bool events = false;
     uint32_t* last_keys = nullptr;  // sorted pair arrays of the last frame
@@ -103,8 +110,11 @@ struct gs_handle {
             b->release();
         if (host_total) (void)hipHostFree(host_total);
         if (host_xtotal) (void)hipHostFree(host_xtotal);
-        if (events)
+        if (events) {
             for (auto& e : ev) (void)hipEventDestroy(e);
+            for (auto& slot : kev)
+                for (auto& e : slot) (void)hipEventDestroy(e);
+        }
     }
 
     gs::SceneDev scene_dev() const {
@@ -226,13 +236,18 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 16, hipHostMallocDefault));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
+        for (auto& slot : h->kev)
+            for (auto& e : slot) GS_HIP(hipEventCreate(&e));
         h->events = true;
     }
     return GS_OK;
 }
 
+// Stage timing (gs_options.stage_timing): 1 = an event between every stage
+// (complete breakdown; each event packet costs a few us of gap), 2 = events
+// carried by the preprocess and composite dispatch packets only (no gaps).
 void mark(gs_handle* h, int k, hipStream_t st) {
-    if (h->opt.stage_timing && h->events) (void)hipEventRecord(h->ev[k], st);
+    if (h->opt.stage_timing == 1 && h->events) (void)hipEventRecord(h->ev[k], st);
     // debugging aid: GS_DEBUG_SYNC=<bitmask of stages> finishes and reports them
     static const long dbg = std::getenv("GS_DEBUG_SYNC") ? std::strtol(std::getenv("GS_DEBUG_SYNC"), nullptr, 0) : 0;
     if (dbg & (1L << k)) {
@@ -243,8 +258,28 @@ void mark(gs_handle* h, int k, hipStream_t st) {
 
 float elapsed(gs_handle* h, int a, int b) {
     float ms = 0.0f;
-    if (h->opt.stage_timing && h->events) (void)hipEventElapsedTime(&ms, h->ev[a], h->ev[b]);
+    if (h->opt.stage_timing == 1 && h->events) (void)hipEventElapsedTime(&ms, h->ev[a], h->ev[b]);
     return ms;
+}
+
+hipEvent_t kernel_event(gs_handle* h, int k) {
+    return h->opt.stage_timing == 2 && h->events ? h->kev[h->kev_slot][k] : nullptr;
+}
+
+// First launch of a frame: pick its packet-event slot.
+void begin_frame(gs_handle* h, hipStream_t st) {
+    h->kev_slot = (int)(h->kev_frames % gs_handle::kKevRing);
+    h->kev_pending = false;
+    mark(h, 0, st);
+}
+
+// Kernel times of packet-event slot `k` (waits for that frame's composite).
+gs_status slot_times(gs_handle* h, int k, float* pre, float* comp, float* total) {
+    GS_HIP(hipEventSynchronize(h->kev[k][3]));
+    GS_HIP(hipEventElapsedTime(pre, h->kev[k][0], h->kev[k][1]));
+    GS_HIP(hipEventElapsedTime(comp, h->kev[k][2], h->kev[k][3]));
+    if (total) GS_HIP(hipEventElapsedTime(total, h->kev[k][0], h->kev[k][3]));
+    return GS_OK;
 }
 
 // Bin-row ownership of the frame as the kernels see it.
@@ -399,7 +434,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     if (s != GS_OK) return s;
     ca.vals = vals;
     ca.ranges = h->ranges.as<uint2>();
-    GS_HIP(gs::launch_composite(ca, h->opt.mode, st));
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, st, kernel_event(h, 2), kernel_event(h, 3)));
     mark(h, 7, st);
     h->stats.pairs = (int64_t)P;
     return GS_OK;
@@ -426,7 +461,13 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
     s.bytes_ranges = T * 8;  // the fill only: ranges come out of the last sort pass
     s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
-    if (h->opt.stage_timing && h->events) {
+    // stage_timing 2: read lazily (gs_last_stats / gs_kernel_times), so a
+    // frame never waits for itself
+    if (h->opt.stage_timing == 2 && h->events) {
+        h->kev_pending = true;
+        ++h->kev_frames;
+    }
+    if (h->opt.stage_timing == 1 && h->events) {
         (void)hipEventSynchronize(h->ev[7]);
         s.ms_preprocess = elapsed(h, 0, 1);
         s.ms_exchange = h->shard_frame ? elapsed(h, 1, 8) : 0.0f;
@@ -572,6 +613,14 @@ gs_status gs_set_mode(gs_handle* h, int32_t mode) {
     return GS_OK;
 }
 
+gs_status gs_set_stage_timing(gs_handle* h, int32_t mode) {
+    if (!h || mode < 0 || mode > 2) return fail(GS_ERR_INVALID_ARG, "stage_timing must be 0, 1 or 2");
+    h->opt.stage_timing = mode;
+    h->kev_frames = 0;
+    h->kev_pending = false;
+    return GS_OK;
+}
+
 gs_status gs_set_cap(gs_handle* h, int32_t cap) {
     if (!h || cap < 0) return fail(GS_ERR_INVALID_ARG, "bad cap");
     h->opt.cap = cap;
@@ -599,9 +648,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     }
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = false;
-    mark(h, 0, st);
+    begin_frame(h, st);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
+                                 kernel_event(h, 1)));
     mark(h, 1, st);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
@@ -628,9 +678,31 @@ gs_status gs_render_bgra8(gs_handle* h, const float* view, const float* proj, in
     return render_frame(h, view, proj, W, H, out_bgra, out_is_device, true, stream);
 }
 
-gs_status gs_last_stats(const gs_handle* h, gs_stats* out) {
+gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
     if (!h || !out) return fail(GS_ERR_INVALID_ARG, "null argument");
+    if (h->kev_pending) {  // stage_timing 2: kernel times of the last frame
+        gs_status s = slot_times(h, h->kev_slot, &h->stats.ms_preprocess, &h->stats.ms_composite,
+                                 &h->stats.ms_total);
+        if (s != GS_OK) return s;
+        h->kev_pending = false;
+    }
     *out = h->stats;
+    return GS_OK;
+}
+
+gs_status gs_kernel_times(gs_handle* h, int32_t max_frames, float* ms_preprocess, float* ms_composite,
+                          int32_t* count) {
+    if (!h || !count || max_frames < 0 || (max_frames > 0 && (!ms_preprocess || !ms_composite)))
+        return fail(GS_ERR_INVALID_ARG, "gs_kernel_times: bad arguments");
+    *count = 0;
+    if (h->opt.stage_timing != 2 || !h->events) return GS_OK;
+    const int64_t n = std::min<int64_t>({(int64_t)max_frames, h->kev_frames, (int64_t)gs_handle::kKevRing});
+    for (int64_t j = 0; j < n; ++j) {  // oldest first
+        const int k = (int)((h->kev_frames - n + j) % gs_handle::kKevRing);
+        gs_status s = slot_times(h, k, &ms_preprocess[j], &ms_composite[j], nullptr);
+        if (s != GS_OK) return s;
+    }
+    *count = (int32_t)n;
     return GS_OK;
 }
 
@@ -746,9 +818,10 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
     if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = true;
-    mark(h, 0, st);
+    begin_frame(h, st);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
+                                 kernel_event(h, 1)));
     mark(h, 1, st);
     GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
     Ownership own;

@@ -18,6 +18,8 @@
 // saturated, and the workgroup stops fetching once all 256 are.
 // Bins are dealt to workgroups XCD-aware: consecutive bins of a row share
 // many of their splats, so they are placed on one XCD's L2.
+#include <hip/hip_ext.h>
+
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -227,19 +229,21 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
 }
 
 template <int MODE, bool CAP>
-static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st) {
+static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
+                              hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
     const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
     if (nwg == 0) return hipSuccess;
-    composite_kernel<MODE, CAP><<<nwg, kTileThreads, 0, st>>>(a, nwg);
+    // t0/t1 (optional) are recorded by the dispatch packet itself
+    hipExtLaunchKernelGGL(composite_kernel<MODE, CAP>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a, nwg);
     return hipGetLastError();
 }
 
-hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st) {
+hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
-    if (mode == 0) return cap ? launch_mode<0, true>(a, st) : launch_mode<0, false>(a, st);
-    return cap ? launch_mode<1, true>(a, st) : launch_mode<1, false>(a, st);
+    if (mode == 0) return cap ? launch_mode<0, true>(a, st, t0, t1) : launch_mode<0, false>(a, st, t0, t1);
+    return cap ? launch_mode<1, true>(a, st, t0, t1) : launch_mode<1, false>(a, st, t0, t1);
 }
 
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {

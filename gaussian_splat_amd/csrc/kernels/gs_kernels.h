@@ -12,8 +12,11 @@ namespace gs {
 // ---- preprocess.hip ------------------------------------------------------
 // Writes the 48-B record (visible splats), the 15-bit depth key and the packed
 // pixel rect (empty rect for culled splats).
+// t0/t1: optional events recorded by the kernel's own dispatch (timing
+// without extra packets).
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
-                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st);
+                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
+                             hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
@@ -83,7 +86,8 @@ struct CompositeArgs {
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break); with a.cap > 0 only fragments
 // with id <= thr[pixel] are composited.
-hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st);
+hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0 = nullptr,
+                            hipEvent_t t1 = nullptr);
 // Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).

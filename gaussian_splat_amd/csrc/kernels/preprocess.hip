@@ -7,6 +7,8 @@
 // Metal's fixed-function quad raster (K6) reduced to a conservative pixel
 // rectangle.  Memory-bound: N·(B_in + 56) bytes per frame.
 #include "gs_device.h"
+#include <hip/hip_ext.h>
+
 #include "gs_kernels.h"
 
 namespace gs {
@@ -308,14 +310,17 @@ __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const Frame
 }
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
-                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st) {
+                             uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
+                             hipEvent_t t1) {
     if (s.n == 0) return hipSuccess;
     dim3 grid((s.n + 255) / 256), block(256);
+    // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
+    // barrier packets around the kernel
     switch (sh_degree) {
-    case 0: preprocess_kernel<0><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 1: preprocess_kernel<1><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 2: preprocess_kernel<2><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 3: preprocess_kernel<3><<<grid, block, 0, st>>>(s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -57,7 +57,9 @@ typedef struct gs_options {
     int32_t sh_degree;     /* 0..3; 0 = loader-converted DC colour (reference behaviour) */
     int32_t crop;          /* 1 = keep |x|,|y|,|z| < crop_radius (instanced_splat_renderer.mm:382-386) */
     float crop_radius;     /* 5.0 in the reference */
-    int32_t stage_timing;  /* 1 = record HIP events around every kernel (gs_last_stats) */
+    int32_t stage_timing;  /* gs_last_stats timing: 0 off; 1 = an event between every stage (full
+                              breakdown; each event adds a few us of gap); 2 = events carried by
+                              the preprocess and composite dispatches only (no gaps) */
     int32_t cap;           /* per-pixel fragment cap by arrival order, 0 = none (contract default);
                               32 = gaussian_splat_tile.metal:7, 50 = gaussian_splat_50layer.metal:8 */
     int32_t reserved[6];
@@ -84,7 +86,8 @@ typedef struct gs_stats {
     int32_t width, height;
     int32_t sort_bits;     /* significant key bits sorted */
     int32_t sort_passes;
-    /* stage times in ms (valid when options.stage_timing = 1) */
+    /* stage times in ms (all with stage_timing = 1; preprocess, composite and
+       total with stage_timing = 2) */
     float ms_preprocess, ms_scan, ms_duplicate, ms_sort, ms_ranges, ms_composite, ms_total;
     int64_t bytes_preprocess, bytes_scan, bytes_duplicate, bytes_sort, bytes_ranges, bytes_composite;
     float ms_depth_sort;   /* splats by depth key (ms_sort = pairs by tile) */
@@ -112,6 +115,8 @@ gs_status gs_set_mode(gs_handle *h, int32_t mode);
  * of each pixel in arrival (= splat index) order, as the reference's
  * fixed-size per-pixel lists do (tile.metal:199-202, 50layer.metal:170). */
 gs_status gs_set_cap(gs_handle *h, int32_t cap);
+/* Switch gs_options.stage_timing (0, 1 or 2) on a live handle. */
+gs_status gs_set_stage_timing(gs_handle *h, int32_t mode);
 
 /* ---- frame (InstancedSplatRenderer::render) --------------------------- */
 /* out_rgba: width*height*4 float32, row-major, y down.  out_is_device = 1:
@@ -123,7 +128,13 @@ gs_status gs_render(gs_handle *h, const float view[16], const float proj[16], in
  * converted inside the composite (clamp [0,1], x255, round to nearest even). */
 gs_status gs_render_bgra8(gs_handle *h, const float view[16], const float proj[16], int32_t width,
                           int32_t height, uint8_t *out_bgra, int32_t out_is_device, void *hip_stream);
-gs_status gs_last_stats(const gs_handle *h, gs_stats *out);
+gs_status gs_last_stats(gs_handle *h, gs_stats *out);
+/* stage_timing 2: preprocess and composite kernel times (ms, from the events
+ * in their dispatch packets) of the last min(max_frames, 64) frames rendered
+ * since stage timing was set, oldest first; waits for those frames.  *count
+ * = frames written (0 when stage_timing != 2). */
+gs_status gs_kernel_times(gs_handle *h, int32_t max_frames, float *ms_preprocess, float *ms_composite,
+                          int32_t *count);
 
 /* ---- stage-level entry points (tests, multi-GPU orchestration) --------- */
 /* Project all splats; copies the 48-byte records (gs_record layout below),

@@ -176,6 +176,35 @@ def test_render_anisotropic_bitexact(built, w, h):
         assert _compare(img, ref) == (0.0, 0)
 
 
+def test_stage_timing_modes(built):
+    """Timing never changes the image; stage_timing 2 reports per-frame
+    preprocess/composite kernel times from the dispatch-packet events (ring
+    of 64 frames), stage_timing 1 the full stage breakdown."""
+    import torch
+    sc = _scene(30000, seed=17, sh=1, aspect=16 / 9)
+    r = _renderer(sc, sh=1)
+    V, P = orbit_views(640, 360)[0]
+    ref = r.render_host(V, P, 640, 360)
+    out = torch.empty((360, 640, 4), dtype=torch.float32, device="cuda:0")
+    for mode in (2, 1, 0):
+        r.set_stage_timing(mode)
+        for _ in range(3 if mode != 2 else 70):
+            r.render(V, P, 640, 360, out=out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        st = r.last_stats()
+        pre, comp = r.kernel_times(100)
+        if mode == 2:
+            assert len(pre) == 64 and np.all(pre > 0) and np.all(comp > 0)
+            assert st["ms_preprocess"] > 0 and st["ms_composite"] > 0 and st["ms_total"] >= st["ms_composite"]
+            assert st["ms_sort"] == 0
+        else:
+            assert len(pre) == 0
+        if mode == 1:
+            assert all(st[f"ms_{k}"] > 0 for k in ("preprocess", "depth_sort", "scan", "duplicate", "sort",
+                                                   "composite"))
+
+
 def test_render_device_out_matches_host(built):
     import torch
     sc = _scene(30000, 5, 0, aspect=4 / 3)
