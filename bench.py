@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU baseline duration")
     ap.add_argument("--traffic", type=int, default=1, help="measure roofline.traffic with rocprofv3 PMC (N=1)")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--scheme", default="rows", choices=["rows", "slabs"],
+                    help="N>1: bin-row ownership (bit-exact, default) or depth slabs + RGBA reduce (DESIGN.md §6b)")
     return ap.parse_args()
 
 
@@ -180,10 +182,14 @@ def main():
         step = lambda: r.render(view, proj, W, H, out=out)
         rh = r
     else:
-        from gaussian_splat_amd.distributed import HipShardBackend, ShardedRenderer
+        from gaussian_splat_amd.distributed import HipShardBackend, HipSlabBackend, ShardedRenderer, SlabRenderer
 
-        be = HipShardBackend(scene, rank, world, rank * args.splats, opts, local)
-        sr = ShardedRenderer(be, rank, world)
+        if args.scheme == "slabs":
+            be = HipSlabBackend(scene, rank, world, rank * args.splats, opts, local)
+            sr = SlabRenderer(be, rank, world)
+        else:
+            be = HipShardBackend(scene, rank, world, rank * args.splats, opts, local)
+            sr = ShardedRenderer(be, rank, world)
         step = lambda: sr.render(view, proj, W, H, gather=True)
         rh = be.r
 
@@ -244,8 +250,10 @@ def main():
             "data": "synthetic (seeded 3DGS-statistics scene; no garden .ply offline)",
             "config": {"workload": f"{args.splats} splats/GPU @ {W}x{H}, SH{args.sh}, {args.mode} contract",
                        "global_splats": total_splats, "width": W, "height": H, "sh_degree": args.sh,
-                       "parallelism": f"splat-shard x{world}, 128-px band ownership, {backend}" if world > 1
-                       else "single GPU",
+                       "parallelism": (f"splat-shard x{world}, 32-px bin-row ownership, all_to_all + gather, {backend}"
+                                       if args.scheme == "rows" else
+                                       f"splat-shard x{world}, depth slabs, all_to_all + T all_gather + RGBA "
+                                       f"reduce, {backend}") if world > 1 else "single GPU",
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},

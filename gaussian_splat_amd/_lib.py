@@ -68,6 +68,11 @@ SIGNATURES = {
     "gs_shard_project": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int64, _I64P, _P]),
     "gs_shard_render": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
     "gs_exchange_record_bytes": (C.c_int32, []),
+    "gs_slab_project": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, _P]),
+    "gs_slab_bounds": (C.c_int, [_P, C.c_int32, _P]),
+    "gs_slab_pack": (C.c_int, [_P, _P, _P, C.c_int64, _I64P, _P]),
+    "gs_slab_render": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
+    "gs_slab_composite": (C.c_int, [_P, _P, _P, _P]),
     "gs_ply_load": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(_FP), _I64P]),
     "gs_ply_free": (None, [_FP]),
     "gs_look_at": (None, [_FP, _FP, _FP, _FP]),

@@ -53,24 +53,29 @@ def _headers() -> list[Path]:
     return (list((ROOT / "include").rglob("*.h")) + list(CSRC.rglob("*.h")))
 
 
-def build_lib(verbose: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+def build_lib(verbose: bool = False, extra: list[str] | None = None, build_dir: Path = BUILD,
+              lib: Path = LIB) -> Path:
+    """Compile and link libgsplat.so.  `extra` flags / `build_dir` / `lib`
+    build a variant (tools/build_variant.py: A/B timing, debug counters)."""
+    extra = list(extra or [])
+    build_dir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     hdrs = _headers()
     jobs = []
     objs = []
     for src in HIP_SOURCES:
-        obj = BUILD / (src.name + ".o")
+        obj = build_dir / (src.name + ".o")
         objs.append(obj)
         if _stale(obj, [src, *hdrs]):
-            jobs.append([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, "-c", str(src), "-o", str(obj)])
+            jobs.append([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, *extra, "-c", str(src), "-o",
+                         str(obj)])
     for src in CXX_SOURCES:
         if not src.exists():
             continue
-        obj = BUILD / (src.name + ".o")
+        obj = build_dir / (src.name + ".o")
         objs.append(obj)
         if _stale(obj, [src, *hdrs]):
-            jobs.append(["g++", *COMMON, "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-c", str(src),
+            jobs.append(["g++", *COMMON, *extra, "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-c", str(src),
                          "-o", str(obj)])
     workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")) or 1) if jobs else 1
     with ThreadPoolExecutor(max_workers=workers) as ex:
@@ -78,10 +83,11 @@ def build_lib(verbose: bool = False) -> Path:
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
         list(ex.map(_run, jobs))
-    if jobs or _stale(LIB, objs):
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+    if jobs or _stale(lib, objs):
+        lib.parent.mkdir(parents=True, exist_ok=True)
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
               "-lpthread"])
-    return LIB
+    return lib
 
 
 def build_oracle() -> None:

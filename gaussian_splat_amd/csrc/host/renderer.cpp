@@ -80,6 +80,11 @@ struct gs_handle {
     DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
+    // depth-slab frames: full-frame ownership; the colour pass
+    // (gs_slab_composite) reuses the bin lists of the transmittance pass
+    bool slab_frame = false;
+    bool slab_lists = false;
+    int32_t slab_w = 0, slab_h = 0;  // frame of the last gs_slab_project
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
     uint64_t* host_total = nullptr;  // pinned
     hipEvent_t ev[9] = {};   // stage boundaries 0..7; 8 = exchange done (shard frames)
@@ -101,6 +106,7 @@ struct gs_handle {
     std::vector<uint8_t> owner_host;    // table currently on the device
     std::vector<uint16_t> rows_host;    // this rank's owned bin rows
     DevBuf owner_dev, rows_dev;
+    gs::CompositeArgs slab_ca{};
     int64_t index_base = 0;
 
     ~gs_handle() {
@@ -299,7 +305,7 @@ std::vector<uint8_t> default_row_owner(int R, int world) {
 
 gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* out) {
     *out = Ownership{};
-    if (h->world == 1) {
+    if (h->world == 1 || h->slab_frame) {  // every bin row
         out->nrows = tiles_y;
         return GS_OK;
     }
@@ -381,7 +387,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 // bin lists (counted in the depth-sort stage time).
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
-                             int compact, float4* out, uint32_t* out_bgra8, hipStream_t st) {
+                             int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr) {
     Ownership own;
     gs_status so = frame_ownership(h, U.tiles_y, st, &own);
     if (so != GS_OK) return so;
@@ -434,7 +440,15 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     if (s != GS_OK) return s;
     ca.vals = vals;
     ca.ranges = h->ranges.as<uint2>();
+    if (slab_t) {  // depth-slab transmittance pass; the colour pass reuses the lists
+        ca.slab = 1;
+        ca.t_out = slab_t;
+    }
     GS_HIP(gs::launch_composite(ca, h->opt.mode, st, kernel_event(h, 2), kernel_event(h, 3)));
+    if (slab_t) {
+        h->slab_ca = ca;
+        h->slab_lists = true;
+    }
     mark(h, 7, st);
     h->stats.pairs = (int64_t)P;
     return GS_OK;
@@ -799,36 +813,43 @@ gs_status gs_shard_set_rows(gs_handle* h, const uint8_t* owner, int32_t nrows) {
     return GS_OK;
 }
 
-gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, void* send,
-                           int64_t send_cap_bytes, int64_t* send_counts, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// Preprocess of a shard frame (both multi-GPU schemes).
+gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
+                           hipStream_t st, gs::FrameUniforms* U) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if (!view || !proj || !send_counts || W <= 0 || H <= 0)
-        return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
+    if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "shard frame: bad arguments");
     if (W > gs::kXMaxDim || H > gs::kXMaxDim)
         return fail(GS_ERR_UNSUPPORTED, "multi-GPU frames are limited to 4096 x 4096 (packed exchange record)");
-    hipStream_t st = static_cast<hipStream_t>(stream);
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
-    const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    *U = make_uniforms(view, proj, W, H);
+    std::memset(&h->stats, 0, sizeof h->stats);
+    h->shard_frame = true;
+    h->slab_lists = false;
+    begin_frame(h, st);
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, *U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
+                                 kernel_event(h, 1)));
+    mark(h, 1, st);
+    return GS_OK;
+}
+
+// Destination masks by `rule`, per-destination counts (to host), then the
+// exchange records grouped by destination, index order inside.
+gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, void* send, int64_t send_cap_bytes,
+                        int64_t* send_counts, hipStream_t st) {
     const uint32_t n = (uint32_t)h->n;
     const uint32_t nb = (n + gs::kScanItems - 1) / gs::kScanItems;
     GS_HIP(h->xmask.reserve((size_t)std::max<uint32_t>(n, 1) * 4));
     GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
     GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
     if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
-    std::memset(&h->stats, 0, sizeof h->stats);
-    h->shard_frame = true;
-    begin_frame(h, st);
-    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
-                                 kernel_event(h, 1)));
-    mark(h, 1, st);
     GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
-    Ownership own;
-    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
-    if (!own.dev.owner) return fail(GS_ERR_STATE, "gs_shard_project: world size 1");
-    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, own.dev.owner,
-                                  U.cell_mask != 0,
+    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, rule, masked,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
@@ -839,23 +860,24 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
         total += h->host_xtotal[d];
     }
     if (total * gs_exchange_record_bytes() > send_cap_bytes)
-        return fail(GS_ERR_OOM, "gs_shard_project: send buffer too small (" +
+        return fail(GS_ERR_OOM, "exchange: send buffer too small (" +
                                     std::to_string(total * gs_exchange_record_bytes()) + " bytes needed)");
-    if (total > 0 && !send) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: null send buffer");
+    if (total > 0 && !send) return fail(GS_ERR_INVALID_ARG, "exchange: null send buffer");
     GS_HIP(gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
                                  h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
                                  static_cast<float4*>(send), st));
     return GS_OK;
 }
 
-gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
-                          void* stream) {
+// Received records -> depth sort -> bin lists -> composite (rows: owned rows
+// into a compact band; slabs: transmittance pass over the full frame).
+gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba, float* slab_t,
+                          hipStream_t st) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !out_rgba || W <= 0 || H <= 0 ||
+    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !(out_rgba || slab_t) || W <= 0 || H <= 0 ||
         W > gs::kXMaxDim || H > gs::kXMaxDim)
-        return fail(GS_ERR_INVALID_ARG, "gs_shard_render: bad arguments");
-    hipStream_t st = static_cast<hipStream_t>(stream);
+        return fail(GS_ERR_INVALID_ARG, "shard render: bad arguments");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     const gs::FrameUniforms U = make_uniforms(I, I, W, H);
@@ -869,13 +891,114 @@ gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));
     if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
-                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, 1,
-                                reinterpret_cast<float4*>(out_rgba), nullptr, st)) != GS_OK)
+                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, slab_t ? 0 : 1,
+                                reinterpret_cast<float4*>(out_rgba), nullptr, st, slab_t)) != GS_OK)
         return s;
-    // stage times span both calls: preprocess (gs_shard_project) ... composite;
-    // the exchange between them falls inside the depth-sort interval
+    // stage times span both calls: preprocess (project) ... composite; the
+    // exchange between them falls inside the depth-sort interval
     fill_stats(h, (uint64_t)h->stats.pairs, U);
     h->stats.tiles = T;
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, void* send,
+                           int64_t send_cap_bytes, int64_t* send_counts, void* stream) {
+    if (!send_counts) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (h) h->slab_frame = false;
+    gs::FrameUniforms U;
+    gs_status s = shard_preprocess(h, view, proj, W, H, st, &U);
+    if (s != GS_OK) return s;
+    Ownership own;
+    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+    if (!own.dev.owner) return fail(GS_ERR_STATE, "gs_shard_project: world size 1");
+    gs::DestRule rule{};
+    rule.owner = own.dev.owner;
+    return pack_exchange(h, rule, U.cell_mask != 0, send, send_cap_bytes, send_counts, st);
+}
+
+gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
+                          void* stream) {
+    if (!out_rgba) return fail(GS_ERR_INVALID_ARG, "gs_shard_render: null output");
+    if (h) h->slab_frame = false;
+    return render_received(h, recv, m, W, H, out_rgba, nullptr, static_cast<hipStream_t>(stream));
+}
+
+// ---- depth slabs ---------------------------------------------
+gs_status gs_slab_project(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, uint64_t* hist,
+                          void* stream) {
+    if (!hist) return fail(GS_ERR_INVALID_ARG, "gs_slab_project: null histogram");
+    if (h && h->opt.cap > 0) return fail(GS_ERR_UNSUPPORTED, "depth slabs: no fragment cap (it spans all slabs)");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (h) h->slab_frame = true;
+    gs::FrameUniforms U;
+    gs_status s = shard_preprocess(h, view, proj, W, H, st, &U);
+    if (s != GS_OK) return s;
+    GS_HIP(hipMemsetAsync(hist, 0, (size_t)gs::kSlabBins * 8, st));
+    GS_HIP(gs::launch_slab_histogram(h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(),
+                                     (uint32_t)h->n, U.cell_mask != 0,
+                                     reinterpret_cast<unsigned long long*>(hist), st));
+    h->slab_w = W;
+    h->slab_h = H;
+    return GS_OK;
+}
+
+gs_status gs_slab_bounds(const uint64_t* hist, int32_t world, uint32_t* bounds) {
+    static_assert(GS_SLAB_BINS == gs::kSlabBins && GS_SLAB_BIN_KEYS == (1 << gs::kSlabBinShift), "gsplat.h");
+    if (!hist || !bounds || world < 1 || world > gs::kMaxWorld)
+        return fail(GS_ERR_INVALID_ARG, "gs_slab_bounds: bad arguments");
+    uint64_t total = 0;
+    for (int k = 0; k < gs::kSlabBins; ++k) total += hist[k];
+    // bounds[d] = first key of the first bin whose preceding pairs reach d/world of the total
+    bounds[0] = 0;
+    uint64_t cum = 0;
+    int k = 0;
+    for (int d = 1; d < world; ++d) {
+        const unsigned __int128 target = (unsigned __int128)total * (unsigned)d;
+        while (k < gs::kSlabBins && (unsigned __int128)cum * (unsigned)world < target) cum += hist[k++];
+        bounds[d] = (uint32_t)k << gs::kSlabBinShift;
+    }
+    bounds[world] = gs::kSlabKeys;
+    return GS_OK;
+}
+
+gs_status gs_slab_pack(gs_handle* h, const uint32_t* bounds, void* send, int64_t send_cap_bytes, int64_t* send_counts,
+                       void* stream) {
+    if (!h || !bounds || !send_counts) return fail(GS_ERR_INVALID_ARG, "gs_slab_pack: bad arguments");
+    if (!h->slab_frame || !h->shard_frame) return fail(GS_ERR_STATE, "gs_slab_pack: call gs_slab_project first");
+    gs::DestRule rule{};
+    rule.dkey = h->dkey.as<uint32_t>();
+    rule.slabs = 1;
+    for (int d = 0; d <= h->world; ++d) {
+        if (d > 0 && bounds[d] < bounds[d - 1]) return fail(GS_ERR_INVALID_ARG, "gs_slab_pack: bounds not ascending");
+        rule.bounds[d] = bounds[d];
+    }
+    const bool masked = h->slab_w <= gs::kCellMaskDim && h->slab_h <= gs::kCellMaskDim;
+    return pack_exchange(h, rule, masked, send, send_cap_bytes, send_counts, static_cast<hipStream_t>(stream));
+}
+
+gs_status gs_slab_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* t_local, void* stream) {
+    if (!t_local) return fail(GS_ERR_INVALID_ARG, "gs_slab_render: null transmittance buffer");
+    if (!h || !h->slab_frame) return fail(GS_ERR_STATE, "gs_slab_render: not a slab frame (gs_slab_project)");
+    return render_received(h, recv, m, W, H, nullptr, t_local, static_cast<hipStream_t>(stream));
+}
+
+gs_status gs_slab_composite(gs_handle* h, const float* t_all, float* out_rgba, void* stream) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if (!out_rgba || (h->rank > 0 && !t_all)) return fail(GS_ERR_INVALID_ARG, "gs_slab_composite: bad arguments");
+    if (!h->slab_lists) return fail(GS_ERR_STATE, "gs_slab_composite: no transmittance pass (gs_slab_render)");
+    gs::CompositeArgs ca = h->slab_ca;
+    ca.slab = 2;
+    ca.slab_rank = h->rank;
+    ca.t_all = t_all;
+    ca.t_out = nullptr;
+    ca.out = reinterpret_cast<float4*>(out_rgba);
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, static_cast<hipStream_t>(stream)));
     return GS_OK;
 }
 

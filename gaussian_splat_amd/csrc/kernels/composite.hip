@@ -25,10 +25,20 @@
 
 namespace gs {
 
+#ifdef GS_COMPOSITE_COUNTERS
+// Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
+__device__ unsigned long long g_cc[8];
+#define GS_CC(i, v) (void)atomicAdd(&g_cc[i], (unsigned long long)(v))
+#else
+#define GS_CC(i, v) (void)0
+#endif
+
 // MODE 0: tile rule, 1: live50 rule, 2: cap threshold pass (index-ordered
 // lists; per pixel the id of the a.cap-th covering fragment).  CAP: composite
 // only fragments with id <= thr[pixel] (the first a.cap in arrival order).
-template <int MODE, bool CAP>
+// SLAB (depth-slab multi-GPU): 1 = transmittance pass, 2 =
+// colour pass from the earlier slabs' transmittance product.
+template <int MODE, bool CAP, int SLAB = 0>
 __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
     __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
@@ -74,6 +84,23 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
     if constexpr (CAP) {
         if (inside) thr = a.thr[(size_t)py * width + px];
     }
+    // slab colour pass: the state the earlier (farther) slabs leave, exactly
+    // the ordered product of their transmittance, rank order = depth order
+    float A0 = 0.0f, T0 = 1.0f;
+    if constexpr (SLAB == 2) {
+        float ts = 1.0f;
+        if (inside)
+            for (int j = 0; j < a.slab_rank; ++j) ts *= a.t_all[((size_t)j * height + py) * width + px];
+        if constexpr (MODE == 0) {
+            A = 1.0f - ts;
+            A0 = A;
+            done = done || A >= kSat;  // saturated before this slab: the loop broke earlier
+        } else {
+            T = ts;
+            T0 = T;
+            done = done || T < kTMin;
+        }
+    }
 
     // Composite update of one fragment (covered = box test and 0.01 cutoff).
     auto step = [&](bool covered, float alpha, float r, float g, float bl, uint32_t id) {
@@ -105,6 +132,13 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
         const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
         const float qq = __builtin_fmaf(v, v, u * u);
         const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+#ifdef GS_COMPOSITE_COUNTERS
+        {
+            const uint64_t m = __ballot(covered && !done);
+            if (lane == 0 && m) GS_CC(4, 1);
+            if (lane == 0) GS_CC(7, __popcll(m));
+        }
+#endif
         step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, id);
     };
 
@@ -146,8 +180,11 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
         }
         if (j + kTileThreads < rg.y) id_next = a.vals[j + kTileThreads];
     }
+    if (lane == 0) GS_CC(0, 1);
+    if (tid == 0) GS_CC(6, rg.y - rg.x);
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
         if (__syncthreads_count(!done) == 0) break;
+        if (tid == 0) GS_CC(5, 1);
         if (b + tid < rg.y) {
             s0[tid] = r0;
             s1[tid] = r1;
@@ -207,10 +244,40 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
                 body_v(a1, b1, c1, i1);
             }
         }
-        if (i < nl && __ballot(!done) != 0) body(wlist[wave][i]);
+        if (i < nl && __ballot(!done) != 0) body(wlist[wave][i++]);
+        if (lane == 0) GS_CC(3, i);
+#ifdef GS_COMPOSITE_COUNTERS
+        {  // iterations a split quadrant would need: max over 8x4 halves / 4x4 quarters
+            uint32_t h[2] = {0, 0}, qc[4] = {0, 0, 0, 0};
+            for (uint32_t j = 0; j < i; ++j) {
+                const float4 c = s2[wlist[wave][j]];
+                const uint32_t lo = rect_coords(__float_as_uint(c.z), a.cell_mask);
+                const uint32_t hi = rect_coords(__float_as_uint(c.w), a.cell_mask);
+                const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
+                for (uint32_t sy = 0; sy < 2; ++sy) {
+                    const bool oy = !(y1 < qy0 + 4 * sy || y0 > qy0 + 4 * sy + 3);
+                    h[sy] += oy;
+                    for (uint32_t sx = 0; sx < 2; ++sx) {
+                        const bool ox = !(x1 < qx0 + 4 * sx || x0 > qx0 + 4 * sx + 3);
+                        qc[sy * 2 + sx] += (oy && ox);
+                    }
+                }
+            }
+            if (lane == 0) {
+                GS_CC(1, h[0] > h[1] ? h[0] : h[1]);
+                GS_CC(2, max(max(qc[0], qc[1]), max(qc[2], qc[3])));
+            }
+        }
+#endif
     }
     if (!inside) return;
-    if constexpr (MODE == 2) {
+    if constexpr (SLAB == 1) {
+        a.t_out[(size_t)py * width + px] = MODE == 0 ? 1.0f - A : T;
+    } else if constexpr (SLAB == 2) {
+        // contributions: colour and the alpha this slab adds (sum over slabs)
+        a.out[(size_t)py * width + px] =
+            make_float4(C0, C1, C2, MODE == 0 ? A - A0 : (any ? T0 - T : 0.0f));
+    } else if constexpr (MODE == 2) {
         a.thr_out[(size_t)py * width + px] = thr;
     } else {
         float4 o;
@@ -228,20 +295,28 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
     }
 }
 
-template <int MODE, bool CAP>
+template <int MODE, bool CAP, int SLAB = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
     const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
     if (nwg == 0) return hipSuccess;
     // t0/t1 (optional) are recorded by the dispatch packet itself
-    hipExtLaunchKernelGGL(composite_kernel<MODE, CAP>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a, nwg);
+    hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
+                          nwg);
     return hipGetLastError();
 }
 
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
+    if (a.slab) {  // full frame, no cap
+        if (cap || a.rows || a.compact || a.out_bgra8 || (a.slab == 1 ? !a.t_out : (!a.out || (a.slab_rank && !a.t_all))))
+            return hipErrorInvalidValue;
+        if (a.slab == 1) return mode == 0 ? launch_mode<0, false, 1>(a, st, t0, t1) : launch_mode<1, false, 1>(a, st, t0, t1);
+        if (a.slab == 2) return mode == 0 ? launch_mode<0, false, 2>(a, st, t0, t1) : launch_mode<1, false, 2>(a, st, t0, t1);
+        return hipErrorInvalidValue;
+    }
     if (mode == 0) return cap ? launch_mode<0, true>(a, st, t0, t1) : launch_mode<0, false>(a, st, t0, t1);
     return cap ? launch_mode<1, true>(a, st, t0, t1) : launch_mode<1, false>(a, st, t0, t1);
 }
@@ -252,3 +327,11 @@ hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {
 }
 
 }  // namespace gs
+
+#ifdef GS_COMPOSITE_COUNTERS
+extern "C" int gs_debug_composite_counters(unsigned long long* out) {
+    unsigned long long zero[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cc), sizeof zero) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_cc), zero, sizeof zero) != hipSuccess;
+}
+#endif

@@ -82,6 +82,15 @@ struct CompositeArgs {
     int cap;
     const uint32_t* thr;    // read by the capped composite
     uint32_t* thr_out;      // written by launch_cap_threshold
+    // Depth-slab multi-GPU.  slab 1: transmittance pass,
+    // t_out[pixel] = the slab's own transmittance (1 - A for the tile rule).
+    // slab 2: colour pass starting from the ordered product of the earlier
+    // slabs' transmittance, t_all[j * W * H + pixel] for j < slab_rank;
+    // writes (C, delta A) contributions that sum over slabs to the frame.
+    int slab;
+    int slab_rank;
+    float* t_out;
+    const float* t_all;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break); with a.cap > 0 only fragments
@@ -93,15 +102,31 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 
-// ---- shard.hip (multi-GPU tile-row ownership) ------------------------------
+// ---- shard.hip (multi-GPU tile-row ownership / depth slabs) ---------------
 constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the record, depth key packed into the rect words
 constexpr int kXMaxDim = 4096;  // frame limit of the packed rect (12-bit coordinates)
 constexpr int kMaxWorld = 32;
-// dest_mask[i]: bit r set iff splat i touches a bin row owned by rank r (owner[by]).
+constexpr int kSlabKeys = 1 << kDepthBits;  // 15-bit depth keys
+constexpr int kSlabBinShift = 4;            // slab histogram: 2048 bins of 16 keys
+constexpr int kSlabBins = kSlabKeys >> kSlabBinShift;
+// Destination rule of a multi-GPU frame: bin-row owners (owner[by]) or, with
+// slabs, depth-key slabs (rank d receives keys in [bounds[d], bounds[d+1])).
+struct DestRule {
+    const uint8_t* owner;
+    const uint32_t* dkey;
+    uint32_t bounds[kMaxWorld + 1];
+    int slabs;
+};
+// dest_mask[i]: bit r set iff splat i goes to rank r (a bin row of its rect
+// owned by r, or its depth key in r's slab).
 // counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
-                              const uint8_t* owner, bool masked,
+                              const DestRule& rule, bool masked,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);
+// hist[key >> kSlabBinShift] += (splat, bin) pairs of every visible splat
+// (hist: kSlabBins u64, zeroed by the caller).
+hipError_t launch_slab_histogram(const uint32_t* dkey, const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n,
+                                 bool masked, unsigned long long* hist, hipStream_t st);
 // Exclusive scan of each destination row; dest_total[world].
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);
 // Pack exchange records grouped by destination, splat-index order inside.

@@ -286,11 +286,15 @@ __global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const Frame
                     const float4 rb = make_float4(e2x * k2, e2y * k2, a0.w, cr);
                     // 8x8 cells of the rect the ellipse provably misses (the
                     // composite skips them; frames up to kCellMaskDim px)
+#ifdef GS_AB_NO_MASKS  // A/B build: masks off (cost of the masks in this kernel)
+                    const uint32_t excl = 0u, bexcl = 0u;
+#else
                     const uint32_t excl =
                         U.cell_mask ? cell_exclusion_mask<3>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1) : 0u;
                     const uint32_t bexcl =
                         U.cell_mask ? cell_exclusion_mask<kBinShift>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1)
                                     : 0u;
+#endif
                     o[0] = ra;
                     o[1] = rb;
                     o[2] = make_float4(cg, cbl,

@@ -1,11 +1,13 @@
 // shard.hip — multi-GPU exchange kernels.
 //
 // Scenes are sharded by splat index (rank r holds a contiguous index range).
-// Every 32-px bin row has an owning rank (owner[by]): every
-// rank projects its shard, then sends each visible splat's 48-B exchange
-// record to the ranks owning a bin row its rect touches.  Received records arrive in source-rank order,
+// Row scheme: every 32-px bin row has an owning rank
+// (owner[by]); each rank projects its shard, then sends each visible splat's
+// 48-B exchange record to the ranks owning a bin row its rect touches.
+// Slab scheme (§6b): each visible splat goes to the rank whose depth-key slab
+// holds its key.  Either way received records arrive in source-rank order,
 // i.e. in global index order, so the receiving rank's stable sort reproduces
-// the single-GPU per-tile order exactly (bit-identical composite).
+// the single-GPU order of its bins (rows) or of its depth range (slabs).
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -31,9 +33,16 @@ __device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const u
     return m;
 }
 
+// Depth slab of a key: the d with bounds[d] <= key < bounds[d + 1].
+__device__ __forceinline__ uint32_t slab_of(uint32_t key, const DestRule& r, int world) {
+    uint32_t d = 0;
+    while ((int)d + 1 < world && key >= r.bounds[d + 1]) ++d;
+    return d;
+}
+
 __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __restrict__ rect_lo,
                                                           const uint32_t* __restrict__ rect_hi, uint32_t n,
-                                                          int world, const uint8_t* __restrict__ owner, bool masked,
+                                                          int world, const DestRule rule, bool masked,
                                                           uint32_t* __restrict__ dest_mask,
                                                           uint32_t* __restrict__ counts, uint32_t nblocks) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];
@@ -45,7 +54,7 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __rest
         uint32_t m = 0;
         if (i < n) {
             const BinRect r = bin_rect(rect_lo[i], rect_hi[i], masked);
-            if (!r.empty) m = row_mask(r.by0, r.by1, owner);
+            if (!r.empty) m = rule.slabs ? 1u << slab_of(rule.dkey[i], rule, world) : row_mask(r.by0, r.by1, rule.owner);
         }
         if (i < n) dest_mask[i] = m;
         for (int d = 0; d < world; ++d) {
@@ -154,13 +163,41 @@ __global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ r
 }
 
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
-                              const uint8_t* owner, bool masked,
+                              const DestRule& rule, bool masked,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st) {
     if (world < 1 || world > kMaxWorld) return hipErrorInvalidValue;
     if (nblocks == 0) return hipSuccess;
-    if (!owner) return hipErrorInvalidValue;
-    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, owner, masked, dest_mask, counts,
+    if (rule.slabs ? !rule.dkey : !rule.owner) return hipErrorInvalidValue;
+    shard_count_kernel<<<nblocks, 256, 0, st>>>(rect_lo, rect_hi, n, world, rule, masked, dest_mask, counts,
                                                 nblocks);
+    return hipGetLastError();
+}
+
+// Depth-slab boundaries are placed on pair counts (the composite's work), so
+// the histogram weighs each visible splat by its (splat, bin) pairs.  2048
+// bins of 16 depth keys, accumulated in LDS per block (keys concentrate in a
+// few hundred bins: global atomics per splat would serialise on them).
+__global__ __launch_bounds__(256) void slab_histogram_kernel(const uint32_t* __restrict__ dkey,
+                                                             const uint32_t* __restrict__ rect_lo,
+                                                             const uint32_t* __restrict__ rect_hi, uint32_t n,
+                                                             bool masked, unsigned long long* __restrict__ hist) {
+    __shared__ uint32_t h[kSlabBins];
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kSlabBins; k += 256) h[k] = 0;
+    __syncthreads();
+    const uint32_t end = min(n, (blockIdx.x + 1) * (uint32_t)kScanItems);
+    for (uint32_t i = blockIdx.x * kScanItems + threadIdx.x; i < end; i += 256) {
+        const uint32_t c = rect_tile_count(rect_lo[i], rect_hi[i], RowOwnership{nullptr, 0}, masked);
+        if (c) atomicAdd(&h[(dkey[i] & (kSlabKeys - 1)) >> kSlabBinShift], c);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kSlabBins; k += 256)
+        if (h[k]) atomicAdd(&hist[k], (unsigned long long)h[k]);
+}
+
+hipError_t launch_slab_histogram(const uint32_t* dkey, const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n,
+                                 bool masked, unsigned long long* hist, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    slab_histogram_kernel<<<(n + kScanItems - 1) / kScanItems, 256, 0, st>>>(dkey, rect_lo, rect_hi, n, masked, hist);
     return hipGetLastError();
 }
 

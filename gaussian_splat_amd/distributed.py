@@ -19,6 +19,19 @@ bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
 tests/test_distributed.py).  The backend object does the per-rank compute:
 `HipShardBackend` (libgsplat.so) in production; the gloo tests plug in a
 CPU backend from tests/.
+
+`SlabRenderer` is the north star's literal scheme: rank d
+composites depth slab d of the whole frame, then an RCCL reduce sums the
+per-pixel RGBA + weight (alpha) contributions:
+
+  1. gs_slab_project    preprocess; pair-weighted 15-bit depth-key histogram
+  2. all_reduce         histogram (SUM) -> slab bounds of equal pair counts
+  3. gs_slab_pack       one exchange record per visible splat, to its slab
+  4. all_to_all         counts, then records
+  5. gs_slab_render     the slab's bin lists + its own transmittance
+  6. all_gather         transmittance of every slab
+  7. gs_slab_composite  colour pass from the product of the farther slabs'
+  8. reduce             SUM of the (C, delta alpha) contributions -> rank 0
 """
 from __future__ import annotations
 
@@ -118,6 +131,65 @@ class HipShardBackend:
         return band
 
 
+SLAB_BINS = 2048      # GS_SLAB_BINS: slab histogram bins ...
+SLAB_BIN_KEYS = 16    # ... of 16 15-bit depth keys
+
+
+def slab_bounds(hist, world: int) -> np.ndarray:
+    """Slab key bounds [world + 1] of equal pair counts from the summed
+    histogram (gs_slab_bounds, host code of libgsplat.so)."""
+    h = np.ascontiguousarray(np.asarray(hist).view(np.uint64) if np.asarray(hist).dtype == np.int64
+                             else np.asarray(hist, np.uint64))
+    assert h.shape == (SLAB_BINS,)
+    b = np.zeros(world + 1, np.uint32)
+    check(lib().gs_slab_bounds(h.ctypes.data, int(world), b.ctypes.data), "gs_slab_bounds")
+    return b
+
+
+class HipSlabBackend(HipShardBackend):
+    """Per-rank compute of the depth-slab scheme through libgsplat.so."""
+
+    def project(self, view, proj, width, height):
+        import torch
+
+        hist = torch.empty(SLAB_BINS, dtype=torch.int64, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_slab_project(self.r._h, _mat16(view), _mat16(proj), width, height,
+                                    C.c_void_p(hist.data_ptr()), C.c_void_p(stream)), "gs_slab_project")
+        return hist
+
+    def pack(self, bounds):
+        import torch
+
+        b = np.ascontiguousarray(bounds, np.uint32)
+        counts = (C.c_int64 * self.world)()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_slab_pack(self.r._h, b.ctypes.data, C.c_void_p(self.send.data_ptr()), self.send.numel(),
+                                 counts, C.c_void_p(stream)), "gs_slab_pack")
+        return self.send, [int(c) for c in counts]
+
+    def render(self, recv, nrec, width, height):
+        import torch
+
+        self._recv = recv  # the colour pass reads the records again
+        t = torch.empty((height, width), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_slab_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
+                                   C.c_void_p(t.data_ptr()), C.c_void_p(stream)), "gs_slab_render")
+        return t
+
+    def composite(self, t_all):
+        import torch
+
+        h, w = t_all.shape[1], t_all.shape[2]
+        out = torch.empty((h, w, 4), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_slab_composite(self.r._h, C.c_void_p(t_all.data_ptr()), C.c_void_p(out.data_ptr()),
+                                      C.c_void_p(stream)), "gs_slab_composite")
+        self._recv = None
+        return out
+
+
 def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous index range of rank `rank` (balanced)."""
     b = n * rank // world
@@ -180,6 +252,101 @@ class ShardedRenderer:
             bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
             dist.gather(band, bands, dst=0, group=self.group)
         return assemble(bands, width, height, self.world, getattr(self.b, "owner", None)) if self.rank == 0 else None
+
+
+def _all_reduce_sum(t, group):
+    import torch.distributed as dist
+
+    if _host_staged(group):
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+    return t
+
+
+def _all_gather(t, world, group):
+    import torch
+    import torch.distributed as dist
+
+    if _host_staged(group):
+        h = t.cpu()
+        out = torch.empty((world,) + tuple(h.shape), dtype=h.dtype)
+        dist.all_gather(list(out.unbind(0)), h, group=group)
+        return out.to(t.device)
+    out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+class SlabRenderer:
+    """One rank of a depth-slab multi-GPU frame (torch.distributed initialised)."""
+
+    def __init__(self, backend, rank: int, world: int, group=None):
+        self.b, self.rank, self.world, self.group = backend, rank, world, group
+
+    def render(self, view, proj, width, height, gather: bool = True):
+        """The frame on rank 0 (None elsewhere) when gather=True (RGBA reduce),
+        else this rank's (C, delta alpha) contribution."""
+        import torch.distributed as dist
+
+        hist = _all_reduce_sum(self.b.project(view, proj, width, height), self.group)
+        bounds = slab_bounds(hist.cpu().numpy(), self.world)
+        send, counts = self.b.pack(bounds)
+        recv, nrec = exchange(send, counts, self.b.xbytes, self.world, self.group)
+        t = self.b.render(recv, nrec, width, height)
+        t_all = _all_gather(t, self.world, self.group) if self.world > 1 else t[None]
+        out = self.b.composite(t_all)
+        if not gather or self.world == 1:
+            return out
+        if _host_staged(self.group):
+            h = out.cpu()
+            dist.reduce(h, dst=0, group=self.group)
+            out.copy_(h)
+        else:
+            dist.reduce(out, dst=0, group=self.group)
+        return out if self.rank == 0 else None
+
+
+def render_virtual_slabs(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,
+                         mode: str = "tile", device: int = 0, parts: bool = False):
+    """Depth-slab scheme with all ranks in one process on one GPU (collectives
+    by slicing / summing in rank order).  Returns the frame, and with
+    parts=True also the bounds, per-slab transmittance and contributions."""
+    import torch
+
+    opts = Options(mode=mode, sh_degree=sh_degree, crop=False)
+    backends = []
+    for r in range(world):
+        b, e = shard_bounds(scene.n, world, r)
+        be = HipSlabBackend(scene.subset(slice(b, e)), r, world, b, opts, device)
+        backends.append(be)
+    hist = sum(be.project(view, proj, width, height) for be in backends)
+    bounds = slab_bounds(hist.cpu().numpy(), world)
+    sends = [be.pack(bounds) for be in backends]
+    xb = backends[0].xbytes
+    ts, recvs = [], []
+    for dst in range(world):
+        chunks = []
+        for src in range(world):
+            buf, counts = sends[src]
+            off = sum(counts[:dst]) * xb
+            chunks.append(buf[off: off + counts[dst] * xb].clone())
+        recv = torch.cat(chunks)
+        nrec = recv.numel() // xb
+        recvs.append(recv if recv.numel() else backends[dst].empty(xb))
+        ts.append(backends[dst].render(recvs[-1], nrec, width, height))
+    t_all = torch.stack(ts)
+    contrib = [be.composite(t_all) for be in backends]
+    frame = contrib[0].clone()
+    for c in contrib[1:]:
+        frame += c
+    torch.cuda.synchronize()
+    if parts:
+        return (frame.cpu().numpy(), bounds, t_all.cpu().numpy(), [c.cpu().numpy() for c in contrib],
+                [r.cpu().numpy() for r in recvs])
+    return frame.cpu().numpy()
 
 
 def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,

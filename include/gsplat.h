@@ -177,6 +177,40 @@ gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t 
                           float *out_rgba, void *hip_stream);
 int32_t gs_exchange_record_bytes(void);
 
+/* ---- multi-GPU: depth slabs + RGBA reduce --------- */
+/* The north star's scheme: splat-index shards, each rank composites one
+ * depth slab of the whole frame, and the per-pixel RGBA+weight contributions
+ * are sum-reduced (RCCL) into the frame.  Per frame, on every rank:
+ *   gs_slab_project   preprocess the shard; hist (device, GS_SLAB_BINS u64) =
+ *                     its (splat, bin) pairs per GS_SLAB_BIN_KEYS 15-bit depth keys
+ *   (all-reduce SUM of hist; gs_slab_bounds on the host, same on every rank)
+ *   gs_slab_pack      one exchange record per visible splat, to the rank whose
+ *                     slab [bounds[d], bounds[d+1]) holds its key
+ *   (all-to-all of counts and records)
+ *   gs_slab_render    sort/bin/composite the slab over the full frame; t_local
+ *                     (device, W*H f32) = the slab's own transmittance
+ *   (all-gather of t_local into t_all, rank-major [world][H][W])
+ *   gs_slab_composite colour pass starting from the product of the earlier
+ *                     ranks' (farther slabs') transmittance; out_rgba (device,
+ *                     W*H*4 f32) = (C, delta alpha) contributions
+ *   (reduce SUM of out_rgba = the frame)
+ * Rank order is composite (far-to-near) order.  The result equals the 1-GPU
+ * frame up to fp32 reassociation of the transmittance product;
+ * the row scheme above is bit-identical.  No fragment cap.  `recv` must stay
+ * alive until gs_slab_composite returns. */
+#define GS_SLAB_BINS 2048   /* histogram bins ... */
+#define GS_SLAB_BIN_KEYS 16 /* ... of 16 depth keys: slab bounds are multiples of 16 */
+gs_status gs_slab_project(gs_handle *h, const float view[16], const float proj[16], int32_t width, int32_t height,
+                          uint64_t *hist, void *hip_stream);
+/* bounds[world + 1] (depth keys) from the summed histogram (host): slabs of
+ * equal pair counts, to one histogram bin. */
+gs_status gs_slab_bounds(const uint64_t *hist, int32_t world, uint32_t *bounds);
+gs_status gs_slab_pack(gs_handle *h, const uint32_t *bounds, void *send, int64_t send_cap_bytes, int64_t *send_counts,
+                       void *hip_stream);
+gs_status gs_slab_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height, float *t_local,
+                         void *hip_stream);
+gs_status gs_slab_composite(gs_handle *h, const float *t_all, float *out_rgba, void *hip_stream);
+
 /* ---- PLY loader (PLYLoader::load drop-in) ----------------------------- */
 /* Loads into a malloc'd PointData array (62 floats/point).  compat = 1
  * reproduces every reference quirk (ASCII 2N points). */

@@ -668,9 +668,13 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
     free(ord);
 }
 
-int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
-                          const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
-                          ora_stats *st) {
+/* slab: 0 = plain composite; 1 = depth-slab transmittance pass (out = W*H
+ * floats, the slab's own transmittance); 2 = colour pass from the ordered
+ * product of the earlier slabs' transmittance t_all[j][py][px], j < slab_rank
+ * (out = (C, delta alpha) contributions).  DESIGN.md §6b. */
+static int composite_records_impl(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
+                                  const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
+                                  ora_stats *st, int slab, int slab_rank, const float *t_all) {
     int mode = opt ? opt->mode : ORA_MODE_TILE;
     int cap = opt ? opt->cap : 0;
     int nth = opt ? opt->nthreads : 0;
@@ -753,8 +757,54 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
             for (int py = ty * TILE; py < ty * TILE + TILE && py < H; ++py) {
                 int orow = compact ? slot[py / OWN_ROW] * OWN_ROW + py % OWN_ROW : py;
                 for (int px = tx * TILE; px < tx * TILE + TILE && px < W; ++px) {
-                    float *o = out + ((size_t)orow * W + px) * 4;
+                    float *o = out + ((size_t)orow * W + px) * (slab == 1 ? 1 : 4);
                     int c = 0;
+                    if (slab) { /* depth slab: same walk, from the slab's start state */
+                        float ts = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+                        if (slab == 2)
+                            for (int j = 0; j < slab_rank; ++j) ts *= t_all[((size_t)j * H + py) * W + px];
+                        if (mode == ORA_MODE_TILE) {
+                            float A = slab == 2 ? 1.0f - ts : 0.0f, A0 = A;
+                            if (!(A >= ORA_SAT))
+                                for (int64_t k = 0; k < m; ++k) {
+                                    const ora_record *r = &rec[ord[k].idx];
+                                    float al = frag_alpha(r, px, py);
+                                    if (al < 0.0f) continue;
+                                    float sa = al * (1.0f - A);
+                                    C0 = fmaf(r->r, sa, C0);
+                                    C1 = fmaf(r->g, sa, C1);
+                                    C2 = fmaf(r->b, sa, C2);
+                                    A = A + sa;
+                                    if (A >= ORA_SAT) break;
+                                }
+                            if (slab == 1) {
+                                o[0] = 1.0f - A;
+                            } else {
+                                o[0] = C0; o[1] = C1; o[2] = C2; o[3] = A - A0;
+                            }
+                        } else {
+                            float T = slab == 2 ? ts : 1.0f, T0 = T;
+                            int any = 0;
+                            if (!(T < ORA_TMIN))
+                                for (int64_t k = 0; k < m; ++k) {
+                                    const ora_record *r = &rec[ord[k].idx];
+                                    float al = frag_alpha(r, px, py);
+                                    if (al < 0.0f) continue;
+                                    any = 1;
+                                    C0 = fmaf(r->r, T, C0);
+                                    C1 = fmaf(r->g, T, C1);
+                                    C2 = fmaf(r->b, T, C2);
+                                    T = T * (1.0f - al);
+                                    if (T < ORA_TMIN) break;
+                                }
+                            if (slab == 1) {
+                                o[0] = T;
+                            } else {
+                                o[0] = C0; o[1] = C1; o[2] = C2; o[3] = any ? T0 - T : 0.0f;
+                            }
+                        }
+                        continue;
+                    }
                     if (cap == 0) {
                         if (mode == ORA_MODE_TILE) { /* fused early-break walk */
                             float A = 0.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -816,6 +866,18 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
     free(list);
     free(cnt);
     return 1;
+}
+
+int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
+                          const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
+                          ora_stats *st) {
+    return composite_records_impl(rec, dkey, n, W, H, opt, owner, rank, compact, out, st, 0, 0, NULL);
+}
+
+int ora_composite_slab(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H, const ora_options *opt,
+                       int pass, int slab_rank, const float *t_all, float *out) {
+    if ((pass != 1 && pass != 2) || (opt && opt->cap > 0) || (pass == 2 && slab_rank > 0 && !t_all)) return 0;
+    return composite_records_impl(rec, dkey, n, W, H, opt, NULL, 0, 0, out, NULL, pass, slab_rank, t_all);
 }
 
 int ora_render(const ora_scene *s, const float V[16], const float P[16], int W, int H,

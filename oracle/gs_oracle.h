@@ -133,6 +133,15 @@ int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n
                           const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
                           ora_stats *stats);
 
+/* Depth-slab multi-GPU decomposition:
+ * pass 1 writes W*H floats, the slab's own transmittance (tile rule: 1 - A,
+ * with the A >= 0.99 break; live50: T with the T < 0.01 break); pass 2 starts
+ * from the product of t_all[j] (j < slab_rank, [world][H][W]) and writes the
+ * (C, delta alpha) contributions, W*H*4 floats, whose sum over slabs is the
+ * frame.  No cap.  Returns 0 on bad arguments. */
+int ora_composite_slab(const ora_record *rec, const uint32_t *dkey, int64_t n, int width, int height,
+                       const ora_options *opt, int pass, int slab_rank, const float *t_all, float *out);
+
 /* Composite a single synthetic fragment list (depth, rgb, alpha) with the S1
  * sort and A1 / A1' rule — the unit the reference's tile_sort_composite and
  * compute_sort_composite operate on.  frags: n*5 floats (depth, r, g, b, a),

@@ -62,6 +62,9 @@ def lib() -> C.CDLL:
                                             C.POINTER(OraOptions), C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                             C.POINTER(OraStats)]
         L.ora_composite_records.restype = C.c_int
+        L.ora_composite_slab.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int, C.POINTER(OraOptions),
+                                         C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.ora_composite_slab.restype = C.c_int
         L.ora_composite_list.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.ora_f32_to_f16_bits.argtypes = [C.c_float]
         L.ora_f32_to_f16_bits.restype = C.c_uint16
@@ -169,6 +172,22 @@ def composite_records(rec, dkey, width, height, owner=None, rank=0, compact=Fals
     lib().ora_composite_records(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
                                 C.byref(o), None if own is None else own.ctypes.data, int(rank),
                                 int(bool(compact)), out.ctypes.data, C.byref(st))
+    return out
+
+
+def composite_slab(rec, dkey, width, height, pas, rank=0, t_all=None, mode="tile", nthreads=0):
+    """Depth-slab passes (gs_oracle.h ora_composite_slab): pass 1 -> (H, W)
+    transmittance, pass 2 -> (H, W, 4) contributions from t_all [world, H, W]."""
+    rec = np.ascontiguousarray(rec, RECORD_DTYPE)
+    dkey = np.ascontiguousarray(dkey, np.uint32)
+    out = np.zeros((height, width) if pas == 1 else (height, width, 4), np.float32)
+    ta = None if t_all is None else np.ascontiguousarray(t_all, np.float32)
+    o = OraOptions(0 if mode == "tile" else 1, 0, int(nthreads))
+    ok = lib().ora_composite_slab(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
+                                  C.byref(o), int(pas), int(rank), None if ta is None else ta.ctypes.data,
+                                  out.ctypes.data)
+    if not ok:
+        raise ValueError("ora_composite_slab: bad arguments")
     return out
 
 

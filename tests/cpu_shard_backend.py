@@ -69,3 +69,51 @@ class OracleShardBackend:
                                   rank=self.rank, compact=True, mode=self.mode, cap=self.cap)
         band[: out.shape[0]] = out
         return torch.from_numpy(band)
+
+
+class OracleSlabBackend(OracleShardBackend):
+    """CPU stand-in for HipSlabBackend: depth slabs, oracle compute, the
+    product's record format, slab rule (gs_slab_bounds) and collectives."""
+
+    def project(self, view, proj, width, height):
+        import torch
+
+        from gaussian_splat_amd.distributed import SLAB_BIN_KEYS, SLAB_BINS
+
+        self._rec, self._dk, self._nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
+        vis = self._nt > 0
+        hist = np.bincount(self._dk[vis] // SLAB_BIN_KEYS, weights=self._nt[vis], minlength=SLAB_BINS).astype(np.int64)
+        return torch.from_numpy(hist)
+
+    def pack(self, bounds):
+        import torch
+
+        rec, dk, vis = self._rec, self._dk, self._nt > 0
+        slab = np.searchsorted(np.asarray(bounds[1:-1], np.int64), dk.astype(np.int64), side="right")
+        parts, counts = [], []
+        for d in range(self.world):
+            idx = np.nonzero(vis & (slab == d))[0]
+            x = rec[idx].copy()
+            x["rect_lo"] = _xpack(rec["rect_lo"][idx], dk[idx] & 0xFF)
+            x["rect_hi"] = _xpack(rec["rect_hi"][idx], dk[idx] >> 8)
+            parts.append(x)
+            counts.append(len(idx))
+        buf = np.concatenate(parts).view(np.uint8)
+        return torch.from_numpy(buf.copy() if buf.size else np.zeros(1, np.uint8)), counts
+
+    def render(self, recv, nrec, width, height):
+        import torch
+
+        raw = recv.numpy()[: nrec * 48].copy().view(XREC)
+        self._srec = raw.copy()
+        self._sdk = (raw["rect_lo"] >> 24) | ((raw["rect_hi"] >> 24) << 8)
+        self._srec["rect_lo"] = _xunpack(raw["rect_lo"])
+        self._srec["rect_hi"] = _xunpack(raw["rect_hi"])
+        return torch.from_numpy(O.composite_slab(self._srec, self._sdk, width, height, 1, mode=self.mode))
+
+    def composite(self, t_all):
+        import torch
+
+        ta = t_all.numpy()
+        return torch.from_numpy(O.composite_slab(self._srec, self._sdk, ta.shape[2], ta.shape[1], 2, rank=self.rank,
+                                                 t_all=ta, mode=self.mode))

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Composite work counters on the bench workload (debug build):
+
+  python tools/build_variant.py cnt -DGS_COMPOSITE_COUNTERS
+  GSPLAT_LIB=ab/cnt.so python tools/composite_counters.py [--splats N]
+"""
+import argparse
+import ctypes as C
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--splats", type=int, default=6_000_000)
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--sh", type=int, default=3)
+ap.add_argument("--seed", type=int, default=2)
+args = ap.parse_args()
+
+import torch  # noqa: E402
+
+from gaussian_splat_amd import scene as S  # noqa: E402
+from gaussian_splat_amd._lib import lib  # noqa: E402
+from gaussian_splat_amd.api import InstancedSplatRenderer, Options, default_camera  # noqa: E402
+
+W, H = args.width, args.height
+scene = S.synthetic_scene(args.splats, seed=args.seed, sh_degree=args.sh, aspect=W / H)
+cam = default_camera(W, H)
+V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+r = InstancedSplatRenderer(scene, Options(mode="tile", sh_degree=args.sh, crop=False))
+r.initialize(0)
+out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
+f = lib().gs_debug_composite_counters
+f.argtypes = [C.POINTER(C.c_uint64)]
+buf = (C.c_uint64 * 8)()
+r.render(V, P, W, H, out=out)
+torch.cuda.synchronize()
+f(buf)
+r.render(V, P, W, H, out=out)
+torch.cuda.synchronize()
+f(buf)
+c = list(buf)
+st = r.last_stats()
+waves, wg = c[0], c[0] // 4
+names = ["waves", "iters if 8x4 halves", "iters if 4x4 quarters", "bodies", "bodies w/ covered lane", "wg-batches", "list entries",
+         "covered lanes"]
+for n, v in zip(names, c):
+    print(f"{n:>24}: {v}")
+print(f"pairs {st['pairs']}  list/bin {st['pairs'] / (st['tiles']):.0f}")
+print(f"per wave: halves {c[1] / waves:.1f}  quarters {c[2] / waves:.1f}  bodies {c[3] / waves:.1f}  "
+      f"covered-bodies {c[4] / waves:.1f}  lanes/covered-body {c[7] / max(c[4], 1):.1f}")
+print(f"per wg: batches {c[5] / wg:.2f}  list {c[6] / wg:.0f}  batches if no exit {c[6] / wg / 256:.2f}")
