@@ -26,7 +26,7 @@ POINT_FLOATS = 62  # sizeof(PointData) / 4, src/ply_loader.h:7-28
 RECORD_DTYPE = np.dtype([("cx", "<f4"), ("cy", "<f4"), ("ax", "<f4"), ("ay", "<f4"), ("bx", "<f4"),
                          ("by", "<f4"), ("opacity", "<f4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4"),
                          ("rect_lo", "<u4"), ("rect_hi", "<u4")])
-MODES = {"tile": 0, "live50": 1}
+MODES = {"tile": 0, "live50": 1, "mlab": 2}
 
 
 def _mat16(m) -> C.Array:

@@ -144,6 +144,8 @@ gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& op
         return fail(GS_ERR_INVALID_ARG, "gs_scene_soa: null array");
     if (opt.sh_degree < 0 || opt.sh_degree > 3) return fail(GS_ERR_INVALID_ARG, "sh_degree must be 0..3");
     if (opt.cap < 0) return fail(GS_ERR_INVALID_ARG, "cap must be >= 0");
+    if (opt.mode != GS_MODE_TILE && opt.mode != GS_MODE_LIVE50 && opt.mode != GS_MODE_MLAB)
+        return fail(GS_ERR_INVALID_ARG, "bad mode");
     if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
     if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
     h->opt = opt;
@@ -410,8 +412,24 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     ca.out = out;
     ca.out_bgra8 = out_bgra8;
     ca.cap = h->opt.cap;
+    ca.dkey = dkey;
     const uint32_t* vals = nullptr;
     uint64_t P = 0;
+    const bool mlab = h->opt.mode == GS_MODE_MLAB;
+    if (mlab && (ca.cap > 0 || slab_t))
+        return fail(GS_ERR_UNSUPPORTED, "MLAB mode has no fragment cap and no depth slabs");
+    if (mlab) {
+        // MLAB k-buffer: arrival (index) order per pixel, no depth sort
+        mark(h, 2, st);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P);
+        if (s != GS_OK) return s;
+        ca.vals = vals;
+        ca.ranges = h->ranges.as<uint2>();
+        GS_HIP(gs::launch_composite(ca, h->opt.mode, st, kernel_event(h, 2), kernel_event(h, 3)));
+        mark(h, 7, st);
+        h->stats.pairs = (int64_t)P;
+        return GS_OK;
+    }
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
@@ -622,7 +640,8 @@ void gs_destroy(gs_handle* h) {
 }
 
 gs_status gs_set_mode(gs_handle* h, int32_t mode) {
-    if (!h || (mode != GS_MODE_TILE && mode != GS_MODE_LIVE50)) return fail(GS_ERR_INVALID_ARG, "bad mode");
+    if (!h || (mode != GS_MODE_TILE && mode != GS_MODE_LIVE50 && mode != GS_MODE_MLAB))
+        return fail(GS_ERR_INVALID_ARG, "bad mode");
     h->opt.mode = mode;
     return GS_OK;
 }
@@ -933,6 +952,7 @@ gs_status gs_slab_project(gs_handle* h, const float* view, const float* proj, in
                           void* stream) {
     if (!hist) return fail(GS_ERR_INVALID_ARG, "gs_slab_project: null histogram");
     if (h && h->opt.cap > 0) return fail(GS_ERR_UNSUPPORTED, "depth slabs: no fragment cap (it spans all slabs)");
+    if (h && h->opt.mode == GS_MODE_MLAB) return fail(GS_ERR_UNSUPPORTED, "depth slabs: no MLAB mode");
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (h) h->slab_frame = true;
     gs::FrameUniforms U;

@@ -33,16 +33,88 @@ __device__ unsigned long long g_cc[8];
 #define GS_CC(i, v) (void)0
 #endif
 
+// MLAB k-buffer (gaussian_splat.metal:201-361): six premultiplied half
+// layers + half depths per pixel in registers, updated per covering fragment
+// in arrival order with the reference's insertion and under-merge, resolved
+// front to back.  Every op is a correctly rounded half op (oracle: mlab_*).
+namespace mlab {
+using h16 = _Float16;
+__device__ __forceinline__ h16 mul(h16 a, h16 b) { return (h16)((float)a * (float)b); }  // exact in f32, one rounding
+__device__ __forceinline__ h16 add(h16 a, h16 b) { return (h16)((float)a + (float)b); }  // no double-rounding tie
+__device__ __forceinline__ h16 sub(h16 a, h16 b) { return (h16)((float)a - (float)b); }
+constexpr int kLayers = 6;  // NUM_OIT_LAYERS (gaussian_splat.metal:11)
+struct KBuf {
+    h16 L[kLayers][4];
+    h16 D[kLayers];
+    __device__ __forceinline__ void clear() {  // all attachments (0,0,0,1) (instanced_splat_renderer.mm:540)
+#pragma unroll
+        for (int i = 0; i < kLayers; ++i) {
+            L[i][0] = L[i][1] = L[i][2] = (h16)0.0f;
+            L[i][3] = (h16)1.0f;
+            D[i] = (h16)0.0f;
+        }
+        D[3] = (h16)1.0f;  // depths01.a
+    }
+    __device__ __forceinline__ void insert(float r, float g, float b, float alpha, h16 nd) {  // :206-294
+        // alpha is rounded to f32 first (float alpha = g * opacity, :200), then
+        // to half: keep the compiler from fusing the product and the
+        // conversion into one v_fma_mix rounding
+        asm volatile("" : "+v"(alpha));
+        const h16 ha = (h16)alpha;
+        h16 nl[4] = {mul((h16)r, ha), mul((h16)g, ha), mul((h16)b, ha), sub((h16)1.0f, ha)};
+#pragma unroll
+        for (int i = 0; i < kLayers; ++i) {
+            const bool ins = nd >= D[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const h16 t = L[i][c];
+                L[i][c] = ins ? nl[c] : t;
+                nl[c] = ins ? t : nl[c];
+            }
+            const h16 t = D[i];
+            D[i] = ins ? nd : t;
+            nd = ins ? t : nd;
+        }
+        const int l = kLayers - 1;
+        const bool closer = nd >= D[l];
+        h16 m[4];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const h16 fr = closer ? nl[c] : L[l][c], bk = closer ? L[l][c] : nl[c];
+            const h16 ba = closer ? L[l][3] : nl[3];
+            m[c] = add(bk, mul(fr, ba));
+        }
+        m[3] = mul(nl[3], L[l][3]);  // front.a * back.a (commutative)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) L[l][c] = m[c];
+        D[l] = closer ? nd : D[l];
+    }
+    __device__ __forceinline__ float4 resolve() const {  // :330-361
+        h16 C0 = (h16)0.0f, C1 = C0, C2 = C0, at = (h16)1.0f;
+#pragma unroll
+        for (int i = 0; i < kLayers; ++i) {
+            C0 = add(C0, mul(L[i][0], at));
+            C1 = add(C1, mul(L[i][1], at));
+            C2 = add(C2, mul(L[i][2], at));
+            at = mul(at, L[i][3]);
+        }
+        return make_float4((float)C0, (float)C1, (float)C2, (float)sub((h16)1.0f, at));
+    }
+};
+}  // namespace mlab
+
 // MODE 0: tile rule, 1: live50 rule, 2: cap threshold pass (index-ordered
-// lists; per pixel the id of the a.cap-th covering fragment).  CAP: composite
+// lists; per pixel the id of the a.cap-th covering fragment), 3: MLAB
+// k-buffer (index-ordered lists, no early out).  CAP: composite
 // only fragments with id <= thr[pixel] (the first a.cap in arrival order).
 // SLAB (depth-slab multi-GPU): 1 = transmittance pass, 2 =
 // colour pass from the earlier slabs' transmittance product.
 template <int MODE, bool CAP, int SLAB = 0>
-__global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
+__global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
     __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
     __shared__ uint32_t sid[kIds ? kTileThreads : 1];
+    __shared__ _Float16 shd[MODE == 3 ? kTileThreads : 1];  // MLAB: half depth of each record
     __shared__ uint8_t wlist[4][kTileThreads];
 
     // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
@@ -87,6 +159,8 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
     // slab colour pass: the state the earlier (farther) slabs leave, exactly
     // the ordered product of their transmittance, rank order = depth order
     float A0 = 0.0f, T0 = 1.0f;
+    mlab::KBuf kb;
+    if constexpr (MODE == 3) kb.clear();
     if constexpr (SLAB == 2) {
         float ts = 1.0f;
         if (inside)
@@ -160,6 +234,8 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
                 thr = sid[k];
                 done = true;
             }
+        } else if constexpr (MODE == 3) {
+            if (!done && covered) kb.insert(bb.w, cc.x, cc.y, bb.z * gs_gauss(qq), shd[k]);
         } else {
             step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, kIds ? sid[k] : 0u);
         }
@@ -190,6 +266,8 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
             s1[tid] = r1;
             s2[tid] = r2;
             if constexpr (kIds) sid[tid] = id_cur;
+            if constexpr (MODE == 3)  // half(zF) from the depth key (dkey = 0x7C00 - half bits)
+                shd[tid] = __builtin_bit_cast(_Float16, (uint16_t)(kDepthInf - a.dkey[id_cur]));
         }
         __syncthreads();
         {
@@ -232,7 +310,7 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
         for (; i + 1 < nl; i += 2) {
             if (__ballot(!done) == 0) break;
             const uint32_t k0 = wlist[wave][i], k1 = wlist[wave][i + 1];
-            if constexpr (MODE == 2) {
+            if constexpr (MODE == 2 || MODE == 3) {
                 body(k0);
                 body(k1);
             } else {
@@ -279,6 +357,13 @@ __global__ __launch_bounds__(256, 8) void composite_kernel(CompositeArgs a, uint
             make_float4(C0, C1, C2, MODE == 0 ? A - A0 : (any ? T0 - T : 0.0f));
     } else if constexpr (MODE == 2) {
         a.thr_out[(size_t)py * width + px] = thr;
+    } else if constexpr (MODE == 3) {
+        const float4 o = kb.resolve();
+        const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
+        if (a.out_bgra8)
+            a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
+        else
+            a.out[(size_t)orow * width + px] = o;
     } else {
         float4 o;
         if constexpr (MODE == 0) {
@@ -317,6 +402,7 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
         if (a.slab == 2) return mode == 0 ? launch_mode<0, false, 2>(a, st, t0, t1) : launch_mode<1, false, 2>(a, st, t0, t1);
         return hipErrorInvalidValue;
     }
+    if (mode == 2) return cap || !a.dkey ? hipErrorInvalidValue : launch_mode<3, false>(a, st, t0, t1);  // MLAB
     if (mode == 0) return cap ? launch_mode<0, true>(a, st, t0, t1) : launch_mode<0, false>(a, st, t0, t1);
     return cap ? launch_mode<1, true>(a, st, t0, t1) : launch_mode<1, false>(a, st, t0, t1);
 }

@@ -69,6 +69,7 @@ struct CompositeArgs {
     const uint32_t* vals;   // sorted splat ids (index into rec)
     const uint2* ranges;    // [bins] -> [start, end) into vals
     const float4* rec;      // records, rec_stride float4 apart (3 local, 4 exchange)
+    const uint32_t* dkey;   // depth keys parallel to rec (MLAB reads half(zF) from them)
     int rec_stride;
     int width, height, tiles_x, tiles_y;  // frame and 32x32 bin grid
     const uint16_t* rows;   // owned bin rows, ascending (nullptr: every row)
@@ -93,8 +94,9 @@ struct CompositeArgs {
     const float* t_all;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
-// break), 1 = live50 rule (T < 0.01 break); with a.cap > 0 only fragments
-// with id <= thr[pixel] are composited.
+// break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals
+// index-ordered, a.dkey set, no cap); with a.cap > 0 only fragments with
+// id <= thr[pixel] are composited.
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0 = nullptr,
                             hipEvent_t t1 = nullptr);
 // Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):

@@ -49,8 +49,10 @@ typedef enum {
 } gs_status;
 
 /* Composite rule.  TILE = gaussian_splat_tile.metal:251-266 (contract
- * default); LIVE50 = gaussian_splat_50layer.metal:208-222. */
-typedef enum { GS_MODE_TILE = 0, GS_MODE_LIVE50 = 1 } gs_mode;
+ * default); LIVE50 = gaussian_splat_50layer.metal:208-222; MLAB = the
+ * 6-layer k-buffer of gaussian_splat.metal:201-361 (arrival order, half
+ * arithmetic, resolve output before the drawable blend; no cap, no slabs). */
+typedef enum { GS_MODE_TILE = 0, GS_MODE_LIVE50 = 1, GS_MODE_MLAB = 2 } gs_mode;
 
 typedef struct gs_options {
     int32_t mode;          /* gs_mode */

@@ -621,6 +621,87 @@ static int kv_cmp(const void *a, const void *b) {
     return x->idx < y->idx ? -1 : (x->idx > y->idx);
 }
 
+/* ---- MLAB k-buffer (gaussian_splat.metal:201-361) ------------------------
+ * Metal half arithmetic is emulated op by op: each half op is computed
+ * exactly in double (sums and products of two halves are exact there) and
+ * rounded once to the nearest half, ties to even, i.e. a correctly rounded
+ * half op, as gfx950's v_*_f16 are.  Halves are carried as floats. */
+static float hr(double x) {
+    if (x != x) return (float)x;
+    double ax = fabs(x);
+    if (ax >= 65520.0) return x > 0 ? INFINITY : -INFINITY; /* RNE past 65504 */
+    if (ax == 0.0) return (float)x;
+    int E;
+    frexp(ax, &E);   /* ax in [2^(E-1), 2^E) */
+    int e = E - 1;
+    if (e < -14) e = -14; /* subnormal quantum 2^-24 */
+    double q = ldexp(1.0, e - 10);
+    double v = rint(ax / q) * q;
+    return (float)(x < 0 ? -v : v);
+}
+
+static float half_from_bits(uint32_t b) {
+    uint32_t e = (b >> 10) & 0x1Fu, m = b & 0x3FFu;
+    float v = e ? ldexpf((float)(m | 0x400u), (int)e - 25) : ldexpf((float)m, -24);
+    return (b & 0x8000u) ? -v : v;
+}
+
+#define MLAB_LAYERS 6 /* NUM_OIT_LAYERS, gaussian_splat.metal:11 */
+typedef struct {
+    float L[MLAB_LAYERS][4]; /* premultiplied rgb + visibility (half values) */
+    float D[MLAB_LAYERS];    /* half depths */
+} mlab_kbuf;
+
+/* Clear to (0,0,0,1) on all 8 attachments (instanced_splat_renderer.mm:540):
+ * layers (0,0,0,1); depths01 = (0,0,0,1) -> depth[3] starts at 1. */
+static void mlab_clear(mlab_kbuf *k) {
+    for (int i = 0; i < MLAB_LAYERS; ++i) {
+        k->L[i][0] = k->L[i][1] = k->L[i][2] = 0.0f;
+        k->L[i][3] = 1.0f;
+        k->D[i] = 0.0f;
+    }
+    k->D[3] = 1.0f;
+}
+
+/* fragment_main (gaussian_splat.metal:206-294), one covering fragment. */
+static void mlab_insert(mlab_kbuf *k, float r, float g, float b, float alpha, float depth_h) {
+    float ha = hr(alpha);
+    float nl[4] = {hr((double)hr(r) * ha), hr((double)hr(g) * ha), hr((double)hr(b) * ha), hr(1.0 - (double)ha)};
+    float nd = depth_h;
+    for (int i = 0; i < MLAB_LAYERS; ++i) { /* :245-259 */
+        if (nd >= k->D[i]) {
+            for (int c = 0; c < 4; ++c) {
+                float t = k->L[i][c];
+                k->L[i][c] = nl[c];
+                nl[c] = t;
+            }
+            float t = k->D[i];
+            k->D[i] = nd;
+            nd = t;
+        }
+    }
+    const int last = MLAB_LAYERS - 1; /* :261-271 merge under */
+    int closer = nd >= k->D[last];
+    const float *front = closer ? nl : k->L[last];
+    const float *back = closer ? k->L[last] : nl;
+    float m[4];
+    for (int c = 0; c < 3; ++c) m[c] = hr((double)back[c] + hr((double)front[c] * back[3]));
+    m[3] = hr((double)front[3] * back[3]);
+    for (int c = 0; c < 4; ++c) k->L[last][c] = m[c];
+    if (closer) k->D[last] = nd;
+}
+
+/* resolve_main (gaussian_splat.metal:330-361): layers front to back. */
+static void mlab_resolve(const mlab_kbuf *k, float out[4]) {
+    float C[3] = {0.0f, 0.0f, 0.0f}, at = 1.0f;
+    for (int i = 0; i < MLAB_LAYERS; ++i) {
+        for (int c = 0; c < 3; ++c) C[c] = hr((double)C[c] + hr((double)k->L[i][c] * at));
+        at = hr((double)at * k->L[i][3]);
+    }
+    out[0] = C[0]; out[1] = C[1]; out[2] = C[2];
+    out[3] = hr(1.0 - (double)at);
+}
+
 /* Composite `cnt` fragments given in S1 order (dkey asc, index asc). */
 static void composite(int mode, const float *frag_rgb_a, int cnt, float out[4]) {
     if (mode == ORA_MODE_TILE) { /* tile.metal:251-266 */
@@ -650,6 +731,16 @@ static void composite(int mode, const float *frag_rgb_a, int cnt, float out[4]) 
 }
 
 void ora_composite_list(const float *frags, int n, int mode, int cap, float out[4]) {
+    if (mode == ORA_MODE_MLAB) { /* arrival order through the k-buffer; no cap */
+        mlab_kbuf kb;
+        mlab_clear(&kb);
+        for (int k = 0; k < n; ++k) {
+            const float *f = frags + k * 5;
+            mlab_insert(&kb, f[1], f[2], f[3], f[4], hr(f[0]));
+        }
+        mlab_resolve(&kb, out);
+        return;
+    }
     int cnt = (cap > 0 && n > cap) ? cap : n; /* overflow dropped by arrival (tile.metal:202) */
     kv *ord = (kv *)malloc(sizeof(kv) * (cnt > 0 ? cnt : 1));
     for (int k = 0; k < cnt; ++k) {
@@ -753,12 +844,24 @@ static int composite_records_impl(const ora_record *rec, const uint32_t *dkey, i
             }
             /* S1 order: descending half depth == ascending dkey; ties keep
              * arrival (index) order. */
-            if (cap == 0) qsort(ord, (size_t)m, sizeof(kv), kv_cmp);
+            if (cap == 0 && mode != ORA_MODE_MLAB) qsort(ord, (size_t)m, sizeof(kv), kv_cmp);
             for (int py = ty * TILE; py < ty * TILE + TILE && py < H; ++py) {
                 int orow = compact ? slot[py / OWN_ROW] * OWN_ROW + py % OWN_ROW : py;
                 for (int px = tx * TILE; px < tx * TILE + TILE && px < W; ++px) {
                     float *o = out + ((size_t)orow * W + px) * (slab == 1 ? 1 : 4);
                     int c = 0;
+                    if (mode == ORA_MODE_MLAB) { /* arrival order, k-buffer, resolve */
+                        mlab_kbuf kb;
+                        mlab_clear(&kb);
+                        for (int64_t k = 0; k < m; ++k) {
+                            const ora_record *r = &rec[ord[k].idx];
+                            float al = frag_alpha(r, px, py);
+                            if (al < 0.0f) continue;
+                            mlab_insert(&kb, r->r, r->g, r->b, al, half_from_bits(0x7C00u - ord[k].key));
+                        }
+                        mlab_resolve(&kb, o);
+                        continue;
+                    }
                     if (slab) { /* depth slab: same walk, from the slab's start state */
                         float ts = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
                         if (slab == 2)
@@ -871,12 +974,15 @@ static int composite_records_impl(const ora_record *rec, const uint32_t *dkey, i
 int ora_composite_records(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H,
                           const ora_options *opt, const uint8_t *owner, int rank, int compact, float *out,
                           ora_stats *st) {
+    if (opt && opt->mode == ORA_MODE_MLAB && opt->cap > 0) return 0;
     return composite_records_impl(rec, dkey, n, W, H, opt, owner, rank, compact, out, st, 0, 0, NULL);
 }
 
 int ora_composite_slab(const ora_record *rec, const uint32_t *dkey, int64_t n, int W, int H, const ora_options *opt,
                        int pass, int slab_rank, const float *t_all, float *out) {
-    if ((pass != 1 && pass != 2) || (opt && opt->cap > 0) || (pass == 2 && slab_rank > 0 && !t_all)) return 0;
+    if ((pass != 1 && pass != 2) || (opt && (opt->cap > 0 || opt->mode == ORA_MODE_MLAB)) ||
+        (pass == 2 && slab_rank > 0 && !t_all))
+        return 0;
     return composite_records_impl(rec, dkey, n, W, H, opt, NULL, 0, 0, out, NULL, pass, slab_rank, t_all);
 }
 

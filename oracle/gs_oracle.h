@@ -96,7 +96,9 @@ typedef struct {
     int visible;
 } ora_debug;
 
-enum { ORA_MODE_TILE = 0, ORA_MODE_LIVE50 = 1 };
+/* MLAB = the 6-layer k-buffer of gaussian_splat.metal:201-361 (half
+ * arithmetic, arrival order, resolve front to back); no cap, no slabs. */
+enum { ORA_MODE_TILE = 0, ORA_MODE_LIVE50 = 1, ORA_MODE_MLAB = 2 };
 
 typedef struct {
     int mode;          /* ORA_MODE_TILE (default contract) or ORA_MODE_LIVE50 */

@@ -78,6 +78,9 @@ def lib() -> C.CDLL:
     return _lib
 
 
+_MODES = {"tile": 0, "live50": 1, "mlab": 2}  # ORA_MODE_*
+
+
 def _col16(m) -> np.ndarray:
     a = np.asarray(m, np.float32)
     if a.shape == (4, 4):
@@ -150,7 +153,7 @@ def project(scene, view, proj, width, height, sh_degree=0, nthreads=0):
 def render(scene, view, proj, width, height, sh_degree=0, mode="tile", cap=0, nthreads=0):
     s, keep = _scene(scene, sh_degree)
     out = np.zeros((height, width, 4), np.float32)
-    o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
+    o = OraOptions(_MODES[mode], int(cap), int(nthreads))
     st = OraStats()
     V, P = _col16(view), _col16(proj)
     lib().ora_render(C.byref(s), V.ctypes.data, P.ctypes.data, int(width), int(height), C.byref(o),
@@ -167,7 +170,7 @@ def composite_records(rec, dkey, width, height, owner=None, rank=0, compact=Fals
     own = None if owner is None else np.ascontiguousarray(owner, np.uint8)
     rows = int((own == rank).sum()) * 32 if (compact and own is not None) else height
     out = np.zeros((rows, width, 4), np.float32)
-    o = OraOptions(0 if mode == "tile" else 1, int(cap), int(nthreads))
+    o = OraOptions(_MODES[mode], int(cap), int(nthreads))
     st = OraStats()
     lib().ora_composite_records(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
                                 C.byref(o), None if own is None else own.ctypes.data, int(rank),
@@ -182,7 +185,7 @@ def composite_slab(rec, dkey, width, height, pas, rank=0, t_all=None, mode="tile
     dkey = np.ascontiguousarray(dkey, np.uint32)
     out = np.zeros((height, width) if pas == 1 else (height, width, 4), np.float32)
     ta = None if t_all is None else np.ascontiguousarray(t_all, np.float32)
-    o = OraOptions(0 if mode == "tile" else 1, 0, int(nthreads))
+    o = OraOptions(_MODES[mode], 0, int(nthreads))
     ok = lib().ora_composite_slab(rec.ctypes.data, dkey.ctypes.data, rec.shape[0], int(width), int(height),
                                   C.byref(o), int(pas), int(rank), None if ta is None else ta.ctypes.data,
                                   out.ctypes.data)
@@ -194,7 +197,7 @@ def composite_slab(rec, dkey, width, height, pas, rank=0, t_all=None, mode="tile
 def composite_list(frags, mode="tile", cap=0) -> np.ndarray:
     f = np.ascontiguousarray(frags, np.float32).reshape(-1, 5)
     out = np.zeros(4, np.float32)
-    lib().ora_composite_list(f.ctypes.data, f.shape[0], 0 if mode == "tile" else 1, int(cap), out.ctypes.data)
+    lib().ora_composite_list(f.ctypes.data, f.shape[0], _MODES[mode], int(cap), out.ctypes.data)
     return out
 
 
