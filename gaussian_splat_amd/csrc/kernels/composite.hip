@@ -146,10 +146,13 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     const float fy = (float)py + 0.5f;
 
     const uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
-    float A = 0.0f;  // tile rule: accumulated alpha
-    float T = 1.0f;  // live50 rule: transmittance
+    // Pixels outside the frame start finished (A = 1 / T = 0): for the tile and
+    // live50 rules "finished" is then just the break test on A / T itself, so
+    // no separate per-lane flag is carried through the loop.
+    float A = inside ? 0.0f : 1.0f;  // tile rule: accumulated alpha
+    float T = inside ? 1.0f : 0.0f;  // live50 rule: transmittance
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-    bool done = !inside;
+    bool done = !inside;  // MODE 2 / 3
     bool any = false;
     uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
     int cnt = 0;                 // MODE 2: covering fragments seen
@@ -165,20 +168,24 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         float ts = 1.0f;
         if (inside)
             for (int j = 0; j < a.slab_rank; ++j) ts *= a.t_all[((size_t)j * height + py) * width + px];
+        // saturated before this slab (A >= 0.99 / T < 0.01): the loop broke earlier
         if constexpr (MODE == 0) {
-            A = 1.0f - ts;
+            if (inside) A = 1.0f - ts;
             A0 = A;
-            done = done || A >= kSat;  // saturated before this slab: the loop broke earlier
         } else {
-            T = ts;
+            if (inside) T = ts;
             T0 = T;
-            done = done || T < kTMin;
         }
     }
+    auto finished = [&]() -> bool {
+        if constexpr (MODE == 0) return A >= kSat;
+        else if constexpr (MODE == 1) return T < kTMin;
+        else return done;
+    };
 
     // Composite update of one fragment (covered = box test and 0.01 cutoff).
     auto step = [&](bool covered, float alpha, float r, float g, float bl, uint32_t id) {
-        bool in = !done && covered;
+        bool in = !finished() && covered;
         if constexpr (CAP) in = in && id <= thr;
         any |= in;
         if constexpr (MODE == 0) {
@@ -188,14 +195,12 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             C1 = __builtin_fmaf(g, sa, C1);
             C2 = __builtin_fmaf(bl, sa, C2);
             A = A + sa;
-            done = done || A >= kSat;
         } else {
             const float tw = in ? T : 0.0f;
             C0 = __builtin_fmaf(r, tw, C0);
             C1 = __builtin_fmaf(g, tw, C1);
             C2 = __builtin_fmaf(bl, tw, C2);
             T = in ? T * (1.0f - alpha) : T;
-            done = done || T < kTMin;
         }
     };
 
@@ -208,7 +213,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
 #ifdef GS_COMPOSITE_COUNTERS
         {
-            const uint64_t m = __ballot(covered && !done);
+            const uint64_t m = __ballot(covered && !finished());
             if (lane == 0 && m) GS_CC(4, 1);
             if (lane == 0) GS_CC(7, __popcll(m));
         }
@@ -259,7 +264,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     if (lane == 0) GS_CC(0, 1);
     if (tid == 0) GS_CC(6, rg.y - rg.x);
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
-        if (__syncthreads_count(!done) == 0) break;
+        if (__syncthreads_count(!finished()) == 0) break;
         if (tid == 0) GS_CC(5, 1);
         if (b + tid < rg.y) {
             s0[tid] = r0;
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
         // wave-level compaction of the splats reaching this quadrant (index order kept)
         uint32_t nl = 0;
-        if (__ballot(!done) != 0) {
+        if (__ballot(!finished()) != 0) {
             for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 bool hit = false;
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         wave_lds_sync();  // wlist[wave] is only touched by this wave
         uint32_t i = 0;
         for (; i + 1 < nl; i += 2) {
-            if (__ballot(!done) == 0) break;
+            if (__ballot(!finished()) == 0) break;
             const uint32_t k0 = wlist[wave][i], k1 = wlist[wave][i + 1];
             if constexpr (MODE == 2 || MODE == 3) {
                 body(k0);
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 body_v(a1, b1, c1, i1);
             }
         }
-        if (i < nl && __ballot(!done) != 0) body(wlist[wave][i++]);
+        if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         if (lane == 0) GS_CC(3, i);
 #ifdef GS_COMPOSITE_COUNTERS
         {  // iterations a split quadrant would need: max over 8x4 halves / 4x4 quarters

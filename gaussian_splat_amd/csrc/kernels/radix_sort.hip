@@ -39,7 +39,13 @@ struct SortIO {
     uint32_t* vout[NV];
 };
 
-constexpr int ipt_for(int nv) { return nv == 1 ? 16 : 8; }
+#ifndef GS_RS_IPT1  // A/B knobs (tools/build_variant.py)
+#define GS_RS_IPT1 16
+#endif
+#ifndef GS_RS_PASS_WAVES  // min waves per SIMD of the pass kernel (HIP launch bounds)
+#define GS_RS_PASS_WAVES 1
+#endif
+constexpr int ipt_for(int nv) { return nv == 1 ? GS_RS_IPT1 : 8; }
 constexpr uint32_t tile_items(int nv) { return (uint32_t)kRsThreads * ipt_for(nv); }
 
 // Exclusive scan over the kRsThreads-lane workgroup (LDS-only barriers).
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(256) void rts_scan_kernel(uint32_t* __restrict__ C,
 // with atomicMin over tiles (order-independent, so deterministic); the
 // caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
 template <int NV>
-__global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
+__global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        int digit_bits, const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
                                                        uint2* __restrict__ ranges) {
@@ -126,7 +132,6 @@ __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n
     __shared__ uint32_t blk_start[kSortBins];     // tile-local start of each digit
     __shared__ uint32_t gbase[kSortBins];         // global start of this tile's digit run
     __shared__ uint32_t stage[TILE];
-    __shared__ uint8_t sdig[TILE];                // digit of each staged slot
     __shared__ uint32_t tmp[kRsWaves];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -182,7 +187,9 @@ __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n
     block_lds_sync();
     const uint32_t t0 = tile * TILE;
     const uint32_t cnt = n - t0 < TILE ? n - t0 : TILE;
-    // keys: stage in tile-local sorted order, remember digits, write out
+    // keys: stage in tile-local sorted order, write out; each slot's global
+    // destination (from its staged key's digit) stays in registers for the
+    // value arrays
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t idx = base + k * 64 + lane;
@@ -190,17 +197,18 @@ __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n
             const uint32_t d = (key[k] >> shift) & mask;
             pos[k] += blk_start[d] + wh[wave][d];
             stage[pos[k]] = key[k];
-            sdig[pos[k]] = (uint8_t)d;
         }
     }
     block_lds_sync();
+    uint32_t gdst[IPT];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t j = tid + k * kRsThreads;
         if (j < cnt) {
-            const uint32_t d = sdig[j];
-            const uint32_t g = gbase[d] + (j - blk_start[d]);
             const uint32_t key = stage[j];
+            const uint32_t d = (key >> shift) & mask;
+            const uint32_t g = gbase[d] + (j - blk_start[d]);
+            gdst[k] = g;
             io.kout[g] = key;
             if (ranges) {
                 // run ends of this key inside the tile (the tile's output is a
@@ -223,10 +231,7 @@ __global__ __launch_bounds__(512) void rts_pass_kernel(SortIO<NV> io, uint32_t n
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t j = tid + k * kRsThreads;
-            if (j < cnt) {
-                const uint32_t d = sdig[j];
-                io.vout[a][gbase[d] + (j - blk_start[d])] = stage[j];
-            }
+            if (j < cnt) io.vout[a][gdst[k]] = stage[j];
         }
     }
 }
