@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU baseline duration")
     ap.add_argument("--traffic", type=int, default=1, help="measure roofline.traffic with rocprofv3 PMC (N=1)")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="N=1: 2 = a frame's projection/sort overlaps the previous frame's composite")
     ap.add_argument("--scheme", default="rows", choices=["rows", "slabs"],
                     help="N>1: bin-row ownership (bit-exact, default) or depth slabs + RGBA reduce (DESIGN.md §6b)")
     return ap.parse_args()
@@ -173,7 +175,8 @@ def main():
     cam = default_camera(W, H)
     view, proj = cam.getViewMatrix(), cam.getProjectionMatrix()
     timing = 0 if args.no_stage_timing else 2  # timed frames: dispatch-packet events only
-    opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=timing)
+    opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=timing,
+                   frames_in_flight=args.frames_in_flight if world == 1 else 1)
 
     if world == 1:
         r = InstancedSplatRenderer(scene, opts)
@@ -253,7 +256,9 @@ def main():
                        "parallelism": (f"splat-shard x{world}, 32-px bin-row ownership, all_to_all + gather, {backend}"
                                        if args.scheme == "rows" else
                                        f"splat-shard x{world}, depth slabs, all_to_all + T all_gather + RGBA "
-                                       f"reduce, {backend}") if world > 1 else "single GPU",
+                                       f"reduce, {backend}") if world > 1 else
+                                      ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the "
+                                       "composite of frame k)" if args.frames_in_flight == 2 else "single GPU"),
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},

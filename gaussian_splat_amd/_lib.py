@@ -17,7 +17,8 @@ LIB_PATH = Path(os.environ.get("GSPLAT_LIB") or Path(__file__).resolve().parent 
 class GsOptions(C.Structure):
     _fields_ = [("mode", C.c_int32), ("sh_degree", C.c_int32), ("crop", C.c_int32),
                 ("crop_radius", C.c_float), ("stage_timing", C.c_int32), ("cap", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("frames_in_flight", C.c_int32),
+                ("reserved", C.c_int32 * 5)]
 
 
 class GsSceneSoa(C.Structure):
@@ -56,6 +57,7 @@ SIGNATURES = {
     "gs_set_mode": (C.c_int, [_P, C.c_int32]),
     "gs_set_cap": (C.c_int, [_P, C.c_int32]),
     "gs_set_stage_timing": (C.c_int, [_P, C.c_int32]),
+    "gs_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
     "gs_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_render_bgra8": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_last_stats": (C.c_int, [_P, C.POINTER(GsStats)]),

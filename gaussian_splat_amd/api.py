@@ -49,6 +49,7 @@ class Options:
     crop_radius: float = 5.0
     stage_timing: int = 0  # 0 off, 1 every stage (adds event gaps), 2 preprocess + composite only
     cap: int = 0  # per-pixel fragment cap by arrival order (0 = none; 32 tile shader, 50 live shader)
+    frames_in_flight: int = 1  # 2: projection/sort of a frame overlaps the previous frame's composite
 
     def to_c(self) -> GsOptions:
         o = GsOptions()
@@ -63,6 +64,9 @@ class Options:
         if int(self.cap) < 0:
             raise ValueError("cap must be >= 0")
         o.cap = int(self.cap)
+        if int(self.frames_in_flight) not in (1, 2):
+            raise ValueError("frames_in_flight must be 1 or 2")
+        o.frames_in_flight = int(self.frames_in_flight)
         return o
 
 
@@ -229,6 +233,12 @@ class InstancedSplatRenderer:
         """0 off, 1 every stage, 2 preprocess + composite via their own dispatch packets."""
         check(lib().gs_set_stage_timing(self._h, int(mode)), "gs_set_stage_timing")
         self.options.stage_timing = int(mode)
+
+    def set_frames_in_flight(self, n: int):
+        """1: every stage on the caller's stream; 2: a frame's projection/sort
+        overlaps the previous frame's composite (internal stream)."""
+        check(lib().gs_set_frames_in_flight(self._h, int(n)), "gs_set_frames_in_flight")
+        self.options.frames_in_flight = int(n)
 
     def set_cap(self, cap: int):
         """Per-pixel fragment cap by arrival order (0 = none)."""

@@ -107,13 +107,36 @@ struct gs_handle {
     std::vector<uint16_t> rows_host;    // this rank's owned bin rows
     DevBuf owner_dev, rows_dev;
     gs::CompositeArgs slab_ca{};
+    // frames_in_flight 2: projection/sort stream, and the second set of the
+    // buffers a frame's composite reads (swapped into the members above)
+    hipStream_t side = nullptr;
+    hipEvent_t sorted_ev = nullptr;        // side stream -> composite stream hand-off
+    hipEvent_t set_free[2] = {};           // last use of each buffer set on a composite stream
+    int set = 0;
+    DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr;
+    void swap_sets() {
+        std::swap(rec, alt_rec);
+        std::swap(dkey, alt_dkey);
+        std::swap(keys, alt_keys);
+        std::swap(vals, alt_vals);
+        std::swap(tkeys, alt_tkeys);
+        std::swap(tvals, alt_tvals);
+        std::swap(ranges, alt_ranges);
+        std::swap(thr, alt_thr);
+        set ^= 1;
+    }
     int64_t index_base = 0;
 
     ~gs_handle() {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
-                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev})
+                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr})
             b->release();
+        if (side) (void)hipStreamDestroy(side);
+        if (sorted_ev) (void)hipEventDestroy(sorted_ev);
+        for (auto& e : set_free)
+            if (e) (void)hipEventDestroy(e);
         if (host_total) (void)hipHostFree(host_total);
         if (host_xtotal) (void)hipHostFree(host_xtotal);
         if (events) {
@@ -146,6 +169,8 @@ gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& op
     if (opt.cap < 0) return fail(GS_ERR_INVALID_ARG, "cap must be >= 0");
     if (opt.mode != GS_MODE_TILE && opt.mode != GS_MODE_LIVE50 && opt.mode != GS_MODE_MLAB)
         return fail(GS_ERR_INVALID_ARG, "bad mode");
+    if (opt.frames_in_flight < 0 || opt.frames_in_flight > 2)
+        return fail(GS_ERR_INVALID_ARG, "frames_in_flight must be 1 or 2");
     if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
     if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
     h->opt = opt;
@@ -389,7 +414,16 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 // bin lists (counted in the depth-sort stage time).
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
-                             int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr) {
+                             int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr,
+                             hipStream_t sc = nullptr) {
+    // the composite runs on sc (frames_in_flight 2: the caller's stream, while
+    // st is the handle's side stream) once the lists are ready on st
+    if (!sc) sc = st;
+    auto handoff = [&]() -> hipError_t {
+        if (sc == st) return hipSuccess;
+        hipError_t e = hipEventRecord(h->sorted_ev, st);
+        return e != hipSuccess ? e : hipStreamWaitEvent(sc, h->sorted_ev, 0);
+    };
     Ownership own;
     gs_status so = frame_ownership(h, U.tiles_y, st, &own);
     if (so != GS_OK) return so;
@@ -425,8 +459,9 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         if (s != GS_OK) return s;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
-        GS_HIP(gs::launch_composite(ca, h->opt.mode, st, kernel_event(h, 2), kernel_event(h, 3)));
-        mark(h, 7, st);
+        GS_HIP(handoff());
+        GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
+        mark(h, 7, sc);
         h->stats.pairs = (int64_t)P;
         return GS_OK;
     }
@@ -462,12 +497,13 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.slab = 1;
         ca.t_out = slab_t;
     }
-    GS_HIP(gs::launch_composite(ca, h->opt.mode, st, kernel_event(h, 2), kernel_event(h, 3)));
+    GS_HIP(handoff());
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
     if (slab_t) {
         h->slab_ca = ca;
         h->slab_lists = true;
     }
-    mark(h, 7, st);
+    mark(h, 7, sc);
     h->stats.pairs = (int64_t)P;
     return GS_OK;
 }
@@ -529,6 +565,7 @@ void gs_default_options(gs_options* o) {
     o->crop = 1;
     o->crop_radius = 5.0f;
     o->stage_timing = 0;
+    o->frames_in_flight = 1;
 }
 
 gs_status gs_create_from_soa(const gs_scene_soa* scene, const gs_options* opt, gs_handle** out) {
@@ -627,6 +664,9 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
         GS_HIP(h->sh1.reserve(n * 4));
         GS_HIP(hipMemcpy(h->sh1.ptr, tail.data(), n * 4, hipMemcpyHostToDevice));
     }
+    GS_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    GS_HIP(hipEventCreateWithFlags(&h->sorted_ev, hipEventDisableTiming));
+    for (auto& e : h->set_free) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->initialized = true;
     return GS_OK;
 }
@@ -651,6 +691,12 @@ gs_status gs_set_stage_timing(gs_handle* h, int32_t mode) {
     h->opt.stage_timing = mode;
     h->kev_frames = 0;
     h->kev_pending = false;
+    return GS_OK;
+}
+
+gs_status gs_set_frames_in_flight(gs_handle* h, int32_t n) {
+    if (!h || n < 1 || n > 2) return fail(GS_ERR_INVALID_ARG, "frames_in_flight must be 1 or 2");
+    h->opt.frames_in_flight = n;
     return GS_OK;
 }
 
@@ -681,16 +727,26 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     }
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = false;
-    begin_frame(h, st);
+    // frames_in_flight 2: projection .. binning on the side stream, into the
+    // other buffer set, once the composite that last read that set is done
+    const bool pipe = h->opt.frames_in_flight >= 2 && out_is_device && h->opt.stage_timing != 1;
+    hipStream_t sp = pipe ? h->side : st;
+    if (pipe) {
+        h->swap_sets();
+        if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    }
+    GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
+    begin_frame(h, sp);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
                                  kernel_event(h, 1)));
-    mark(h, 1, st);
+    mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
-                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, st)) != GS_OK)
+                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, st)) != GS_OK)
         return s;
+    GS_HIP(hipEventRecord(h->set_free[h->set], st));  // this set's last reader
     const uint64_t P = (uint64_t)h->stats.pairs;
     if (!out_is_device) {
         GS_HIP(hipMemcpyAsync(out_user, out, bytes, hipMemcpyDeviceToHost, st));
@@ -747,6 +803,7 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
     hipStream_t st = nullptr;
+    GS_HIP(hipEventSynchronize(h->set_free[h->set]));  // a pipelined composite may still read the set
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st));
     GS_HIP(hipStreamSynchronize(st));
@@ -846,6 +903,7 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
         return fail(GS_ERR_UNSUPPORTED, "multi-GPU frames are limited to 4096 x 4096 (packed exchange record)");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     *U = make_uniforms(view, proj, W, H);
+    GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));  // a pipelined composite may still read the set
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = true;
     h->slab_lists = false;
@@ -917,6 +975,7 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     // exchange between them falls inside the depth-sort interval
     fill_stats(h, (uint64_t)h->stats.pairs, U);
     h->stats.tiles = T;
+    GS_HIP(hipEventRecord(h->set_free[h->set], st));
     return GS_OK;
 }
 
@@ -1019,6 +1078,7 @@ gs_status gs_slab_composite(gs_handle* h, const float* t_all, float* out_rgba, v
     ca.t_out = nullptr;
     ca.out = reinterpret_cast<float4*>(out_rgba);
     GS_HIP(gs::launch_composite(ca, h->opt.mode, static_cast<hipStream_t>(stream)));
+    GS_HIP(hipEventRecord(h->set_free[h->set], static_cast<hipStream_t>(stream)));
     return GS_OK;
 }
 

@@ -64,7 +64,13 @@ typedef struct gs_options {
                               the preprocess and composite dispatches only (no gaps) */
     int32_t cap;           /* per-pixel fragment cap by arrival order, 0 = none (contract default);
                               32 = gaussian_splat_tile.metal:7, 50 = gaussian_splat_50layer.metal:8 */
-    int32_t reserved[6];
+    int32_t frames_in_flight; /* 1 (default): a gs_render runs entirely on the caller's stream.
+                              2: projection, sorting and binning of a frame run on an internal
+                              stream of the handle and overlap the previous frame's composite
+                              (double-buffered scratch); the composite, and so the output, stays
+                              on the caller's stream in call order.  Device outputs only;
+                              stage_timing 1 renders with 1. */
+    int32_t reserved[5];
 } gs_options;
 
 /* Scene as SoA host arrays (all float32, n splats).  Used by
@@ -119,6 +125,8 @@ gs_status gs_set_mode(gs_handle *h, int32_t mode);
 gs_status gs_set_cap(gs_handle *h, int32_t cap);
 /* Switch gs_options.stage_timing (0, 1 or 2) on a live handle. */
 gs_status gs_set_stage_timing(gs_handle *h, int32_t mode);
+/* Switch gs_options.frames_in_flight (1 or 2) on a live handle. */
+gs_status gs_set_frames_in_flight(gs_handle *h, int32_t n);
 
 /* ---- frame (InstancedSplatRenderer::render) --------------------------- */
 /* out_rgba: width*height*4 float32, row-major, y down.  out_is_device = 1:

@@ -231,6 +231,38 @@ def test_stage_timing_modes(built):
                                                    "composite"))
 
 
+def test_frames_in_flight_bitexact(built):
+    """frames_in_flight 2: a frame's projection/sort runs on the handle's side
+    stream while the previous frame composites; every output equals the
+    single-stream render, across camera changes, both output formats and an
+    interleaved gs_project_host (which must wait for the pipelined composite)."""
+    import torch
+    W, H = 640, 360
+    sc = _scene(80000, seed=71, sh=2, aspect=W / H)
+    views = orbit_views(W, H, 3)
+    r1 = _renderer(sc, sh=2)
+    refs = [r1.render_host(V, P, W, H) for V, P in views]
+    r2 = _renderer(sc, sh=2)
+    r2.set_frames_in_flight(2)
+    outs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in range(7)]
+    seq = [0, 1, 2, 2, 0, 1, 0]
+    for k, v in enumerate(seq):
+        r2.render(*views[v], W, H, out=outs[k])
+        if k == 3:
+            rec, dk, nt = r2.project_host(*views[1], W, H)
+    bg = r2.render_bgra8(*views[2], W, H)
+    torch.cuda.synchronize()
+    for k, v in enumerate(seq):
+        assert _compare(outs[k].cpu().numpy(), refs[v]) == (0.0, 0), k
+    from oracle import oracle_py as O
+    np.testing.assert_array_equal(bg.cpu().numpy(), O.to_bgra8(refs[2]))
+    rec1, dk1, nt1 = r1.project_host(*views[1], W, H)
+    vis = nt1 > 0  # records of culled splats are not written (undefined)
+    np.testing.assert_array_equal(nt, nt1)
+    np.testing.assert_array_equal(dk, dk1)
+    np.testing.assert_array_equal(rec[vis].view(np.uint8), rec1[vis].view(np.uint8))
+
+
 def test_render_device_out_matches_host(built):
     import torch
     sc = _scene(30000, 5, 0, aspect=4 / 3)
