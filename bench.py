@@ -218,6 +218,9 @@ def main():
     value = total_splats / (ms * 1e-3) / 1e6
 
     s0 = rh.last_stats()
+    # the order the timed frames built their bin lists in (the default picks
+    # it per frame from the previous frame's pair count)
+    binning = {1: "depth-first", 2: "bin-first"}.get(int(s0.get("binning", 0)), "?")
     timed = {}
     if timing == 2:  # kernel times of the timed frames (last <= 64)
         pre, comp = rh.kernel_times(args.steps)
@@ -259,13 +262,16 @@ def main():
                                        f"reduce, {backend}") if world > 1 else
                                       ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the "
                                        "composite of frame k)" if args.frames_in_flight == 2 else "single GPU"),
-                       "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
+                       "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning},
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
             "timed_kernel_ms": {k: round(v, 4) for k, v in timed.items()},
         }
         if world == 1 and rl is not None and args.traffic:
-            traffic, why = pmc_traffic(args, STAGE_KERNEL[rl["kernel"]])
+            kern = STAGE_KERNEL[rl["kernel"]]
+            if rl["kernel"] == "depth_sort" and binning == "bin-first":
+                kern = "bin_depth_sort_kernel"
+            traffic, why = pmc_traffic(args, kern)
             rl["traffic"] = round(traffic) if traffic is not None else None
             if why:
                 rl["traffic_note"] = why

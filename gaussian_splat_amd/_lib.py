@@ -18,7 +18,8 @@ class GsOptions(C.Structure):
     _fields_ = [("mode", C.c_int32), ("sh_degree", C.c_int32), ("crop", C.c_int32),
                 ("crop_radius", C.c_float), ("stage_timing", C.c_int32), ("cap", C.c_int32),
                 ("frames_in_flight", C.c_int32),
-                ("reserved", C.c_int32 * 5)]
+                ("binning", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class GsSceneSoa(C.Structure):
@@ -34,7 +35,8 @@ class GsStats(C.Structure):
                 ("ms_total", C.c_float),
                 ("bytes_preprocess", C.c_int64), ("bytes_scan", C.c_int64), ("bytes_duplicate", C.c_int64),
                 ("bytes_sort", C.c_int64), ("bytes_ranges", C.c_int64), ("bytes_composite", C.c_int64),
-                ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64)]
+                ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
+                ("binning", C.c_int32), ("reserved_stats", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

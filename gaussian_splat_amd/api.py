@@ -27,6 +27,7 @@ RECORD_DTYPE = np.dtype([("cx", "<f4"), ("cy", "<f4"), ("ax", "<f4"), ("ay", "<f
                          ("by", "<f4"), ("opacity", "<f4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4"),
                          ("rect_lo", "<u4"), ("rect_hi", "<u4")])
 MODES = {"tile": 0, "live50": 1, "mlab": 2}
+BINNING = {"default": 0, "depth_first": 1, "bin_first": 2}  # gs_binning
 
 
 def _mat16(m) -> C.Array:
@@ -50,6 +51,7 @@ class Options:
     stage_timing: int = 0  # 0 off, 1 every stage (adds event gaps), 2 preprocess + composite only
     cap: int = 0  # per-pixel fragment cap by arrival order (0 = none; 32 tile shader, 50 live shader)
     frames_in_flight: int = 1  # 2: projection/sort of a frame overlaps the previous frame's composite
+    binning: str = "default"  # bin-list build order: "default" (= bin-first), "depth_first", "bin_first"
 
     def to_c(self) -> GsOptions:
         o = GsOptions()
@@ -67,6 +69,9 @@ class Options:
         if int(self.frames_in_flight) not in (1, 2):
             raise ValueError("frames_in_flight must be 1 or 2")
         o.frames_in_flight = int(self.frames_in_flight)
+        if self.binning not in BINNING:
+            raise ValueError(f"binning must be one of {list(BINNING)}")
+        o.binning = BINNING[self.binning]
         return o
 
 

@@ -99,6 +99,18 @@ struct gs_handle {
     bool events = false;
     uint32_t* last_keys = nullptr;  // sorted pair arrays of the last frame
     uint32_t* last_vals = nullptr;
+    uint32_t* last_tmp_keys = nullptr;  // the bin sort's other buffers (free once it is done)
+    uint32_t* last_tmp_vals = nullptr;
+    int last_key_bits = 0;              // bin id bits of the pair keys (depth key above, bin-first)
+    bool bin_first_frame = false;       // the last frame used the bin-first order
+    DevBuf seg_sample;                  // per-bin depth sort sample (launch_bin_depth_sort)
+    struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
+        int32_t w = 0, h = 0;
+        int64_t n = -1;
+        uint64_t frame_pairs = 0;       // P of the last scanned frame
+        uint64_t sample_pairs = 0;      // P of the last bin-first frame (the sample's frame)
+        double long_share = 0.0;        // share of its pairs in lists longer than kSegLdsMax
+    } order;
     gs_stats stats{};
     // multi-GPU shard config
     int32_t rank = 0, world = 1;
@@ -131,7 +143,7 @@ struct gs_handle {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
-                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr})
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -171,6 +183,7 @@ gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& op
         return fail(GS_ERR_INVALID_ARG, "bad mode");
     if (opt.frames_in_flight < 0 || opt.frames_in_flight > 2)
         return fail(GS_ERR_INVALID_ARG, "frames_in_flight must be 1 or 2");
+    if (opt.binning < 0 || opt.binning > 2) return fail(GS_ERR_INVALID_ARG, "binning must be 0, 1 or 2");
     if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
     if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
     h->opt = opt;
@@ -250,6 +263,42 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
     return b;
 }
 
+// Binning order of a frame (gs_options.binning).  Both orders
+// build the same lists; the default picks the cheaper one with a cost model
+// measured on MI355X (bench config and the 4K scale runs):
+//   depth-first: global depth sort, ~25 ps per splat (2 passes over N);
+//   bin-first:   per-bin depth sort, ~6 ps per pair in lists that fit LDS,
+//                ~20 ps per pair in longer lists, ~4.9 ns per bin
+// (6M splats: 1080p 85 vs 150 us -> bin-first; 4K 176 vs 150 us and
+// 50M @ 4K 3.7 vs 1.2 ms -> depth-first).
+// P (scaled by the item count: multi-GPU frames receive a varying number of
+// records) and the long-list share come from the previous frames at the same
+// resolution; with no history the frame goes depth-first.
+// Bin-first needs the depth key to fit above the bin id in a 32-bit pair key.
+// GS_BINNING=depth|bin overrides the option (A/B timing).
+bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
+    static const char* env = std::getenv("GS_BINNING");
+    int b = h->opt.binning;
+    if (env && std::strcmp(env, "depth") == 0) b = GS_BINNING_DEPTH_FIRST;
+    if (env && std::strcmp(env, "bin") == 0) b = GS_BINNING_BIN_FIRST;
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    if (b == GS_BINNING_DEPTH_FIRST || bits_for(T) + gs::kDepthBits > 32) return false;
+    if (b == GS_BINNING_BIN_FIRST) return true;
+    auto& o = h->order;
+    if (o.w != U.width || o.h != U.height) {  // new history
+        o = gs_handle::OrderModel{};
+        o.w = U.width;
+        o.h = U.height;
+    }
+    const bool known = o.frame_pairs > 0 && o.n > 0;
+    const double P = known ? (double)o.frame_pairs * (double)m / (double)o.n : 0.0;  // pairs scale with items
+    o.n = (int64_t)m;  // items of this frame (the scan that follows reads its P)
+    if (!known) return false;
+    const double f = o.long_share;
+    const double bin_ps = 6.0 * P * (1.0 - f) + 20.0 * P * f + 4900.0 * T;
+    return bin_ps < 25.0 * (double)m;
+}
+
 gs_status check_ready(gs_handle* h) {
     if (!h) return fail(GS_ERR_INVALID_ARG, "null handle");
     if (!h->initialized) return fail(GS_ERR_STATE, "gs_initialize not called");
@@ -265,8 +314,12 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->rhi.reserve(n * 4));
     GS_HIP(h->offsets.reserve(n * 4));
     GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
-    GS_HIP(h->total.reserve(16));
-    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 16, hipHostMallocDefault));
+    GS_HIP(h->total.reserve(32));
+    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 32, hipHostMallocDefault));
+    if (!h->seg_sample.ptr) {
+        GS_HIP(h->seg_sample.reserve(8));
+        GS_HIP(hipMemset(h->seg_sample.ptr, 0, 8));
+    }
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
         for (auto& slot : h->kev)
@@ -366,15 +419,21 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
 // ranges.  Marks 3..6 when `timed`.
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
-                          hipStream_t st, const uint32_t** vals_out, uint64_t* pairs) {
+                          hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
+                          const uint32_t* carry_dkey = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->offsets.as<uint32_t>(),
-                                      h->partials.as<uint64_t>(), h->total.as<uint64_t>(), st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 16, hipMemcpyDeviceToHost, st));
+                                      h->partials.as<uint64_t>(), h->total.as<uint64_t>(),
+                                      h->seg_sample.as<uint32_t>(), st));
+    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 32, hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));
     if (timed) mark(h, 3, st);
     const uint64_t P = h->host_total[0];
     h->stats.visible = (int64_t)h->host_total[1];
+    // the last per-bin depth sort's share of pairs in lists too long for LDS
+    if ((h->host_total[3] & gs::kSegSampleValid) && h->order.sample_pairs)
+        h->order.long_share = (double)h->host_total[2] / (double)h->order.sample_pairs;
+    h->order.frame_pairs = P;
     if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
     const size_t p = (size_t)std::max<uint64_t>(P, 1);
     GS_HIP(h->keys.reserve(p * 4));
@@ -383,13 +442,13 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->tvals.reserve(p * 4));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
-    // pairs (bin, splat) in visiting order
+    // pairs (bin, splat) in visiting order (bin-first: the depth key above the bin id)
+    const int bits = bits_for(T);
     GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, own.dev,
-                                U.cell_mask != 0,
+                                U.cell_mask != 0, carry_dkey, bits,
                                 h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
     if (timed) mark(h, 4, st);
     // stable sort by bin id only; the last pass also writes the bin ranges
-    const int bits = bits_for(T);
     bool in_tmp = false;
     GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), st));
     GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
@@ -399,8 +458,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
     h->last_keys = sk;
     h->last_vals = sv;
+    h->last_tmp_keys = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
+    h->last_tmp_vals = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+    h->last_key_bits = bits;
     if (timed) mark(h, 5, st);
-    if (timed) mark(h, 6, st);  // (ranges come out of the last sort pass)
+    if (timed && !carry_dkey) mark(h, 6, st);  // (ranges come out of the last sort pass)
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
     *vals_out = sv;
@@ -465,6 +527,43 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         h->stats.pairs = (int64_t)P;
         return GS_OK;
     }
+    if (!mlab && bin_first_order(h, U, m)) {
+        // Bin-first: bin lists in arrival (index) order with
+        // the depth key carried in the pair keys, then each list stably
+        // sorted by depth key -> (depth, index) order, the same lists as the
+        // depth-first order below.
+        h->bin_first_frame = true;
+        mark(h, 2, st);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey);
+        if (s != GS_OK) return s;
+        h->order.sample_pairs = P;
+        ca.vals = vals;
+        ca.ranges = h->ranges.as<uint2>();
+        if (ca.cap > 0) {  // per-pixel cap thresholds from the lists in arrival order
+            GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
+            ca.thr_out = h->thr.as<uint32_t>();
+            GS_HIP(gs::launch_cap_threshold(ca, st));
+            ca.thr = h->thr.as<uint32_t>();
+        }
+        GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
+                                         h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
+                                         h->seg_sample.as<uint32_t>(), st));
+        mark(h, 6, st);
+        if (slab_t) {
+            ca.slab = 1;
+            ca.t_out = slab_t;
+        }
+        GS_HIP(handoff());
+        GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
+        if (slab_t) {
+            h->slab_ca = ca;
+            h->slab_lists = true;
+        }
+        mark(h, 7, sc);
+        h->stats.pairs = (int64_t)P;
+        return GS_OK;
+    }
+    h->bin_first_frame = false;
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
@@ -526,6 +625,13 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_depth_sort = dpass > 0 ? N * (4 * dpass + 28 + 32 * (dpass - 1)) : 0;
     s.bytes_scan = N * 20;
     s.bytes_duplicate = N * 20 + Pi * 8;
+    s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
+    if (h->bin_first_frame) {
+        // per-bin depth sort: keys read, vals gathered and written back (12 B
+        // per pair); the duplicate also reads the depth keys (4 B per splat)
+        s.bytes_depth_sort = Pi * 12;
+        s.bytes_duplicate += N * 4;
+    }
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
     s.bytes_ranges = T * 8;  // the fill only: ranges come out of the last sort pass
     s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
@@ -544,6 +650,10 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         s.ms_duplicate = elapsed(h, 3, 4);
         s.ms_sort = elapsed(h, 4, 5);
         s.ms_ranges = elapsed(h, 5, 6);
+        if (h->bin_first_frame) {  // the per-bin depth sort runs between marks 5 and 6
+            s.ms_depth_sort = s.ms_ranges;
+            s.ms_ranges = 0.0f;
+        }
         s.ms_composite = elapsed(h, 6, 7);
         s.ms_total = elapsed(h, 0, 7);
     }
@@ -841,7 +951,12 @@ gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int
     int64_t m = std::min(P, cap);
     GS_HIP(hipSetDevice(h->device));
     GS_HIP(hipDeviceSynchronize());
-    if (keys) GS_HIP(hipMemcpy(keys, h->last_keys, (size_t)m * 4, hipMemcpyDeviceToHost));
+    if (keys) {
+        GS_HIP(hipMemcpy(keys, h->last_keys, (size_t)m * 4, hipMemcpyDeviceToHost));
+        // bin-first pair keys carry the depth key above the bin id
+        const uint32_t mask = h->last_key_bits >= 32 ? 0xFFFFFFFFu : (1u << h->last_key_bits) - 1u;
+        for (int64_t i = 0; i < m; ++i) keys[i] &= mask;
+    }
     if (vals) GS_HIP(hipMemcpy(vals, h->last_vals, (size_t)m * 4, hipMemcpyDeviceToHost));
     return GS_OK;
 }

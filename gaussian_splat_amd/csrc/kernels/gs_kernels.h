@@ -22,19 +22,39 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
 constexpr int kScanItems = 4096;  // per block
 // Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], own) into
 // offsets[n]; total[0] (device u64) = sum, total[1] = items with a nonzero
-// count.  partials: 2 * ceil(n / kScanItems) u64.
+// count, total[2..3] = the per-bin depth sort sample (seg_sample, 2 words,
+// may be null; reset), see launch_bin_depth_sort.  partials: 2 *
+// ceil(n / kScanItems) u64.
 hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                   bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                  hipStream_t st);
+                                  uint32_t* seg_sample, hipStream_t st);
 
 // ---- binning.hip -----------------------------------------------------------
 // Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
 // rect_hi[j]) emits (bin, order[j]) for each bin of its rect whose row is
 // owned by this rank, starting at offsets[j].  order == nullptr
-// means the identity (pairs in index order).
+// means the identity (pairs in index order).  dkey (index order only, may be
+// null): key = dkey[j] << bin_bits | bin, the depth key riding above the bin
+// id for the per-bin depth sort.
 hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                             const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                            uint32_t* keys, uint32_t* vals, hipStream_t st);
+                            const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st);
+
+// ---- bin_depth_sort.hip ------------------------------------------------------
+// Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
+// pairs, key = dkey << bin_bits | b: stable sort of the list by dkey
+// (ties keep list order).  vals are permuted in place; keys of lists longer
+// than kSegLdsMax are permuted too (they go through tmp_keys / tmp_vals, at
+// the same offsets), shorter ones keep their keys unsorted.  Afterwards each
+// bin's vals are in (dkey, list position) order.
+// sample (2 words, zeroed by the next scan): [0] += pairs of the lists longer
+// than kSegLdsMax (sorted through global memory, ~3x the cost per pair),
+// [1] |= kSegSampleValid once the sort ran.
+constexpr uint32_t kSegLdsMax = 8192;  // = the kernel's NT * IPT (bin_depth_sort.hip)
+constexpr uint32_t kSegSampleValid = 0x80000000u;
+hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
+                                 uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
+                                 hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
 constexpr int kSortTile = 8192;  // items per sort tile (512 lanes x 16)

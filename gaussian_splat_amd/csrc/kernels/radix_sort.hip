@@ -116,15 +116,17 @@ __global__ __launch_bounds__(256) void rts_scan_kernel(uint32_t* __restrict__ C,
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-// ranges (last pass only, may be null): per key value k, the global extent
-// [x, ~y) of k's run in the sorted output, stored as {x, ~end} and merged
-// with atomicMin over tiles (order-independent, so deterministic); the
-// caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
+// ranges (last pass only, may be null): per key value k = key & rmask, the
+// global extent [x, ~y) of k's run in the sorted output, stored as {x, ~end}
+// and merged with atomicMin over tiles (order-independent, so deterministic);
+// the caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
+// Bits above rmask ride along unsorted (the bin-first binning carries each
+// pair's depth key there, bin_depth_sort.hip).
 template <int NV>
 __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        int digit_bits, const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
-                                                       uint2* __restrict__ ranges) {
+                                                       uint2* __restrict__ ranges, uint32_t rmask) {
     constexpr int IPT = ipt_for(NV);
     constexpr uint32_t TILE = tile_items(NV);
     constexpr uint32_t WAVE_ITEMS = 64u * IPT;
@@ -213,8 +215,9 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
             if (ranges) {
                 // run ends of this key inside the tile (the tile's output is a
                 // contiguous, fully sorted slice of the final order per digit)
-                if (j == 0 || stage[j - 1] != key) atomicMin(&ranges[key].x, g);
-                if (j + 1 == cnt || stage[j + 1] != key) atomicMin(&ranges[key].y, ~(g + 1u));
+                const uint32_t rk = key & rmask;
+                if (j == 0 || (stage[j - 1] & rmask) != rk) atomicMin(&ranges[rk].x, g);
+                if (j + 1 == cnt || (stage[j + 1] & rmask) != rk) atomicMin(&ranges[rk].y, ~(g + 1u));
             }
         }
     }
@@ -284,7 +287,8 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles);
         rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
         rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
-                                                          totals, tiles, p + 1 == plan.passes ? ranges : nullptr);
+                                                          totals, tiles, p + 1 == plan.passes ? ranges : nullptr,
+                                                          bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u);
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;

@@ -43,8 +43,18 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
 }
 
 // One workgroup scans all partials (<= a few thousand) exclusively in place.
+// seg_sample (may be null): the per-bin depth sort's sample since the last
+// scan (bin_depth_sort.hip) is moved into total[2..3] and reset, so it comes
+// back to the host with the pair count.
 __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
-                                                            uint64_t* __restrict__ total) {
+                                                            uint64_t* __restrict__ total,
+                                                            uint32_t* __restrict__ seg_sample) {
+    if (seg_sample && threadIdx.x == 0) {
+        total[2] = seg_sample[0];
+        total[3] = seg_sample[1];
+        seg_sample[0] = 0u;
+        seg_sample[1] = 0u;
+    }
     __shared__ uint64_t tmp[4];
     uint64_t carry = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
@@ -107,14 +117,14 @@ __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n
 
 hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                   bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                  hipStream_t st) {
+                                  uint32_t* seg_sample, hipStream_t st) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
-        return hipMemsetAsync(total, 0, 2 * sizeof(uint64_t), st);
+        return hipMemsetAsync(total, 0, 4 * sizeof(uint64_t), st);
     }
     scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials);
-    scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total);
+    scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample);
     scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
     return hipGetLastError();
 }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 2
+#define GSPLAT_ABI_VERSION 3
 
 typedef enum {
     GS_OK = 0,
@@ -53,6 +53,7 @@ typedef enum {
  * 6-layer k-buffer of gaussian_splat.metal:201-361 (arrival order, half
  * arithmetic, resolve output before the drawable blend; no cap, no slabs). */
 typedef enum { GS_MODE_TILE = 0, GS_MODE_LIVE50 = 1, GS_MODE_MLAB = 2 } gs_mode;
+typedef enum { GS_BINNING_DEFAULT = 0, GS_BINNING_DEPTH_FIRST = 1, GS_BINNING_BIN_FIRST = 2 } gs_binning;
 
 typedef struct gs_options {
     int32_t mode;          /* gs_mode */
@@ -70,7 +71,11 @@ typedef struct gs_options {
                               (double-buffered scratch); the composite, and so the output, stays
                               on the caller's stream in call order.  Device outputs only;
                               stage_timing 1 renders with 1. */
-    int32_t reserved[5];
+    int32_t binning;       /* order in which the bin lists are built (same lists, same image):
+                              0 = default (bin-first), 1 = depth-first (global depth sort of the
+                              splats, then binning), 2 = bin-first (bin lists in arrival order,
+                              then a stable per-bin depth sort).  DESIGN.md §1 */
+    int32_t reserved[4];
 } gs_options;
 
 /* Scene as SoA host arrays (all float32, n splats).  Used by
@@ -101,6 +106,10 @@ typedef struct gs_stats {
     float ms_depth_sort;   /* splats by depth key (ms_sort = pairs by tile) */
     float ms_exchange;     /* multi-GPU: destination count + pack + exchange (between the shard calls) */
     int64_t bytes_depth_sort;
+    int32_t binning;       /* order the last frame's bin lists were built in: GS_BINNING_DEPTH_FIRST
+                              (ms_depth_sort = global depth sort) or GS_BINNING_BIN_FIRST
+                              (ms_depth_sort = per-bin depth sort after the bin sort) */
+    int32_t reserved_stats;
 } gs_stats;
 
 typedef struct gs_handle gs_handle;

@@ -306,6 +306,53 @@ def test_sorted_pairs_match_stable_sort(built, n, huge):
     np.testing.assert_array_equal(vals, ev[order])
 
 
+@pytest.mark.parametrize("n,w,h,mode,cap,wall,zr", [
+    (40000, 64, 64, "tile", 0, 0, (1, 9)),       # 8193..16384 pairs per bin (12-bit key span: 6+6)
+    (100000, 64, 64, "tile", 0, 0, (1, 9)),      # > 16384: global-memory path
+    (100000, 64, 64, "live50", 32, 0, (1, 9)),
+    (30000, 512, 384, "tile", 0, 0, (1, 9)),     # <= 8192
+    (30000, 512, 384, "tile", 0, 0, (4, 4.2)),   # key span < 256: one pass
+    (30000, 512, 384, "live50", 0, 0, (0.3, 9)), # 13-bit span: 8+7
+    (30000, 512, 384, "tile", 0, 1, (1, 9)),     # half the splats at one depth
+    (12000, 64, 64, "tile", 0, 2, (1, 9))])      # all at one depth (span 0 or 1)
+def test_bin_first_equals_depth_first(built, n, w, h, mode, cap, wall, zr):
+    """Bin-first order (bin lists in arrival order, then a stable per-bin
+    depth sort, bin_depth_sort.hip) builds exactly the depth-first order's
+    bin lists and image in every list size class and every key-span path,
+    and matches the oracle."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd import scene as S
+    from oracle import oracle_py as O
+    sc = S.activate(S.synthetic_raw(n, seed=21, aspect=w / h, zrange=zr), 0)
+    V, P = orbit_views(w, h, 1)[0]
+    if wall:  # splats on a plane at view depth 5 (one or two half-depth keys)
+        rng = np.random.default_rng(5)
+        eye, fwd = np.array([0.0, 2.0, 5.0]), -np.array([0.0, 2.0, 5.0]) / np.sqrt(29.0)
+        right = np.cross(fwd, [0.0, -1.0, 0.0]); right /= np.linalg.norm(right)
+        up = np.cross(right, fwd)
+        k = n // 2 if wall == 1 else n
+        a, b = rng.uniform(-1.5, 1.5, (2, k))
+        sc.pos[:k] = (eye + 5.0 * fwd + a[:, None] * right + b[:, None] * up).astype(np.float32)
+    out = {}
+    for b in ("depth_first", "bin_first"):
+        r = InstancedSplatRenderer(sc, Options(mode=mode, cap=cap, binning=b))
+        r.initialize(0)
+        img = r.render_host(V, P, w, h)
+        keys, vals = r.sorted_pairs()
+        out[b] = (img, keys, vals, r.last_stats()["pairs"])
+    img0, k0, v0, p0 = out["depth_first"]
+    img1, k1, v1, p1 = out["bin_first"]
+    assert p0 == p1
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(v1, v0)
+    assert _compare(img1, img0) == (0.0, 0)
+    per_bin = np.bincount(k0, minlength=((w + 31) // 32) * ((h + 31) // 32))
+    assert per_bin.max() > (16384 if n == 100000 else 8192 if n == 40000 else 0)
+    ref, _ = O.render(sc, V, P, w, h, mode=mode, cap=cap)
+    linf, nbit = _compare(img1, ref)
+    assert linf <= TOL and nbit == 0, (linf, nbit)
+
+
 @pytest.mark.parametrize("n,bits", [(0, 8), (1, 8), (4095, 13), (4096, 16), (4097, 20), (100000, 28),
                                     (1 << 20, 32), (3_000_001, 30)])
 def test_radix_sort(built, n, bits):
