@@ -99,8 +99,8 @@ def cpu_baseline(scene, view, proj, w, h, sh, sample, seconds):
                       f"(oracle/gs_oracle.c, OpenMP, {threads} threads), {dt:.1f} s"}
 
 
-STAGE_KERNEL = {"preprocess": "preprocess_kernel", "depth_sort": "rts_pass_kernel<3>", "scan": "scan_down_kernel",
-                "duplicate": "duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "rts_pass_kernel<1>",
+STAGE_KERNEL = {"preprocess": "preprocess_kernel", "depth_sort": "rts_pass_kernel<3>", "scan": "scan_reduce_kernel",
+                "duplicate": "scan_duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "rts_pass_kernel<1>",
                 "composite": "composite_kernel"}
 
 

@@ -77,7 +77,7 @@ struct gs_handle {
     bool initialized = false;
     DevBuf p0, p1, p2, p3, sh4, sh1;
     // per-frame scratch
-    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
+    DevBuf rec, dkey, rlo, rhi, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     // depth-slab frames: full-frame ownership; the colour pass
@@ -140,7 +140,7 @@ struct gs_handle {
     int64_t index_base = 0;
 
     ~gs_handle() {
-        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
+        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &partials, &total, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample})
@@ -312,7 +312,6 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->dkey.reserve(n * 4));
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
-    GS_HIP(h->offsets.reserve(n * 4));
     GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
     GS_HIP(h->total.reserve(32));
     if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 32, hipHostMallocDefault));
@@ -414,17 +413,16 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
 }
 
 // Bin lists from m splats visited in `order` (nullptr = index order) with
-// rects (rect_lo, rect_hi) in that order: ordered scan of bin counts (P and
-// the visible count to host) -> duplicate -> stable sort by bin id ->
-// ranges.  Marks 3..6 when `timed`.
+// rects (rect_lo, rect_hi) in that order: per-block pair totals and their
+// scan (P and the visible count to host) -> down-sweep fused with the
+// duplicate -> stable sort by bin id -> ranges.  Marks 3..6 when `timed`.
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
                           const uint32_t* carry_dkey = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    GS_HIP(gs::launch_tile_count_scan(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->offsets.as<uint32_t>(),
-                                      h->partials.as<uint64_t>(), h->total.as<uint64_t>(),
-                                      h->seg_sample.as<uint32_t>(), st));
+    GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
+                                        h->total.as<uint64_t>(), h->seg_sample.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 32, hipMemcpyDeviceToHost, st));
     GS_HIP(hipStreamSynchronize(st));
     if (timed) mark(h, 3, st);
@@ -444,9 +442,9 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the bin id)
     const int bits = bits_for(T);
-    GS_HIP(gs::launch_duplicate(order, rect_lo, rect_hi, h->offsets.as<uint32_t>(), m, (uint32_t)U.tiles_x, own.dev,
-                                U.cell_mask != 0, carry_dkey, bits,
-                                h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), st));
+    GS_HIP(gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m, (uint32_t)U.tiles_x,
+                                     own.dev, U.cell_mask != 0, carry_dkey, bits, h->keys.as<uint32_t>(),
+                                     h->vals.as<uint32_t>(), st));
     if (timed) mark(h, 4, st);
     // stable sort by bin id only; the last pass also writes the bin ranges
     bool in_tmp = false;
@@ -490,7 +488,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     gs_status so = frame_ownership(h, U.tiles_y, st, &own);
     if (so != GS_OK) return so;
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
-    for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth, &h->offsets})
+    for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth})
         GS_HIP(b->reserve(mm * 4));
     GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)mm) * 4));
@@ -623,14 +621,16 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     // and the scatter moves key + values (read + write); the depth sort's
     // first pass generates the index values instead of reading them
     s.bytes_depth_sort = dpass > 0 ? N * (4 * dpass + 28 + 32 * (dpass - 1)) : 0;
-    s.bytes_scan = N * 20;
-    s.bytes_duplicate = N * 20 + Pi * 8;
+    // scan: per-block totals from the rects (8 B); fused down-sweep +
+    // duplicate: rects again plus the splat order (depth-first) or the depth
+    // keys (bin-first), 4 B, and the pairs written
+    s.bytes_scan = N * 8;
+    s.bytes_duplicate = N * 12 + Pi * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
         // per-bin depth sort: keys read, vals gathered and written back (12 B
-        // per pair); the duplicate also reads the depth keys (4 B per splat)
+        // per pair)
         s.bytes_depth_sort = Pi * 12;
-        s.bytes_duplicate += N * 4;
     }
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
     s.bytes_ranges = T * 8;  // the fill only: ranges come out of the last sort pass

@@ -160,6 +160,23 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, co
     return n;
 }
 
+// The (bin, splat) pairs of one splat, from pair offset `off` on: one per bin
+// of its rect in an owned bin row, minus the bins its ellipse provably misses
+// (row-major bin order).  key = key_hi | bin id.
+__device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
+                                               uint32_t key_hi, uint32_t val, uint32_t off,
+                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    for (uint32_t by = r.by0; by <= r.by1; ++by) {
+        if (!owns_bin_row(by, own)) continue;
+        for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx) {
+            if (bin_excluded(r, by, bx)) continue;  // the ellipse misses this bin
+            keys[off] = key_hi | (by * tiles_x + bx);
+            vals[off] = val;
+            ++off;
+        }
+    }
+}
+
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to
 // nearest even (the Metal/Vulkan unorm conversion rule; parity unpinned: no
 // Metal runtime here), bytes B, G, R, A from low to high address.

@@ -20,25 +20,22 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
-// Exclusive scan of rect_tile_count(rect_lo[i], rect_hi[i], own) into
-// offsets[n]; total[0] (device u64) = sum, total[1] = items with a nonzero
-// count, total[2..3] = the per-bin depth sort sample (seg_sample, 2 words,
-// may be null; reset), see launch_bin_depth_sort.  partials: 2 *
-// ceil(n / kScanItems) u64.
-hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
-                                  bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                  uint32_t* seg_sample, hipStream_t st);
-
-// ---- binning.hip -----------------------------------------------------------
-// Pairs in depth order: for j < n, splat order[j] with rect (rect_lo[j],
-// rect_hi[j]) emits (bin, order[j]) for each bin of its rect whose row is
-// owned by this rank, starting at offsets[j].  order == nullptr
-// means the identity (pairs in index order).  dkey (index order only, may be
-// null): key = dkey[j] << bin_bits | bin, the depth key riding above the bin
-// id for the per-bin depth sort.
-hipError_t launch_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                            const uint32_t* offsets, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                            const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st);
+// Per-block sums of rect_tile_count(rect_lo[i], rect_hi[i], own) and their
+// exclusive scan into partials (2 * ceil(n / kScanItems) u64); total[0]
+// (device u64) = P, total[1] = items with a nonzero count, total[2..3] = the
+// per-bin depth sort sample (seg_sample, 2 words, may be null; reset), see
+// launch_bin_depth_sort.  Then launch_scan_duplicate.
+hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
+                                    bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
+                                    hipStream_t st);
+// Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
+// when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
+// for each bin of its rect whose row this rank owns, minus the excluded bins,
+// at its pair offset.  dkey (index order only, may be null): key = dkey[j] <<
+// bin_bits | bin, the depth key riding above the bin id for the per-bin sort.
+hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
+                                 const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)

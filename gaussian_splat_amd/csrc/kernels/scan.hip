@@ -1,5 +1,17 @@
-// scan.hip — exclusive prefix sum of per-splat tile counts (reduce-then-scan);
-// the counts are derived from the depth-sorted packed rects on the fly.
+// scan.hip — binning: exclusive prefix sum of per-splat
+// bin counts (reduce-then-scan; the counts come from the packed rects on the
+// fly) and the duplicate step that emits the (bin, splat) pairs.
+//
+// Depth-first order: splats sorted by their 15-bit depth key (stable, so
+// equal half depths keep index = arrival order,
+// shaders/gaussian_splat_tile.metal:244) are visited in that order and each
+// emits one (bin, splat index) pair per 32x32 bin of its conservative pixel
+// rect; a stable sort of the pairs by bin id alone (radix_sort.hip, 2 digit
+// passes over P at 1080p, ranges from the last pass) yields each bin's list
+// in S1 order.  Bin-first order: the same pairs in splat index
+// order with the depth key carried above the bin id (key = dkey << bin_bits
+// | bin); after the bin sort each list is put in depth order by a stable
+// per-bin sort (bin_depth_sort.hip).
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -75,57 +87,100 @@ __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict
     }
 }
 
-// Down-sweep: counts are loaded striped (coalesced), transposed through LDS
-// so each lane scans kScanIpt consecutive items, and stored striped again
-// (lane-consecutive stores would be 64 partial-line writes per instruction).
 __device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }  // LDS bank spread
 
-__global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n,
-                                                        const uint64_t* __restrict__ partials,
-                                                        uint32_t* __restrict__ offsets) {
-    __shared__ uint32_t tmp[4];
+// Down-sweep fused with the duplicate: the block's pair offsets are scanned
+// in LDS (counts loaded striped, transposed so each lane scans kScanIpt
+// consecutive items, read back striped), then every splat emits its pairs
+// straight from its rect in registers (striped, one splat per lane per
+// round: neighbouring lanes write neighbouring pair runs).  The rects are
+// read once here and the offsets never leave LDS.
+constexpr int kDupThreads = 1024;                    // 16 waves: many waves to hide the pair stores
+constexpr int kDupIpt = kScanItems / kDupThreads;    // 4 items per lane
+
+// Exclusive scan over a kDupThreads-lane workgroup (LDS-only barriers).
+__device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_t* tmp, uint32_t* total) {
+    constexpr int W = kDupThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_scan_dpp<false>(v);
+    if (lane == 63) tmp[wave] = inc;
+    block_lds_sync();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const uint32_t x = tmp[w];
+        base += (uint32_t)w < wave ? x : 0u;
+        tot += x;
+    }
+    *total = tot;
+    block_lds_sync();
+    return base + inc - v;
+}
+
+__global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
+                                                                     const uint64_t* __restrict__ partials,
+                                                                     const uint32_t* __restrict__ order,
+                                                                     const uint32_t* __restrict__ dkey, int bin_bits,
+                                                                     uint32_t tiles_x, uint32_t* __restrict__ keys,
+                                                                     uint32_t* __restrict__ vals) {
+    __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    uint32_t rlo[kDupIpt], rhi[kDupIpt];
 #pragma unroll
-    for (int k = 0; k < kScanIpt; ++k) {
-        const uint32_t i = k * 256 + tid;
-        st[pad32(i)] = blk + i < n ? count_at(src, blk + i) : 0u;
+    for (int k = 0; k < kDupIpt; ++k) {
+        const uint32_t i = k * kDupThreads + tid;
+        const bool ok = blk + i < n;
+        rlo[k] = ok ? src.lo[blk + i] : kEmptyRectLo;
+        rhi[k] = ok ? src.hi[blk + i] : 0u;
+        st[pad32(i)] = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
     }
-    __syncthreads();
-    uint32_t v[kScanIpt];
+    block_lds_sync();
+    uint32_t v[kDupIpt];
     uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < kScanIpt; ++k) {
-        v[k] = st[pad32(tid * kScanIpt + k)];
+    for (int k = 0; k < kDupIpt; ++k) {
+        v[k] = st[pad32(tid * kDupIpt + k)];
         s += v[k];
     }
     uint32_t t;
-    const uint32_t ex = block256_exclusive_scan<uint32_t>(s, tmp, &t);  // (ends with a barrier)
+    const uint32_t ex = block_dup_exclusive_scan(s, tmp, &t);  // (ends with a barrier)
     uint32_t run = (uint32_t)partials[blockIdx.x] + ex;
 #pragma unroll
-    for (int k = 0; k < kScanIpt; ++k) {
-        st[pad32(tid * kScanIpt + k)] = run;
+    for (int k = 0; k < kDupIpt; ++k) {
+        st[pad32(tid * kDupIpt + k)] = run;
         run += v[k];
     }
-    __syncthreads();
+    block_lds_sync();
 #pragma unroll
-    for (int k = 0; k < kScanIpt; ++k) {
-        const uint32_t i = k * 256 + tid;
-        if (blk + i < n) offsets[blk + i] = st[pad32(i)];
+    for (int k = 0; k < kDupIpt; ++k) {
+        const uint32_t i = k * kDupThreads + tid, j = blk + i;
+        const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);
+        if (j >= n || r.empty) continue;
+        const uint32_t key_hi = dkey ? dkey[j] << bin_bits : 0u;  // depth key above the bin id
+        emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, st[pad32(i)], keys, vals);
     }
 }
 
-hipError_t launch_tile_count_scan(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
-                                  bool masked, uint32_t* offsets, uint64_t* partials, uint64_t* total,
-                                  uint32_t* seg_sample, hipStream_t st) {
+hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
+                                    bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
+                                    hipStream_t st) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
-    uint32_t nb = (n + kScanItems - 1) / kScanItems;
-    if (nb == 0) {
-        return hipMemsetAsync(total, 0, 4 * sizeof(uint64_t), st);
-    }
+    const uint32_t nb = (n + kScanItems - 1) / kScanItems;
+    if (nb == 0) return hipMemsetAsync(total, 0, 4 * sizeof(uint64_t), st);
     scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials);
     scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample);
-    scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
+                                 const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st) {
+    const uint32_t nb = (n + kScanItems - 1) / kScanItems;
+    if (nb == 0) return hipSuccess;
+    if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
+    const CountSrc src{rect_lo, rect_hi, own, masked};
+    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals);
     return hipGetLastError();
 }
 
