@@ -125,6 +125,7 @@ struct gs_handle {
     hipEvent_t sorted_ev = nullptr;        // side stream -> composite stream hand-off
     hipEvent_t set_free[2] = {};           // last use of each buffer set on a composite stream
     int set = 0;
+    bool last_pipe = false;  // the last frame ran pipelined (a switch into pipelining waits for the caller's stream)
     DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr;
     void swap_sets() {
         std::swap(rec, alt_rec);
@@ -846,6 +847,11 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     }
     GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
+    if (pipe && !h->last_pipe) {  // the side stream starts after everything the caller's stream holds
+        GS_HIP(hipEventRecord(h->sorted_ev, st));
+        GS_HIP(hipStreamWaitEvent(sp, h->sorted_ev, 0));
+    }
+    h->last_pipe = pipe;
     begin_frame(h, sp);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),

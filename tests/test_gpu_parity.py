@@ -353,6 +353,31 @@ def test_bin_first_equals_depth_first(built, n, w, h, mode, cap, wall, zr):
     assert linf <= TOL and nbit == 0, (linf, nbit)
 
 
+def test_bin_first_frame_sequences(built):
+    """Sequences of bin-first frames (repeats, camera and resolution
+    switches, pipelined frames with host-output frames in between, which
+    switch pipelining off and on) all equal the depth-first renders."""
+    import torch
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    sc = _scene(60000, 33, 1, aspect=16 / 9)
+    seq = [(640, 360, 0), (640, 360, 0), (640, 360, 1), (800, 450, 2), (640, 360, 1), (800, 450, 0)]
+    refr = InstancedSplatRenderer(sc, Options(sh_degree=1, binning="depth_first"))
+    refr.initialize(0)
+    refs = [refr.render_host(*orbit_views(w, h, 3)[v], w, h) for w, h, v in seq]
+    for fif in (1, 2):
+        r = InstancedSplatRenderer(sc, Options(sh_degree=1, binning="bin_first", frames_in_flight=fif))
+        r.initialize(0)
+        outs = []
+        for w, h, v in seq:
+            outs.append(r.render(*orbit_views(w, h, 3)[v], w, h))
+            if v == 2:  # a host-output frame in between (never pipelined)
+                assert _compare(r.render_host(*orbit_views(w, h, 3)[v], w, h), refs[len(outs) - 1]) == (0.0, 0)
+        torch.cuda.synchronize()
+        for k, o in enumerate(outs):
+            assert _compare(o.cpu().numpy(), refs[k]) == (0.0, 0), (fif, k)
+        assert r.last_stats()["binning"] == 2
+
+
 @pytest.mark.parametrize("n,bits", [(0, 8), (1, 8), (4095, 13), (4096, 16), (4097, 20), (100000, 28),
                                     (1 << 20, 32), (3_000_001, 30)])
 def test_radix_sort(built, n, bits):
