@@ -25,6 +25,10 @@
 
 namespace gs {
 
+#ifndef GS_COMP_MASKSTEP  // A/B knob (tools/build_variant.py): 0 = the branch-free update
+#define GS_COMP_MASKSTEP 1
+#endif
+
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
 __device__ unsigned long long g_cc[8];
@@ -188,6 +192,26 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         bool in = !finished() && covered;
         if constexpr (CAP) in = in && id <= thr;
         any |= in;
+#if GS_COMP_MASKSTEP
+        if constexpr (MODE == 0) {
+            // skipping a lane is bit-identical to adding its exact zero; the
+            // update shares the gaussian's exec-masked block
+            if (in) {
+                const float sa = alpha * (1.0f - A);
+                C0 = __builtin_fmaf(r, sa, C0);
+                C1 = __builtin_fmaf(g, sa, C1);
+                C2 = __builtin_fmaf(bl, sa, C2);
+                A = A + sa;
+            }
+        } else if constexpr (MODE == 1) {
+            if (in) {
+                C0 = __builtin_fmaf(r, T, C0);
+                C1 = __builtin_fmaf(g, T, C1);
+                C2 = __builtin_fmaf(bl, T, C2);
+                T = T * (1.0f - alpha);
+            }
+        } else {
+#else
         if constexpr (MODE == 0) {
             // out-of-support lanes add an exact zero: bit-identical to skipping
             const float sa = in ? alpha * (1.0f - A) : 0.0f;
@@ -196,6 +220,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             C2 = __builtin_fmaf(bl, sa, C2);
             A = A + sa;
         } else {
+#endif
             const float tw = in ? T : 0.0f;
             C0 = __builtin_fmaf(r, tw, C0);
             C1 = __builtin_fmaf(g, tw, C1);
