@@ -54,7 +54,6 @@ hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* 
                                  hipStream_t st);
 
 // ---- radix_sort.hip --------------------------------------------------------
-constexpr int kSortTile = 8192;  // items per sort tile (512 lanes x 16)
 constexpr int kSortBins = 256;   // 8-bit digits
 constexpr int kMaxSortPasses = 4;
 struct SortPlan {

@@ -40,7 +40,7 @@ struct SortIO {
 };
 
 #ifndef GS_RS_IPT1  // A/B knobs (tools/build_variant.py)
-#define GS_RS_IPT1 16
+#define GS_RS_IPT1 12  // 6144-pair tiles: 148 vs 157 us (8: 150, 16: 157, 24: 200) at the bench config
 #endif
 #ifndef GS_RS_PASS_WAVES  // min waves per SIMD of the pass kernel (HIP launch bounds)
 #define GS_RS_PASS_WAVES 1
@@ -256,7 +256,8 @@ SortPlan make_sort_plan(int bits) {
 }
 
 size_t radix_sort_scratch_words(uint32_t n) {
-    const size_t tiles = (n + tile_items(3) - 1) / tile_items(3);  // the smaller tile bounds both
+    const uint32_t t = tile_items(1) < tile_items(3) ? tile_items(1) : tile_items(3);  // the smaller tile bounds both
+    const size_t tiles = (n + t - 1) / t;
     return (size_t)(tiles ? tiles : 1) * kSortBins + kSortBins;
 }
 
