@@ -28,6 +28,9 @@ namespace gs {
 #ifndef GS_COMP_MASKSTEP  // A/B knob (tools/build_variant.py): 0 = the branch-free update
 #define GS_COMP_MASKSTEP 1
 #endif
+#ifndef GS_COMP_QMASK  // A/B knob: per-record quadrant mask computed once at staging
+#define GS_COMP_QMASK 1
+#endif
 
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     __shared__ uint32_t sid[kIds ? kTileThreads : 1];
     __shared__ _Float16 shd[MODE == 3 ? kTileThreads : 1];  // MLAB: half depth of each record
     __shared__ uint8_t wlist[4][kTileThreads];
+    __shared__ uint8_t sqm[GS_COMP_QMASK ? kTileThreads : 1];  // per staged record: quadrants it may reach
 
     // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
     // residue class a contiguous run of tiles (cdna_hip_programming.md §5, T1).
@@ -295,6 +299,29 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             s0[tid] = r0;
             s1[tid] = r1;
             s2[tid] = r2;
+#if GS_COMP_QMASK
+            {
+                // which of the tile's 8x8 quadrants (wave w: column w & 1, row
+                // w >> 1) the record's rect reaches and its cell mask does not
+                // rule out: computed once here instead of by every wave
+                const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
+                const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
+                const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
+                const bool c0 = !(x1 < tx0 || x0 > tx0 + 7u), c1 = !(x1 < tx0 + 8u || x0 > tx0 + 15u);
+                const bool w0 = !(y1 < ty0 || y0 > ty0 + 7u), w1 = !(y1 < ty0 + 8u || y0 > ty0 + 15u);
+                uint32_t qm = (uint32_t)(c0 && w0) | (uint32_t)(c1 && w0) << 1 | (uint32_t)(c0 && w1) << 2 |
+                              (uint32_t)(c1 && w1) << 3;
+                if (a.cell_mask && qm) {
+                    const uint32_t cm = rect_cell_mask(wlo, whi);
+#pragma unroll
+                    for (uint32_t w = 0; w < 4; ++w) {
+                        const uint32_t dcx = (tx0 >> 3) + (w & 1u) - (x0 >> 3), dcy = (ty0 >> 3) + (w >> 1) - (y0 >> 3);
+                        if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) qm &= ~(1u << w);
+                    }
+                }
+                sqm[tid] = (uint8_t)qm;
+            }
+#endif
             if constexpr (kIds) sid[tid] = id_cur;
             if constexpr (MODE == 3)  // half(zF) from the depth key (dkey = 0x7C00 - half bits)
                 shd[tid] = __builtin_bit_cast(_Float16, (uint16_t)(kDepthInf - a.dkey[id_cur]));
@@ -318,6 +345,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 bool hit = false;
+#if GS_COMP_QMASK
+                if (k < cnt_b) hit = (sqm[k] >> wave) & 1u;
+#else
                 if (k < cnt_b) {
                     const float4 c = s2[k];
                     const uint32_t wlo = __float_as_uint(c.z), whi = __float_as_uint(c.w);
@@ -330,6 +360,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                         if (dcx < 4u && dcy < 4u) hit = !((rect_cell_mask(wlo, whi) >> (dcy * 4u + dcx)) & 1u);
                     }
                 }
+#endif
                 const uint64_t m = __ballot(hit);
                 if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
                 nl += (uint32_t)__popcll(m);

@@ -139,7 +139,7 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
 }
 
 template <int DEG>
-__global__ __launch_bounds__(256) void preprocess_kernel(SceneDev s, const FrameUniforms U,
+__global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
                                                          uint32_t* __restrict__ rect_hi) {
