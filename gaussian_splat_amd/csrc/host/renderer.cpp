@@ -77,7 +77,7 @@ struct gs_handle {
     bool initialized = false;
     DevBuf p0, p1, p2, p3, sh4, sh1;
     // per-frame scratch
-    DevBuf rec, dkey, rlo, rhi, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
+    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     // depth-slab frames: full-frame ownership; the colour pass
@@ -141,7 +141,7 @@ struct gs_handle {
     int64_t index_base = 0;
 
     ~gs_handle() {
-        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &partials, &total, &keys,
+        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample})
@@ -443,9 +443,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the bin id)
     const int bits = bits_for(T);
+    if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
     GS_HIP(gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m, (uint32_t)U.tiles_x,
                                      own.dev, U.cell_mask != 0, carry_dkey, bits, h->keys.as<uint32_t>(),
-                                     h->vals.as<uint32_t>(), st));
+                                     h->vals.as<uint32_t>(), st, h->offsets.as<uint32_t>()));
     if (timed) mark(h, 4, st);
     // stable sort by bin id only; the last pass also writes the bin ranges
     bool in_tmp = false;
@@ -622,11 +623,12 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     // and the scatter moves key + values (read + write); the depth sort's
     // first pass generates the index values instead of reading them
     s.bytes_depth_sort = dpass > 0 ? N * (4 * dpass + 28 + 32 * (dpass - 1)) : 0;
-    // scan: per-block totals from the rects (8 B); fused down-sweep +
-    // duplicate: rects again plus the splat order (depth-first) or the depth
-    // keys (bin-first), 4 B, and the pairs written
+    // scan: per-block totals from the rects (8 B).  Duplicate, bin-first:
+    // one fused kernel reads the rects again and the depth keys (12 B);
+    // depth-first: down-sweep (rects + offsets written, 12 B) and duplicate
+    // (rects, order, offsets, 16 B).  Both write the pairs (8 B each).
     s.bytes_scan = N * 8;
-    s.bytes_duplicate = N * 12 + Pi * 8;
+    s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pi * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
         // per-bin depth sort: keys read, vals gathered and written back (12 B

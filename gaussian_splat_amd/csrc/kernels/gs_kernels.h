@@ -33,9 +33,12 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // for each bin of its rect whose row this rank owns, minus the excluded bins,
 // at its pair offset.  dkey (index order only, may be null): key = dkey[j] <<
 // bin_bits | bin, the depth key riding above the bin id for the per-bin sort.
+// Index order runs one fused kernel; depth order (order set) a down-sweep
+// into offsets (n words of scratch) and a one-splat-per-lane duplicate.
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st);
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st,
+                                 uint32_t* offsets = nullptr);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)

@@ -162,6 +162,56 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     }
 }
 
+// Depth-ordered items: the down-sweep writes every item's pair offset and a
+// second kernel emits one splat per lane.  In depth order the splats' sizes
+// follow their depth (near splats are large), so 4096-item blocks of the fused
+// kernel are badly unbalanced (the last blocks emit many times the pairs):
+// 245 us against 123 + 16 us for these two kernels at 6M splats / 4K.
+__global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n,
+                                                        const uint64_t* __restrict__ partials,
+                                                        uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t tmp[4];
+    __shared__ uint32_t st[kScanItems + kScanItems / 32];
+    const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t i = k * 256 + tid;
+        st[pad32(i)] = blk + i < n ? count_at(src, blk + i) : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kScanIpt];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        v[k] = st[pad32(tid * kScanIpt + k)];
+        s += v[k];
+    }
+    uint32_t t;
+    const uint32_t ex = block256_exclusive_scan<uint32_t>(s, tmp, &t);  // (ends with a barrier)
+    uint32_t run = (uint32_t)partials[blockIdx.x] + ex;
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        st[pad32(tid * kScanIpt + k)] = run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t i = k * 256 + tid;
+        if (blk + i < n) offsets[blk + i] = st[pad32(i)];
+    }
+}
+
+__global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n, const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ offsets, uint32_t tiles_x,
+                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (j >= n) return;
+    const BinRect r = bin_rect(src.lo[j], src.hi[j], src.masked);
+    if (r.empty) return;  // culled
+    emit_bin_pairs(r, tiles_x, src.own, 0u, order ? order[j] : j, offsets[j], keys, vals);
+}
+
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     hipStream_t st) {
@@ -175,11 +225,18 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st) {
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st,
+                                 uint32_t* offsets) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked};
+    if (order) {  // depth order: per-item offsets, then one splat per lane
+        if (!offsets) return hipErrorInvalidValue;
+        scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
+        duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals);
+        return hipGetLastError();
+    }
     scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals);
     return hipGetLastError();
 }
