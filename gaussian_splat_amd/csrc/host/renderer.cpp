@@ -77,7 +77,7 @@ struct gs_handle {
     bool initialized = false;
     DevBuf p0, p1, p2, p3, sh4, sh1;
     // per-frame scratch
-    DevBuf rec, dkey, rlo, rhi, offsets, partials, total, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
+    DevBuf rec, dkey, rlo, rhi, offsets, partials, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
     DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
     // depth-slab frames: full-frame ownership; the colour pass
@@ -86,7 +86,8 @@ struct gs_handle {
     bool slab_lists = false;
     int32_t slab_w = 0, slab_h = 0;  // frame of the last gs_slab_project
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
-    uint64_t* host_total = nullptr;  // pinned
+    uint64_t* host_total = nullptr;  // pinned, mapped: the scan writes P here directly
+    uint64_t* dev_total = nullptr;   // its device-side address
     hipEvent_t ev[9] = {};   // stage boundaries 0..7; 8 = exchange done (shard frames)
     // stage_timing 2: packet events (preprocess start/stop, composite start/stop)
     // in a ring of per-frame slots, read without stalling the frames
@@ -141,7 +142,7 @@ struct gs_handle {
     int64_t index_base = 0;
 
     ~gs_handle() {
-        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &total, &keys,
+        for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample})
@@ -314,8 +315,10 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
     GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
-    GS_HIP(h->total.reserve(32));
-    if (!h->host_total) GS_HIP(hipHostMalloc((void**)&h->host_total, 32, hipHostMallocDefault));
+    if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
+        GS_HIP(hipHostMalloc((void**)&h->host_total, 32, hipHostMallocMapped | hipHostMallocCoherent));
+        GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
+    }
     if (!h->seg_sample.ptr) {
         GS_HIP(h->seg_sample.reserve(8));
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 8));
@@ -422,9 +425,9 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
                           const uint32_t* carry_dkey = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
-                                        h->total.as<uint64_t>(), h->seg_sample.as<uint32_t>(), st));
-    GS_HIP(hipMemcpyAsync(h->host_total, h->total.ptr, 32, hipMemcpyDeviceToHost, st));
+                                        h->dev_total, h->seg_sample.as<uint32_t>(), h->ranges.as<uint2>(), T, st));
     GS_HIP(hipStreamSynchronize(st));
     if (timed) mark(h, 3, st);
     const uint64_t P = h->host_total[0];
@@ -440,7 +443,6 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(h->tkeys.reserve(p * 4));
     GS_HIP(h->tvals.reserve(p * 4));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
-    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the bin id)
     const int bits = bits_for(T);
     if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
@@ -450,7 +452,6 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     if (timed) mark(h, 4, st);
     // stable sort by bin id only; the last pass also writes the bin ranges
     bool in_tmp = false;
-    GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), st));
     GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
                                  h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
                                  bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>()));
@@ -627,7 +628,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     // one fused kernel reads the rects again and the depth keys (12 B);
     // depth-first: down-sweep (rects + offsets written, 12 B) and duplicate
     // (rects, order, offsets, 16 B).  Both write the pairs (8 B each).
-    s.bytes_scan = N * 8;
+    s.bytes_scan = N * 8 + T * 8;  // (+ the empty bin ranges, filled on the way)
     s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pi * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
@@ -636,7 +637,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         s.bytes_depth_sort = Pi * 12;
     }
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
-    s.bytes_ranges = T * 8;  // the fill only: ranges come out of the last sort pass
+    s.bytes_ranges = 0;  // ranges come out of the last sort pass
     s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
     // stage_timing 2: read lazily (gs_last_stats / gs_kernel_times), so a
     // frame never waits for itself

@@ -21,13 +21,15 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
 // Per-block sums of rect_tile_count(rect_lo[i], rect_hi[i], own) and their
-// exclusive scan into partials (2 * ceil(n / kScanItems) u64); total[0]
-// (device u64) = P, total[1] = items with a nonzero count, total[2..3] = the
-// per-bin depth sort sample (seg_sample, 2 words, may be null; reset), see
-// launch_bin_depth_sort.  Then launch_scan_duplicate.
+// exclusive scan into partials (2 * ceil(n / kScanItems) u64); total[0] = P,
+// total[1] = items with a nonzero count, total[2..3] = the per-bin depth sort
+// sample (seg_sample, 2 words, may be null; reset), see launch_bin_depth_sort.
+// total may be host-mapped (the host reads it after a stream sync, no copy).
+// ranges[0..nranges) are set to the empty range (~0, ~0) on the way.  Then
+// launch_scan_duplicate.
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
-                                    hipStream_t st);
+                                    uint2* ranges, uint32_t nranges, hipStream_t st);
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
 // when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
 // for each bin of its rect whose row this rank owns, minus the excluded bins,

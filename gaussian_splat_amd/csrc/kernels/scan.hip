@@ -32,8 +32,12 @@ __device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
 
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
-                                                          uint64_t* __restrict__ partials) {
+                                                          uint64_t* __restrict__ partials,
+                                                          uint2* __restrict__ fill, uint32_t nfill) {
     __shared__ uint64_t tmp[4];
+    // the frame's bin ranges start empty (saves a fill dispatch)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nfill; i += gridDim.x * 256u)
+        fill[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
     const uint32_t base = blockIdx.x * kScanItems;
     uint64_t s = 0, vis = 0;
 #pragma unroll
@@ -214,11 +218,17 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
 
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
-                                    hipStream_t st) {
+                                    uint2* ranges, uint32_t nranges, hipStream_t st) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
-    if (nb == 0) return hipMemsetAsync(total, 0, 4 * sizeof(uint64_t), st);
-    scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials);
+    if (nb == 0) {
+        if (nranges) {
+            const hipError_t e = hipMemsetAsync(ranges, 0xFF, (size_t)nranges * sizeof(uint2), st);
+            if (e != hipSuccess) return e;
+        }
+    } else {
+        scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges);
+    }
     scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample);
     return hipGetLastError();
 }
