@@ -478,10 +478,12 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
                              int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr,
-                             hipStream_t sc = nullptr) {
-    // the composite runs on sc (frames_in_flight 2: the caller's stream, while
-    // st is the handle's side stream) once the lists are ready on st
-    if (!sc) sc = st;
+                             const hipStream_t* composite_stream = nullptr) {
+    // the composite runs on *composite_stream when given (frames_in_flight 2:
+    // the caller's stream, while st is the handle's side stream) once the
+    // lists are ready on st.  A pointer, since the caller's stream may be the
+    // null stream.
+    const hipStream_t sc = composite_stream ? *composite_stream : st;
     auto handoff = [&]() -> hipError_t {
         if (sc == st) return hipSuccess;
         hipError_t e = hipEventRecord(h->sorted_ev, st);
@@ -778,7 +780,16 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
         GS_HIP(h->sh1.reserve(n * 4));
         GS_HIP(hipMemcpy(h->sh1.ptr, tail.data(), n * 4, hipMemcpyHostToDevice));
     }
-    GS_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    // frames_in_flight 2: the side stream (projection .. per-bin sort, the
+    // frame's critical path, HBM- and latency-bound) runs at the highest queue
+    // priority, so the dispatcher prefers its workgroups and the overlapping
+    // composite (VALU-bound) fills the remaining slots.  GS_SIDE_PRIORITY=0:
+    // default priority (A/B).
+    int least = 0, greatest = 0;
+    GS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* sp_env = std::getenv("GS_SIDE_PRIORITY");
+    const bool high = !(sp_env && sp_env[0] == '0');
+    GS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, high ? greatest : 0));
     GS_HIP(hipEventCreateWithFlags(&h->sorted_ev, hipEventDisableTiming));
     for (auto& e : h->set_free) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->initialized = true;
@@ -863,7 +874,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
-                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, st)) != GS_OK)
+                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st)) != GS_OK)
         return s;
     GS_HIP(hipEventRecord(h->set_free[h->set], st));  // this set's last reader
     const uint64_t P = (uint64_t)h->stats.pairs;
