@@ -105,6 +105,8 @@ struct gs_handle {
     int last_key_bits = 0;              // bin id bits of the pair keys (depth key above, bin-first)
     bool bin_first_frame = false;       // the last frame used the bin-first order
     DevBuf seg_sample;                  // per-bin depth sort sample (launch_bin_depth_sort)
+    DevBuf npairs;                      // P on the device (0 when it overflows the pair buffers)
+    hipEvent_t totals_ev = nullptr;     // P is in host_total
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
         int32_t w = 0, h = 0;
         int64_t n = -1;
@@ -145,10 +147,11 @@ struct gs_handle {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
-                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample})
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
+        if (totals_ev) (void)hipEventDestroy(totals_ev);
         for (auto& e : set_free)
             if (e) (void)hipEventDestroy(e);
         if (host_total) (void)hipHostFree(host_total);
@@ -323,6 +326,8 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(h->seg_sample.reserve(8));
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 8));
     }
+    GS_HIP(h->npairs.reserve(4));
+    if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
         for (auto& slot : h->kev)
@@ -420,16 +425,57 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
 // rects (rect_lo, rect_hi) in that order: per-block pair totals and their
 // scan (P and the visible count to host) -> down-sweep fused with the
 // duplicate -> stable sort by bin id -> ranges.  Marks 3..6 when `timed`.
+// The duplicate and the sort are queued before the host waits for P: they
+// read the pair count on the device and are sized by the pair buffers'
+// capacity (grown to the last frame's P); a frame whose P exceeds it runs
+// them as no-ops, and they are queued again once the buffers have grown.
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
                           const uint32_t* carry_dkey = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    const int bits = bits_for(T);
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
+    if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
+    // pair capacity of this buffer set: at least the last frame's P
+    auto reserve_pairs = [&](uint64_t want) -> uint32_t {
+        const size_t p = (size_t)std::max<uint64_t>(want, 1) * 4;
+        // growing frees the set's buffers: its last composite must be done
+        if (p > std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) &&
+            hipEventSynchronize(h->set_free[h->set]) != hipSuccess)
+            return 0;
+        for (DevBuf* b : {&h->keys, &h->vals, &h->tkeys, &h->tvals})
+            if (b->reserve(p) != hipSuccess) return 0;
+        const size_t c = std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) / 4;
+        const uint32_t cap = (uint32_t)std::min<size_t>(c, UINT32_MAX - 1);
+        if (h->sort_scratch.reserve(gs::radix_sort_scratch_words(cap) * 4) != hipSuccess) return 0;
+        return cap;
+    };
+    uint32_t cap = reserve_pairs(h->order.frame_pairs);
+    if (!cap) return fail(GS_ERR_OOM, "pair buffers");
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
-                                        h->dev_total, h->seg_sample.as<uint32_t>(), h->ranges.as<uint2>(), T, st));
-    GS_HIP(hipStreamSynchronize(st));
+                                        h->dev_total, h->seg_sample.as<uint32_t>(), h->ranges.as<uint2>(), T,
+                                        h->npairs.as<uint32_t>(), cap, st));
+    GS_HIP(hipEventRecord(h->totals_ev, st));
     if (timed) mark(h, 3, st);
+    // pairs (bin, splat) in visiting order (bin-first: the depth key above the
+    // bin id), then a stable sort by bin id only; the last pass also writes
+    // the bin ranges
+    bool in_tmp = false;
+    auto enqueue_lists = [&]() -> hipError_t {
+        hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
+                                                 (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
+                                                 h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
+                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>());
+        if (e != hipSuccess) return e;
+        if (timed) mark(h, 4, st);
+        return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
+                                     h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap,
+                                     bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>(),
+                                     h->npairs.as<uint32_t>());
+    };
+    GS_HIP(enqueue_lists());
+    GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
     const uint64_t P = h->host_total[0];
     h->stats.visible = (int64_t)h->host_total[1];
     // the last per-bin depth sort's share of pairs in lists too long for LDS
@@ -437,24 +483,14 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         h->order.long_share = (double)h->host_total[2] / (double)h->order.sample_pairs;
     h->order.frame_pairs = P;
     if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
-    const size_t p = (size_t)std::max<uint64_t>(P, 1);
-    GS_HIP(h->keys.reserve(p * 4));
-    GS_HIP(h->vals.reserve(p * 4));
-    GS_HIP(h->tkeys.reserve(p * 4));
-    GS_HIP(h->tvals.reserve(p * 4));
-    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)p) * 4));
-    // pairs (bin, splat) in visiting order (bin-first: the depth key above the bin id)
-    const int bits = bits_for(T);
-    if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
-    GS_HIP(gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m, (uint32_t)U.tiles_x,
-                                     own.dev, U.cell_mask != 0, carry_dkey, bits, h->keys.as<uint32_t>(),
-                                     h->vals.as<uint32_t>(), st, h->offsets.as<uint32_t>()));
-    if (timed) mark(h, 4, st);
-    // stable sort by bin id only; the last pass also writes the bin ranges
-    bool in_tmp = false;
-    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
-                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), (uint32_t)P,
-                                 bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>()));
+    if (P > cap) {
+        // the queued lists were no-ops (ranges still empty): grow, queue again
+        GS_HIP(hipStreamSynchronize(st));
+        if (!(cap = reserve_pairs(P))) return fail(GS_ERR_OOM, "pair buffers");
+        const uint32_t p32 = (uint32_t)P;
+        GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
+        GS_HIP(enqueue_lists());
+    }
     uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
     uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
     h->last_keys = sk;

@@ -25,11 +25,15 @@ constexpr int kScanItems = 4096;  // per block
 // total[1] = items with a nonzero count, total[2..3] = the per-bin depth sort
 // sample (seg_sample, 2 words, may be null; reset), see launch_bin_depth_sort.
 // total may be host-mapped (the host reads it after a stream sync, no copy).
-// ranges[0..nranges) are set to the empty range (~0, ~0) on the way.  Then
-// launch_scan_duplicate.
+// ranges[0..nranges) are set to the empty range (~0, ~0) on the way.
+// npairs (device u32) = P when P <= cap (the pair buffers' capacity), else 0:
+// the kernels after it read the pair count from there, so they can be queued
+// before the host has seen P (an overflowing frame makes them no-ops and the
+// host re-queues them with larger buffers).  Then launch_scan_duplicate.
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
-                                    uint2* ranges, uint32_t nranges, hipStream_t st);
+                                    uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
+                                    hipStream_t st);
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
 // when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
 // for each bin of its rect whose row this rank owns, minus the excluded bins,
@@ -37,9 +41,11 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // bin_bits | bin, the depth key riding above the bin id for the per-bin sort.
 // Index order runs one fused kernel; depth order (order set) a down-sweep
 // into offsets (n words of scratch) and a one-splat-per-lane duplicate.
+// Nothing is written when *npairs == 0 (see launch_tile_count_totals).
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st,
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
+                                 const uint32_t* npairs, hipStream_t st,
                                  uint32_t* offsets = nullptr);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
@@ -77,9 +83,13 @@ size_t radix_sort_scratch_words(uint32_t n);
 // ranges (optional): key-value extents of the sorted output, stored as
 // {start, ~end} (fill with 0xFF before; empty key = {~0, ~0}); see
 // decode_range.
+// n_dev (optional): the item count is read on the device from *n_dev (<= n;
+// n sizes the grids and the scratch), so the sort can be queued before the
+// host knows it.
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
-                             bool* result_in_tmp, hipStream_t st, uint2* ranges = nullptr);
+                             bool* result_in_tmp, hipStream_t st, uint2* ranges = nullptr,
+                             const uint32_t* n_dev = nullptr);
 // Same with three value arrays (vals_in[0] may be null: value = index).
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,

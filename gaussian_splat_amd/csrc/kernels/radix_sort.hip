@@ -79,8 +79,10 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int digi
 
 template <int NV>
 __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                        uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles) {
+                                                        uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles,
+                                                        const uint32_t* __restrict__ n_dev) {
     constexpr uint32_t TILE = tile_items(NV);
+    if (n_dev) n = *n_dev;  // tiles past it count zeros
     __shared__ uint32_t h[kRsWaves][kSortBins];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
@@ -126,9 +128,12 @@ template <int NV>
 __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        int digit_bits, const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
-                                                       uint2* __restrict__ ranges, uint32_t rmask) {
+                                                       uint2* __restrict__ ranges, uint32_t rmask,
+                                                       const uint32_t* __restrict__ n_dev) {
     constexpr int IPT = ipt_for(NV);
     constexpr uint32_t TILE = tile_items(NV);
+    if (n_dev) n = *n_dev;
+    if (blockIdx.x * TILE >= n) return;  // (whole workgroup: before any barrier)
     constexpr uint32_t WAVE_ITEMS = 64u * IPT;
     __shared__ uint32_t wh[kRsWaves][kSortBins];  // wave-private running counts -> wave offsets
     __shared__ uint32_t blk_start[kSortBins];     // tile-local start of each digit
@@ -264,7 +269,8 @@ size_t radix_sort_scratch_words(uint32_t n) {
 template <int NV>
 static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
-                                  int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st) {
+                                  int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
+                                  const uint32_t* n_dev) {
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -285,11 +291,11 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     for (int p = 0; p < plan.passes; ++p) {
         io.kout = to_final ? keys : tmp_keys;
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
-        rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles);
+        rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
         rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
         rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
                                                           totals, tiles, p + 1 == plan.passes ? ranges : nullptr,
-                                                          bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u);
+                                                          bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev);
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;
@@ -299,18 +305,19 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
 
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
-                             bool* result_in_tmp, hipStream_t st, uint2* ranges) {
+                             bool* result_in_tmp, hipStream_t st, uint2* ranges, const uint32_t* n_dev) {
     const uint32_t* vi[1] = {vals_in};
     uint32_t* vo[1] = {vals};
     uint32_t* vt[1] = {tmp_vals};
-    return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, ranges, st);
+    return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, ranges, st,
+                              n_dev);
 }
 
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                               int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
     return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp,
-                              nullptr, st);
+                              nullptr, st, nullptr);
 }
 
 }  // namespace gs

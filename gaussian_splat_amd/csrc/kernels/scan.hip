@@ -64,7 +64,8 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
 // back to the host with the pair count.
 __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                             uint64_t* __restrict__ total,
-                                                            uint32_t* __restrict__ seg_sample) {
+                                                            uint32_t* __restrict__ seg_sample,
+                                                            uint32_t* __restrict__ npairs, uint64_t cap) {
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
+        if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
     }
 }
 
@@ -126,7 +128,9 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                                                      const uint32_t* __restrict__ order,
                                                                      const uint32_t* __restrict__ dkey, int bin_bits,
                                                                      uint32_t tiles_x, uint32_t* __restrict__ keys,
-                                                                     uint32_t* __restrict__ vals) {
+                                                                     uint32_t* __restrict__ vals,
+                                                                     const uint32_t* __restrict__ npairs) {
+    if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
@@ -208,9 +212,10 @@ __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n
 
 __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n, const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ offsets, uint32_t tiles_x,
-                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ npairs) {
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    if (j >= n) return;
+    if (j >= n || *npairs == 0u) return;
     const BinRect r = bin_rect(src.lo[j], src.hi[j], src.masked);
     if (r.empty) return;  // culled
     emit_bin_pairs(r, tiles_x, src.own, 0u, order ? order[j] : j, offsets[j], keys, vals);
@@ -218,7 +223,8 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
 
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
-                                    uint2* ranges, uint32_t nranges, hipStream_t st) {
+                                    uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
+                                    hipStream_t st) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
@@ -229,14 +235,14 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
     } else {
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges);
     }
-    scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample);
+    scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample, npairs, cap);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
-                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals, hipStream_t st,
-                                 uint32_t* offsets) {
+                                 const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
+                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
@@ -244,10 +250,11 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
-        duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals);
+        duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
         return hipGetLastError();
     }
-    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals);
+    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
+                                                      npairs);
     return hipGetLastError();
 }
 

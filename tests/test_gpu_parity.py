@@ -378,6 +378,40 @@ def test_bin_first_frame_sequences(built):
         assert r.last_stats()["binning"] == 2
 
 
+@pytest.mark.parametrize("binning", ["depth_first", "bin_first"])
+def test_pair_count_growth(built, binning):
+    """The duplicate and the bin sort are queued before the host sees the
+    frame's pair count, sized by the last frame's: frames whose count grows
+    (camera moving in, P several times the last) take the re-queue path and
+    still equal a fresh renderer's frame, pipelined or not."""
+    import torch
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd.api import default_camera
+    sc = _scene(50000, 41, 0, aspect=16 / 9)
+    W, H = 640, 360
+    views = []
+    for d in (2.0, 3.0, 12.0, 6.0, 2.0):  # P grows over the first four frames here
+        cam = default_camera(W, H)
+        cam.setDistance(d)
+        views.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
+    refs, pairs = [], []
+    for v in views:  # a fresh renderer per frame: its first frame always re-queues
+        fr = InstancedSplatRenderer(sc, Options(sh_degree=0, binning=binning))
+        fr.initialize(0)
+        refs.append(fr.render_host(*v, W, H))
+        pairs.append(fr.last_stats()["pairs"])
+    # each growth step exceeds the last frame's capacity (P + 1/8 slack)
+    assert pairs[1] > 1.3 * pairs[0] and pairs[2] > 1.3 * pairs[1] and pairs[3] > pairs[2], pairs
+    for fif in (1, 2):
+        r = InstancedSplatRenderer(sc, Options(sh_degree=0, binning=binning, frames_in_flight=fif))
+        r.initialize(0)
+        outs = [r.render(*v, W, H) for v in views]
+        torch.cuda.synchronize()
+        for k, o in enumerate(outs):
+            assert _compare(o.cpu().numpy(), refs[k]) == (0.0, 0), (fif, k)
+        assert r.last_stats()["pairs"] == pairs[-1]
+
+
 @pytest.mark.parametrize("n,bits", [(0, 8), (1, 8), (4095, 13), (4096, 16), (4097, 20), (100000, 28),
                                     (1 << 20, 32), (3_000_001, 30)])
 def test_radix_sort(built, n, bits):
