@@ -323,8 +323,8 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
     }
     if (!h->seg_sample.ptr) {
-        GS_HIP(h->seg_sample.reserve(8));
-        GS_HIP(hipMemset(h->seg_sample.ptr, 0, 8));
+        GS_HIP(h->seg_sample.reserve(16));
+        GS_HIP(hipMemset(h->seg_sample.ptr, 0, 16));
     }
     GS_HIP(h->npairs.reserve(4));
     if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
@@ -454,7 +454,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     uint32_t cap = reserve_pairs(h->order.frame_pairs);
     if (!cap) return fail(GS_ERR_OOM, "pair buffers");
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
-                                        h->dev_total, h->seg_sample.as<uint32_t>(), h->ranges.as<uint2>(), T,
+                                        h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
                                         h->npairs.as<uint32_t>(), cap, st));
     GS_HIP(hipEventRecord(h->totals_ev, st));
     if (timed) mark(h, 3, st);
@@ -578,16 +578,20 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         h->order.sample_pairs = P;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
+        // (the per-bin sort stays on the side stream: on the composite stream,
+        // beside the next frame's projection, it was starved)
+        const hipStream_t sd = st;
         if (ca.cap > 0) {  // per-pixel cap thresholds from the lists in arrival order
             GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
             ca.thr_out = h->thr.as<uint32_t>();
-            GS_HIP(gs::launch_cap_threshold(ca, st));
+            GS_HIP(gs::launch_cap_threshold(ca, sd));
             ca.thr = h->thr.as<uint32_t>();
         }
+        // (one sample word pair per buffer set)
         GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
                                          h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
-                                         h->seg_sample.as<uint32_t>(), st));
-        mark(h, 6, st);
+                                         h->seg_sample.as<uint32_t>() + 2 * h->set, sd));
+        mark(h, 6, sd);
         if (slab_t) {
             ca.slab = 1;
             ca.t_out = slab_t;
