@@ -13,6 +13,34 @@
 
 namespace gs {
 
+#ifndef GS_PRE_NT  // A/B knob: scene loads with the non-temporal hint (read once per frame)
+#define GS_PRE_NT 1
+#endif
+typedef float gs_f4 __attribute__((ext_vector_type(4)));
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 scene_load(const float4* p) {
+#if GS_PRE_NT
+    const gs_f4 v = __builtin_nontemporal_load(reinterpret_cast<const gs_f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float2 scene_load(const float2* p) {
+#if GS_PRE_NT
+    const gs_f2 v = __builtin_nontemporal_load(reinterpret_cast<const gs_f2*>(p));
+    return make_float2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float scene_load(const float* p) {
+#if GS_PRE_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 
 template <int DEG>
 __device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px, float py, float pz,
@@ -60,13 +88,13 @@ __device__ __forceinline__ void sh_color(const SceneDev& s, uint32_t i, float px
         float coef[NF];
 #pragma unroll
         for (int m = 0; m < NP4; ++m) {
-            float4 v = s.sh4[(size_t)m * s.n + i];
+            float4 v = scene_load(&s.sh4[(size_t)m * s.n + i]);
             coef[4 * m + 0] = v.x;
             coef[4 * m + 1] = v.y;
             coef[4 * m + 2] = v.z;
             coef[4 * m + 3] = v.w;
         }
-        if constexpr (NF % 4 != 0) coef[NF - 1] = s.sh1[i];
+        if constexpr (NF % 4 != 0) coef[NF - 1] = scene_load(&s.sh1[i]);
         float acc0 = SH_C0 * c0, acc1 = SH_C0 * c1, acc2 = SH_C0 * c2;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -150,7 +178,7 @@ __global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const Fr
     uint32_t key = 0;
     uint32_t rlo = kEmptyRectLo, rhi = 0u;
 
-    float4 a0 = s.p0[i];
+    float4 a0 = scene_load(&s.p0[i]);
     float px = a0.x, py = a0.y, pz = a0.z;
     // K3: view position, zFront (tile.metal:94-105)
     float vx = xform_row(V, 0, px, py, pz);
@@ -166,8 +194,8 @@ __global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const Fr
         float invw = 1.0f / clw;
         float ndcz = clz * invw;
         if (ndcz >= 0.0f && ndcz <= 1.0f && zf >= 0.001f) {
-            float4 q = s.p1[i];
-            float4 a2 = s.p2[i];
+            float4 q = scene_load(&s.p1[i]);
+            float4 a2 = scene_load(&s.p2[i]);
             // K1 (tile.metal:40-49)
             float qs = q.x * q.x;
             qs = __builtin_fmaf(q.y, q.y, qs);
@@ -279,7 +307,7 @@ __global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const Fr
                 if (x0f <= x1f && y0f <= y1f) {
                     uint32_t x0 = (uint32_t)x0f, x1 = (uint32_t)x1f, y0 = (uint32_t)y0f, y1 = (uint32_t)y1f;
                     float cr, cg, cbl;
-                    float2 a3 = s.p3[i];
+                    float2 a3 = scene_load(&s.p3[i]);
                     sh_color<DEG>(s, i, px, py, pz, U.campos, a2.w, a3.x, a3.y, cr, cg, cbl);
                     float4* o = rec + 3 * (size_t)i;
                     const float4 ra = make_float4(cx, cy, e1x * k1, e1y * k1);
