@@ -453,9 +453,23 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     };
     uint32_t cap = reserve_pairs(h->order.frame_pairs);
     if (!cap) return fail(GS_ERR_OOM, "pair buffers");
+    // index order: the duplicate counts the first sort pass's digits itself
+    const gs::SortPlan plan = gs::make_sort_plan(bits);
+    auto pass_counts = [&]() {
+        gs::PassCounts pc;
+        if (!order && plan.passes > 0) {
+            pc.C = h->sort_scratch.as<uint32_t>();
+            pc.tile = gs::radix_sort_tile_items();
+            pc.mask = plan.mask[0];
+            pc.ntiles = (cap + pc.tile - 1) / pc.tile;
+        }
+        return pc;
+    };
+    gs::PassCounts pc = pass_counts();
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                         h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
-                                        h->npairs.as<uint32_t>(), cap, st));
+                                        h->npairs.as<uint32_t>(), cap, pc.C, pc.C ? (pc.mask + 1) * pc.ntiles : 0u,
+                                        st));
     GS_HIP(hipEventRecord(h->totals_ev, st));
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
@@ -466,13 +480,13 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>());
+                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
                                      h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap,
                                      bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>(),
-                                     h->npairs.as<uint32_t>());
+                                     h->npairs.as<uint32_t>(), pc.C != nullptr);
     };
     GS_HIP(enqueue_lists());
     GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
@@ -489,6 +503,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (!(cap = reserve_pairs(P))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
+        pc = pass_counts();
+        if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         GS_HIP(enqueue_lists());
     }
     uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();

@@ -163,18 +163,28 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, co
 // The (bin, splat) pairs of one splat, from pair offset `off` on: one per bin
 // of its rect in an owned bin row, minus the bins its ellipse provably misses
 // (row-major bin order).  key = key_hi | bin id.
+// on_pair(offset, bin) is called for every pair written.
+template <typename F>
 __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
                                                uint32_t key_hi, uint32_t val, uint32_t off,
-                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                               F&& on_pair) {
     for (uint32_t by = r.by0; by <= r.by1; ++by) {
         if (!owns_bin_row(by, own)) continue;
         for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx) {
             if (bin_excluded(r, by, bx)) continue;  // the ellipse misses this bin
-            keys[off] = key_hi | (by * tiles_x + bx);
+            const uint32_t bin = by * tiles_x + bx;
+            keys[off] = key_hi | bin;
             vals[off] = val;
+            on_pair(off, bin);
             ++off;
         }
     }
+}
+__device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
+                                               uint32_t key_hi, uint32_t val, uint32_t off,
+                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    emit_bin_pairs(r, tiles_x, own, key_hi, val, off, keys, vals, [](uint32_t, uint32_t) {});
 }
 
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to

@@ -30,10 +30,21 @@ constexpr int kScanItems = 4096;  // per block
 // the kernels after it read the pair count from there, so they can be queued
 // before the host has seen P (an overflowing frame makes them no-ops and the
 // host re-queues them with larger buffers).  Then launch_scan_duplicate.
+// zero[0..nzero) is cleared on the way (the first sort pass's digit counts,
+// PassCounts).
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    hipStream_t st);
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st);
+// The first LSD pass's digit counts of the pairs, C[digit][tile] with
+// `ntiles` columns, tiles of `tile` pairs, digit = bin & mask: the index-order
+// duplicate adds them up as it writes (C zeroed before), so the sort skips
+// that pass's count kernel (launch_radix_sort first_counted).  C null: off.
+struct PassCounts {
+    uint32_t* C = nullptr;
+    uint32_t tile = 0, mask = 0, ntiles = 0;
+};
+constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts in LDS (the rest: global atomics)
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
 // when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
 // for each bin of its rect whose row this rank owns, minus the excluded bins,
@@ -46,7 +57,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
-                                 uint32_t* offsets = nullptr);
+                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{});
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -76,6 +87,9 @@ struct SortPlan {
 SortPlan make_sort_plan(int bits);
 // Scratch words (uint32) needed by launch_radix_sort for n items.
 size_t radix_sort_scratch_words(uint32_t n);
+// Items per tile of launch_radix_sort (its C matrix has ceil(n / tile) columns
+// at the start of the scratch).
+uint32_t radix_sort_tile_items();
 // Stable LSD sort on key bits [0, bits).  Reads (keys_in, vals_in) — vals_in
 // may be null (value = index) — and leaves the result in (keys, vals), or in
 // (tmp_keys, tmp_vals) when *result_in_tmp (only if the inputs alias the
@@ -89,7 +103,7 @@ size_t radix_sort_scratch_words(uint32_t n);
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
                              bool* result_in_tmp, hipStream_t st, uint2* ranges = nullptr,
-                             const uint32_t* n_dev = nullptr);
+                             const uint32_t* n_dev = nullptr, bool first_counted = false);
 // Same with three value arrays (vals_in[0] may be null: value = index).
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,

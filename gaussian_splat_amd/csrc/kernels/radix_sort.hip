@@ -260,6 +260,8 @@ SortPlan make_sort_plan(int bits) {
     return p;
 }
 
+uint32_t radix_sort_tile_items() { return tile_items(1); }
+
 size_t radix_sort_scratch_words(uint32_t n) {
     const uint32_t t = tile_items(1) < tile_items(3) ? tile_items(1) : tile_items(3);  // the smaller tile bounds both
     const size_t tiles = (n + t - 1) / t;
@@ -270,7 +272,7 @@ template <int NV>
 static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
-                                  const uint32_t* n_dev) {
+                                  const uint32_t* n_dev, bool first_counted) {
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -291,7 +293,8 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     for (int p = 0; p < plan.passes; ++p) {
         io.kout = to_final ? keys : tmp_keys;
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
-        rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
+        if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
+            rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
         rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
         rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
                                                           totals, tiles, p + 1 == plan.passes ? ranges : nullptr,
@@ -305,19 +308,20 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
 
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
-                             bool* result_in_tmp, hipStream_t st, uint2* ranges, const uint32_t* n_dev) {
+                             bool* result_in_tmp, hipStream_t st, uint2* ranges, const uint32_t* n_dev,
+                             bool first_counted) {
     const uint32_t* vi[1] = {vals_in};
     uint32_t* vo[1] = {vals};
     uint32_t* vt[1] = {tmp_vals};
     return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, ranges, st,
-                              n_dev);
+                              n_dev, first_counted);
 }
 
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                               int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
     return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp,
-                              nullptr, st, nullptr);
+                              nullptr, st, nullptr, false);
 }
 
 }  // namespace gs

@@ -33,11 +33,14 @@ __device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials,
-                                                          uint2* __restrict__ fill, uint32_t nfill) {
+                                                          uint2* __restrict__ fill, uint32_t nfill,
+                                                          uint32_t* __restrict__ zero, uint32_t nzero) {
     __shared__ uint64_t tmp[4];
-    // the frame's bin ranges start empty (saves a fill dispatch)
+    // the frame's bin ranges start empty and the first sort pass's digit
+    // counts at zero (saves two fill dispatches)
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nfill; i += gridDim.x * 256u)
         fill[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
     const uint32_t base = blockIdx.x * kScanItems;
     uint64_t s = 0, vis = 0;
 #pragma unroll
@@ -129,11 +132,15 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                                                      const uint32_t* __restrict__ dkey, int bin_bits,
                                                                      uint32_t tiles_x, uint32_t* __restrict__ keys,
                                                                      uint32_t* __restrict__ vals,
-                                                                     const uint32_t* __restrict__ npairs) {
+                                                                     const uint32_t* __restrict__ npairs,
+                                                                     PassCounts pc) {
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
+    __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    if (pc.C)
+        for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
     uint32_t rlo[kDupIpt], rhi[kDupIpt];
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
@@ -160,13 +167,39 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         run += v[k];
     }
     block_lds_sync();
+    // the first sort pass's digit counts per tile of pc.tile pairs (rts_count
+    // without its key re-read): the block's pairs are contiguous from its
+    // partial, so its first kDupCountTiles tiles count in LDS
+    const uint32_t t_lo = pc.C ? (uint32_t)(partials[blockIdx.x] / pc.tile) : 0u;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid, j = blk + i;
         const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);
         if (j >= n || r.empty) continue;
         const uint32_t key_hi = dkey ? dkey[j] << bin_bits : 0u;  // depth key above the bin id
-        emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, st[pad32(i)], keys, vals);
+        const uint32_t off = st[pad32(i)];
+        if (pc.C) {
+            uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, off, keys, vals,
+                           [&](uint32_t g, uint32_t bin) {
+                               if (g == next) {
+                                   ++t;
+                                   next += pc.tile;
+                               }
+                               const uint32_t d = bin & pc.mask;
+                               if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
+                               else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
+                           });
+        } else {
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, off, keys, vals);
+        }
+    }
+    if (pc.C) {
+        block_lds_sync();
+        for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) {
+            const uint32_t t = i / kSortBins, d = i % kSortBins, v = (&lh[0][0])[i];
+            if (v && t_lo + t < pc.ntiles) atomicAdd(&pc.C[(size_t)d * pc.ntiles + t_lo + t], v);
+        }
     }
 }
 
@@ -224,7 +257,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    hipStream_t st) {
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
@@ -232,8 +265,12 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
             const hipError_t e = hipMemsetAsync(ranges, 0xFF, (size_t)nranges * sizeof(uint2), st);
             if (e != hipSuccess) return e;
         }
+        if (nzero) {
+            const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * 4, st);
+            if (e != hipSuccess) return e;
+        }
     } else {
-        scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges);
+        scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
     scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample, npairs, cap);
     return hipGetLastError();
@@ -242,7 +279,7 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
-                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets) {
+                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
@@ -254,7 +291,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
         return hipGetLastError();
     }
     scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
-                                                      npairs);
+                                                      npairs, pc);
     return hipGetLastError();
 }
 
