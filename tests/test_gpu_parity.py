@@ -412,6 +412,28 @@ def test_pair_count_growth(built, binning):
         assert r.last_stats()["pairs"] == pairs[-1]
 
 
+def test_large_splats_bin_first(built):
+    """Large splats: a duplicate block's 4096 splats emit far more pairs than
+    its LDS digit counts cover (4 sort tiles of 6144 pairs), so the first
+    sort pass's counts also go through the global-atomic path; bin-first
+    and depth-first frames stay identical."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd import scene as S
+    raw = S.synthetic_raw(40000, seed=77, aspect=16 / 9)
+    raw.log_scale += np.float32(np.log(12.0))
+    sc = S.activate(raw, 0)
+    W, H = 960, 540
+    outs = {}
+    for b in ("depth_first", "bin_first"):
+        r = InstancedSplatRenderer(sc, Options(sh_degree=0, binning=b))
+        r.initialize(0)
+        v, p = orbit_views(W, H, 1)[0]
+        outs[b] = r.render_host(v, p, W, H)
+        st = r.last_stats()
+    assert st["pairs"] / 40000 * 4096 > 4 * 6144, st["pairs"]  # pairs per duplicate block
+    assert _compare(outs["bin_first"], outs["depth_first"]) == (0.0, 0)
+
+
 @pytest.mark.parametrize("n,bits", [(0, 8), (1, 8), (4095, 13), (4096, 16), (4097, 20), (100000, 28),
                                     (1 << 20, 32), (3_000_001, 30)])
 def test_radix_sort(built, n, bits):
