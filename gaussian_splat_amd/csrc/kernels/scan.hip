@@ -65,30 +65,64 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
 // seg_sample (may be null): the per-bin depth sort's sample since the last
 // scan (bin_depth_sort.hip) is moved into total[2..3] and reset, so it comes
 // back to the host with the pair count.
-__global__ __launch_bounds__(256) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
-                                                            uint64_t* __restrict__ total,
-                                                            uint32_t* __restrict__ seg_sample,
-                                                            uint32_t* __restrict__ npairs, uint64_t cap) {
+// One 1024-lane workgroup: each lane scans kPartIpt consecutive block sums in
+// registers, one block-wide scan joins them (a single pass for nb <= 4096;
+// larger grids loop).
+constexpr int kPartThreads = 1024;
+constexpr int kPartIpt = 4;
+
+template <typename T>
+__device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
+    constexpr int W = kPartThreads / 64;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const T inc = wave_inclusive_scan(v);
+    if (lane == 63) tmp[wave] = inc;
+    __syncthreads();
+    T base = T(0), tot = T(0);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const T x = tmp[w];
+        base += (uint32_t)w < wave ? x : T(0);
+        tot += x;
+    }
+    *total = tot;
+    __syncthreads();
+    return base + inc - v;
+}
+
+__global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
+                                                                     uint64_t* __restrict__ total,
+                                                                     uint32_t* __restrict__ seg_sample,
+                                                                     uint32_t* __restrict__ npairs, uint64_t cap) {
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
         seg_sample[0] = 0u;
         seg_sample[1] = 0u;
     }
-    __shared__ uint64_t tmp[4];
-    uint64_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
-        uint32_t i = b0 + threadIdx.x;
-        uint64_t v = i < nb ? partials[i] : 0;
+    __shared__ uint64_t tmp[kPartThreads / 64];
+    constexpr uint32_t CH = kPartThreads * kPartIpt;
+    uint64_t carry = 0, vis = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
+        const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
+        uint64_t v[kPartIpt], s = 0;
+#pragma unroll
+        for (int k = 0; k < kPartIpt; ++k) {
+            v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
+            s += v[k];
+            vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
+        }
         uint64_t t;
-        uint64_t ex = block256_exclusive_scan<uint64_t>(v, tmp, &t);
-        if (i < nb) partials[i] = carry + ex;
+        uint64_t run = carry + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
+#pragma unroll
+        for (int k = 0; k < kPartIpt; ++k) {
+            if (i0 + k < nb) partials[i0 + k] = run;
+            run += v[k];
+        }
         carry += t;
     }
-    uint64_t vis = 0;
-    for (uint32_t b = threadIdx.x; b < nb; b += 256) vis += partials[nb + b];
     uint64_t vt;
-    block256_exclusive_scan<uint64_t>(vis, tmp, &vt);
+    block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
@@ -272,7 +306,7 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
     } else {
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
-    scan_partials_kernel<<<1, 256, 0, st>>>(partials, nb, total, seg_sample, npairs, cap);
+    scan_partials_kernel<<<1, kPartThreads, 0, st>>>(partials, nb, total, seg_sample, npairs, cap);
     return hipGetLastError();
 }
 
