@@ -102,18 +102,46 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void rts_scan_kernel(uint32_t* __restrict__ C, uint32_t ntiles,
-                                                       uint32_t* __restrict__ totals) {
-    __shared__ uint32_t tmp[4];
+// One 1024-lane workgroup per digit: each lane scans kRsScanIpt consecutive
+// tile counts in registers, one block-wide scan joins them (one pass for up
+// to 4096 tiles; larger grids loop).
+constexpr int kRsScanThreads = 1024;
+constexpr int kRsScanIpt = 4;
+
+__global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __restrict__ C, uint32_t ntiles,
+                                                                  uint32_t* __restrict__ totals) {
+    constexpr int W = kRsScanThreads / 64;
+    constexpr uint32_t CH = kRsScanThreads * kRsScanIpt;
+    __shared__ uint32_t tmp[W];
     uint32_t* row = C + (size_t)blockIdx.x * ntiles;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < ntiles; b0 += 256) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t v = i < ntiles ? row[i] : 0u;
-        uint32_t t;
-        const uint32_t ex = block256_exclusive_scan<uint32_t>(v, tmp, &t);
-        if (i < ntiles) row[i] = carry + ex;
-        carry += t;
+    for (uint32_t b0 = 0; b0 < ntiles; b0 += CH) {
+        const uint32_t i0 = b0 + threadIdx.x * kRsScanIpt;
+        uint32_t v[kRsScanIpt], s = 0;
+#pragma unroll
+        for (int k = 0; k < kRsScanIpt; ++k) {
+            v[k] = i0 + k < ntiles ? row[i0 + k] : 0u;
+            s += v[k];
+        }
+        const uint32_t inc = wave_scan_dpp<false>(s);
+        if (lane == 63) tmp[wave] = inc;
+        __syncthreads();
+        uint32_t base = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t x = tmp[w];
+            base += (uint32_t)w < wave ? x : 0u;
+            tot += x;
+        }
+        __syncthreads();
+        uint32_t run = carry + base + inc - s;
+#pragma unroll
+        for (int k = 0; k < kRsScanIpt; ++k) {
+            if (i0 + k < ntiles) row[i0 + k] = run;
+            run += v[k];
+        }
+        carry += tot;
     }
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
@@ -295,7 +323,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
         if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
             rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
-        rts_scan_kernel<<<plan.mask[p] + 1, 256, 0, st>>>(C, tiles, totals);
+        rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
         rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
                                                           totals, tiles, p + 1 == plan.passes ? ranges : nullptr,
                                                           bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev);
