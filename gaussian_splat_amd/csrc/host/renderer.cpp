@@ -453,11 +453,15 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     };
     uint32_t cap = reserve_pairs(h->order.frame_pairs);
     if (!cap) return fail(GS_ERR_OOM, "pair buffers");
-    // index order: the duplicate counts the first sort pass's digits itself
+    // index order: the duplicate counts the first sort pass's digits itself,
+    // when a duplicate block's pairs (estimated from the last frame's P) fit
+    // its LDS count tiles; beyond them counts go to contended global atomics
     const gs::SortPlan plan = gs::make_sort_plan(bits);
-    auto pass_counts = [&]() {
+    auto pass_counts = [&](uint64_t p_est) {
         gs::PassCounts pc;
-        if (!order && plan.passes > 0) {
+        const double per_block = (double)p_est * gs::kScanItems / (double)std::max<uint32_t>(m, 1);
+        if (!order && plan.passes > 0 &&
+            per_block <= (double)(gs::kDupCountTiles - 1) * gs::radix_sort_tile_items()) {
             pc.C = h->sort_scratch.as<uint32_t>();
             pc.tile = gs::radix_sort_tile_items();
             pc.mask = plan.mask[0];
@@ -465,7 +469,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         }
         return pc;
     };
-    gs::PassCounts pc = pass_counts();
+    gs::PassCounts pc = pass_counts(h->order.frame_pairs);
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                         h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
                                         h->npairs.as<uint32_t>(), cap, pc.C, pc.C ? (pc.mask + 1) * pc.ntiles : 0u,
@@ -503,7 +507,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (!(cap = reserve_pairs(P))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
-        pc = pass_counts();
+        pc = pass_counts(P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         GS_HIP(enqueue_lists());
     }

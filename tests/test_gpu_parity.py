@@ -413,25 +413,33 @@ def test_pair_count_growth(built, binning):
 
 
 def test_large_splats_bin_first(built):
-    """Large splats: a duplicate block's 4096 splats emit far more pairs than
-    its LDS digit counts cover (4 sort tiles of 6144 pairs), so the first
-    sort pass's counts also go through the global-atomic path; bin-first
-    and depth-first frames stay identical."""
+    """One duplicate block (4096 splats in index order) of large splats among
+    small ones: the block's pairs span more sort tiles than its LDS digit
+    counts cover, so the first sort pass's counts also go through the
+    global-atomic path (the average per block keeps the fused counts on).
+    Bin-first frames, first and repeated, equal the depth-first frame."""
     from gaussian_splat_amd import InstancedSplatRenderer, Options
     from gaussian_splat_amd import scene as S
-    raw = S.synthetic_raw(40000, seed=77, aspect=16 / 9)
-    raw.log_scale += np.float32(np.log(12.0))
-    sc = S.activate(raw, 0)
     W, H = 960, 540
-    outs = {}
-    for b in ("depth_first", "bin_first"):
-        r = InstancedSplatRenderer(sc, Options(sh_degree=0, binning=b))
+    v, p = orbit_views(W, H, 1)[0]
+
+    def frame(raw, binning, repeat=1):
+        r = InstancedSplatRenderer(S.activate(raw, 0), Options(sh_degree=0, binning=binning))
         r.initialize(0)
-        v, p = orbit_views(W, H, 1)[0]
-        outs[b] = r.render_host(v, p, W, H)
-        st = r.last_stats()
-    assert st["pairs"] / 40000 * 4096 > 4 * 6144, st["pairs"]  # pairs per duplicate block
-    assert _compare(outs["bin_first"], outs["depth_first"]) == (0.0, 0)
+        for _ in range(repeat):
+            img = r.render_host(v, p, W, H)
+        return img, r.last_stats()["pairs"]
+
+    base = S.synthetic_raw(40960, seed=77, aspect=16 / 9)
+    _, p0 = frame(base, "depth_first")
+    raw = S.synthetic_raw(40960, seed=77, aspect=16 / 9)
+    raw.log_scale[8192:12288] += np.float32(np.log(14.0))
+    ref, p1 = frame(raw, "depth_first")
+    assert p1 - p0 > 4 * 6144, (p0, p1)            # the large block's extra pairs: > 4 sort tiles
+    assert p1 / 10 <= 3 * 6144, p1                 # average per block: fused counts stay on
+    img, pb = frame(raw, "bin_first", repeat=2)    # (frame 2: P known, no re-queue)
+    assert pb == p1
+    assert _compare(img, ref) == (0.0, 0)
 
 
 @pytest.mark.parametrize("n,bits", [(0, 8), (1, 8), (4095, 13), (4096, 16), (4097, 20), (100000, 28),
