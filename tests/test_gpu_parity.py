@@ -231,6 +231,35 @@ def test_stage_timing_modes(built):
                                                    "composite"))
 
 
+def test_frames_in_flight_empty_frames_user_stream(built):
+    """frames_in_flight 2 on a user (non-null) stream, with empty frames (camera
+    facing away, no pairs) between normal ones: every output equals the
+    single-stream render, and the empty frames are the clear colour."""
+    import torch
+    from gaussian_splat_amd.api import default_camera
+    W, H = 480, 270
+    sc = _scene(30000, seed=72, sh=1, aspect=W / H)
+    views = orbit_views(W, H, 2)
+    cam = default_camera(W, H)
+    cam.setTarget(2 * cam.position - cam.target)  # the scene is behind the camera
+    views.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
+    r1 = _renderer(sc, sh=1)
+    refs = [r1.render_host(V, P, W, H) for V, P in views]
+    assert r1.last_stats()["pairs"] == 0
+    r2 = _renderer(sc, sh=1)
+    r2.set_frames_in_flight(2)
+    seq = [0, 2, 1, 2, 2, 0, 1]
+    stream = torch.cuda.Stream()
+    outs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in seq]
+    with torch.cuda.stream(stream):
+        for k, v in enumerate(seq):
+            r2.render(*views[v], W, H, out=outs[k], stream=stream.cuda_stream)
+    stream.synchronize()
+    for k, v in enumerate(seq):
+        assert _compare(outs[k].cpu().numpy(), refs[v]) == (0.0, 0), k
+    assert not np.any(refs[2][..., 3])  # nothing drawn
+
+
 def test_frames_in_flight_bitexact(built):
     """frames_in_flight 2: a frame's projection/sort runs on the handle's side
     stream while the previous frame composites; every output equals the
