@@ -226,6 +226,20 @@ def main():
     if timing == 2:  # kernel times of the timed frames (last <= 64)
         pre, comp = rh.kernel_times(args.steps)
         timed = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
+    # pipelined frames overlap the composite of frame k with the projection of
+    # frame k+1, so their kernel durations include the co-running kernel: the
+    # roofline takes the standalone kernels from extra unpipelined frames,
+    # timed by the same dispatch-packet events
+    standalone = {}
+    if timing == 2 and pipelined:
+        rh.set_frames_in_flight(1)
+        n_sa = min(max(args.steps, 3), 10)
+        for _ in range(n_sa):
+            step()
+        torch.cuda.synchronize()
+        pre, comp = rh.kernel_times(n_sa)
+        standalone = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
+        rh.set_frames_in_flight(args.frames_in_flight)
     # full stage breakdown: extra untimed frames, an event between every stage
     st = {}
     if not args.no_stage_timing:
@@ -243,11 +257,10 @@ def main():
             dom = max((k for k in st if k != "exchange"), key=lambda k: st[k]["ms"])
             d = st[dom]
             kms, src = d["ms"], "stage events, extra untimed frames"
-            if pipelined:
-                # pipelined frames run the composite of frame k beside the
-                # projection of frame k+1, so their kernel durations include
-                # the co-running kernel: the roofline takes the standalone
-                # kernel from the stage-timed frames, which run unpipelined
+            if pipelined and dom in standalone:
+                kms = standalone[dom]
+                src = f"dispatch-packet events, {n_sa} extra unpipelined frames (standalone kernel)"
+            elif pipelined:
                 src = "stage events, extra untimed unpipelined frames (standalone kernel)"
             elif dom in timed:
                 kms, src = timed[dom], f"dispatch-packet events, {min(args.steps, 64)} timed frames"
@@ -273,6 +286,7 @@ def main():
             "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
             "timed_kernel_ms": {k: round(v, 4) for k, v in timed.items()},
+            "standalone_kernel_ms": {k: round(v, 4) for k, v in standalone.items()},
             "timed_kernel_note": ("timed frames, preprocess of frame k+1 co-running with the composite of frame k"
                                   if pipelined else "timed frames"),
         }
