@@ -1,36 +1,50 @@
 #!/usr/bin/env python3
-"""Benchmark: Msplats/s of the full frame (preprocess -> depth sort -> scan ->
-duplicate -> bin sort -> ranges -> composite [-> exchange -> gather]) on
-BASELINE.json's headline workload: 6M-splat scene @ 1920x1080, SH degree 3
-(configs[2]; a seeded synthetic scene with 3DGS statistics — no garden .ply
-exists offline).  Inputs are resident in HBM before the timed region.
+"""Benchmark: Msplats/s of the full frame (preprocess -> sort/binning ->
+composite [-> exchange -> gather / reduce]) and the frame's achieved HBM GB/s,
+on BASELINE.json's workloads, inputs resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+  python bench.py [--gpus N --steps K --warmup W --config 1080p|4k|50m|1m]
 
-Multi-GPU is weak scaling: every rank holds its own 6M-splat shard of a
-(6M x N)-splat scene and owns 1/N of the tile rows; value = all splats / frame
-time (max over ranks).  Prints one JSON line on rank 0.
+Workloads (seeded synthetic scenes with 3DGS statistics; the garden .ply
+does not exist offline):
+  1080p (default)  BASELINE config 3: 6M-splat scene @1920x1080, SH degree 3
+  4k               BASELINE config 4: the same scene @3840x2160
+  50m              BASELINE config 5: 50M-splat stress scene @3840x2160, SH 0
+  1m               BASELINE config 2: 1M splats @1920x1080, SH 0
+
+Multi-GPU is STRONG scaling over one global scene: `--gpus N` (without
+torchrun) starts N rank processes itself (torch.distributed.run, one rank per
+GPU, 127.0.0.1) before anything touches a GPU; under torchrun WORLD_SIZE must
+equal --gpus.  Rank r renders the splat-index shard [r*N/g, (r+1)*N/g) of the
+global scene (generated chunk-wise, so a rank builds only its shard), value =
+global splats / frame time (max over ranks).  Both multi-GPU schemes run
+(--scheme both): "rows" (bin-row ownership + all_to_all + band gather; the
+frame is bit-identical to one GPU's) gives `value`; "slabs" (the north star's
+depth slabs + transmittance all_gather + RGBA reduce; approximate, DESIGN.md
+§6b) is reported beside it.
 
 At N=1 the line also carries
-  roofline      the slowest stage's algorithmic bytes / its average kernel
-                time; for preprocess / composite that time comes from HIP
-                events carried in the kernels' own dispatch packets over the
-                K timed frames (stage_timing 2: no extra packets, no syncs);
-                the full per-stage table ("stages") comes from a few extra
-                untimed frames with an event between every stage
-                and `traffic`: its HBM bytes per launch from two rocprofv3
-                PMC passes (FETCH_SIZE, WRITE_SIZE) run as child processes
-                (FETCH_SIZE doubled: gfx950 tallies 128-B reads at 64 B,
-                MI355X_MICROARCH.md §HBM); null if rocprofv3 is unavailable
-  cpu_baseline  the CPU oracle (oracle/gs_oracle.c, OpenMP) on the same
-                scene and camera, repeated for >= --cpu-seconds
+  roofline      the dominant kernel's algorithmic bytes / its standalone
+                duration (HIP events in its own dispatch packet, extra
+                unpipelined frames), and `kernels`: preprocess and composite
+                (the north star's kernel) always, each with its HBM fraction
+                (composite bytes from the records its workgroups actually
+                fetched, early-out included), PMC traffic (rocprofv3
+                FETCH_SIZE x 2 + WRITE_SIZE per launch, MI355X_MICROARCH.md
+                §HBM) and VALU-issue fraction (SQ_INSTS_VALU x 2 cycles per
+                wave64 instruction over 1024 SIMDs at 2.4 GHz)
+  cpu_baseline  the CPU oracle (oracle/gs_oracle.c, OpenMP) on the same scene
+                and camera on all host threads, and on 1 thread over a
+                bounded subset (cpu_baseline_1core)
+Prints one JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -40,31 +54,66 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TOPS = 78.6     # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s (fp32 non-FMA)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SIMDS = 1024                 # 256 CUs x 4 SIMD-32
+CLOCK_HZ = 2.4e9             # peak engine clock
+VALU_ISSUE_CYC = 2           # cycles per wave64 VALU instruction per SIMD, waves interleaved (MI355X_MICROARCH.md:54)
+
+CONFIGS = {
+    "1080p": dict(splats=6_000_000, width=1920, height=1080, sh=3, seed=2,
+                  label="BASELINE config 3: 6M-splat scene @1920x1080, SH3"),
+    "4k": dict(splats=6_000_000, width=3840, height=2160, sh=3, seed=2,
+               label="BASELINE config 4: 6M-splat scene @3840x2160, SH3"),
+    "50m": dict(splats=50_000_000, width=3840, height=2160, sh=0, seed=4,
+                label="BASELINE config 5: 50M-splat stress scene @3840x2160, SH0"),
+    "1m": dict(splats=1_000_000, width=1920, height=1080, sh=0, seed=1,
+               label="BASELINE config 2: 1M-splat scene @1920x1080, SH0"),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--splats", type=int, default=6_000_000, help="splats per GPU")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--sh", type=int, default=3)
+    ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
+    ap.add_argument("--splats", type=int, default=0, help="global splats (0 = the config's)")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--sh", type=int, default=-1)
+    ap.add_argument("--seed", type=int, default=-1)
+    ap.add_argument("--profile", default="uniform", choices=["uniform", "heavy"],
+                    help="scale distribution: uniform 3DGS statistics or the heavy-tailed stress variant")
     ap.add_argument("--mode", default="tile")
-    ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=0, help="splats in the CPU baseline sample (0 = all)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU baseline duration")
-    ap.add_argument("--traffic", type=int, default=1, help="measure roofline.traffic with rocprofv3 PMC (N=1)")
+    ap.add_argument("--pmc", type=int, default=1, help="N=1: rocprofv3 PMC passes (traffic, VALU instructions)")
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="N=1: 2 = a frame's projection/sort overlaps the previous frame's composite")
-    ap.add_argument("--scheme", default="rows", choices=["rows", "slabs"],
-                    help="N>1: bin-row ownership (bit-exact, default) or depth slabs + RGBA reduce (DESIGN.md §6b)")
-    return ap.parse_args()
+    ap.add_argument("--scheme", default="both", choices=["rows", "slabs", "both"],
+                    help="N>1: bin-row ownership (exact; value), depth slabs + RGBA reduce, or both")
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    a.splats = a.splats or c["splats"]
+    a.width = a.width or c["width"]
+    a.height = a.height or c["height"]
+    a.sh = c["sh"] if a.sh < 0 else a.sh
+    a.seed = c["seed"] if a.seed < 0 else a.seed
+    a.label = c["label"] if (a.splats, a.width, a.height, a.sh) == (c["splats"], c["width"], c["height"], c["sh"]) \
+        else f"{a.splats} splats @{a.width}x{a.height}, SH{a.sh}"
+    return a
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N outside torchrun: one rank process per GPU (the parent never
+    touches a GPU), the driver's own launch line; returns their exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def stage_summary(stats_list):
@@ -80,79 +129,96 @@ def stage_summary(stats_list):
     return out
 
 
-def cpu_baseline(scene, view, proj, w, h, sh, sample, seconds):
+def cpu_baseline(scene, view, proj, w, h, sh, threads, seconds, max_frames=50):
     from oracle import oracle_py as O
 
-    n = scene.n if sample <= 0 else min(sample, scene.n)
-    sub = scene if n == scene.n else scene.subset(slice(0, n))
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    O.render(sub.subset(slice(0, min(n, 20000))), view, proj, w, h, sh_degree=sh, nthreads=threads)  # warm
+    O.render(scene.subset(slice(0, min(scene.n, 20000))), view, proj, w, h, sh_degree=sh, nthreads=threads)  # warm
     frames, t0 = 0, time.perf_counter()
     while True:
-        O.render(sub, view, proj, w, h, sh_degree=sh, nthreads=threads)
+        O.render(scene, view, proj, w, h, sh_degree=sh, nthreads=threads)
         frames += 1
         dt = time.perf_counter() - t0
-        if dt >= seconds or frames >= 50:
+        if dt >= seconds or frames >= max_frames:
             break
-    return {"value": round(n * frames / dt / 1e6, 3), "unit": "Msplats/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} x one {w}x{h} SH{sh} frame of {n} splats of the same scene and camera "
-                      f"(oracle/gs_oracle.c, OpenMP, {threads} threads), {dt:.1f} s"}
+    return {"value": round(scene.n * frames / dt / 1e6, 3), "unit": "Msplats/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} x one {w}x{h} SH{sh} frame of {scene.n} splats of the same scene and camera "
+                      f"(oracle/gs_oracle.c, OpenMP, {threads} thread{'s' if threads > 1 else ''}), {dt:.1f} s"}
 
 
-STAGE_KERNEL = {"preprocess": "preprocess_kernel", "depth_sort": "rts_pass_kernel<3>", "scan": "scan_reduce_kernel",
-                "duplicate": "scan_duplicate_kernel", "sort": "rts_pass_kernel<1>", "ranges": "rts_pass_kernel<1>",
-                "composite": "composite_kernel"}
+KERNEL_NAME = {"preprocess": "preprocess_kernel", "composite": "composite_kernel"}
 
 
-def pmc_traffic(args, kernel):
-    """HBM bytes per launch of `kernel`: two rocprofv3 --pmc passes over a
-    short run of this benchmark in child processes (counters and traces are
-    never combined; each pass its own process)."""
+def pmc_passes(args):
+    """Per-launch PMC means of the preprocess and composite kernels: one
+    rocprofv3 --kernel-trace --pmc child process per counter group (counters
+    never combined with traces of other domains)."""
     import csv
     import shutil
-    import subprocess
     import tempfile
 
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not found"
     bench = [sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--cpu-baseline", "0",
-             "--traffic", "0", "--no-stage-timing", "--splats", str(args.splats), "--width", str(args.width),
-             "--height", str(args.height), "--sh", str(args.sh), "--mode", args.mode, "--seed", str(args.seed)]
+             "--pmc", "0", "--no-stage-timing", "--frames-in-flight", "1", "--splats", str(args.splats),
+             "--width", str(args.width), "--height", str(args.height), "--sh", str(args.sh), "--mode", args.mode,
+             "--seed", str(args.seed), "--profile", args.profile]
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
-    kb = {}
+    out = {k: {} for k in KERNEL_NAME}
     with tempfile.TemporaryDirectory(dir=env["TMPDIR"]) as td:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            out = Path(td) / ctr
-            cmd = [exe, "--kernel-trace", "--pmc", ctr, "-d", str(out), "-o", "run", "--output-format", "csv",
+        for grp in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_WAVES"]):
+            d = Path(td) / grp[0]
+            cmd = [exe, "--kernel-trace", "--pmc", *grp, "-d", str(d), "-o", "run", "--output-format", "csv",
                    "--"] + bench
             try:
                 p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300, env=env,
                                    cwd=str(ROOT))
             except subprocess.TimeoutExpired:
-                return None, f"rocprofv3 {ctr} timed out"
+                return None, f"rocprofv3 {grp} timed out"
             if p.returncode != 0:
-                return None, f"rocprofv3 {ctr} exited {p.returncode}"
-            vals = []
-            for f in out.rglob("*counter_collection.csv"):
+                return None, f"rocprofv3 {grp} exited {p.returncode}"
+            vals = {(k, c): [] for k in KERNEL_NAME for c in grp}
+            for f in d.rglob("*counter_collection.csv"):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                            vals.append(float(row["Counter_Value"]))
-            if not vals:
-                return None, f"no {ctr} samples for {kernel}"
-            kb[ctr] = sum(vals) / len(vals)
-    return 1024.0 * (2.0 * kb["FETCH_SIZE"] + kb["WRITE_SIZE"]), None
+                        for k, kn in KERNEL_NAME.items():
+                            if kn in row.get("Kernel_Name", "") and row.get("Counter_Name") in grp:
+                                vals[(k, row["Counter_Name"])].append(float(row["Counter_Value"]))
+            for (k, c), v in vals.items():
+                if v:
+                    out[k][c] = sum(v) / len(v)
+    for k, cs in out.items():
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:  # KB; FETCH_SIZE counts 128-B reads at 64 B on gfx950
+            cs["traffic"] = 1024.0 * (2.0 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"])
+    return out, None
+
+
+def kernel_entry(ms, nbytes, pmc):
+    e = {"ms": round(ms, 4), "bytes": int(nbytes), "hbm_gbs": round(nbytes / (ms * 1e6), 1) if ms > 0 else 0.0,
+         "hbm_frac": round(nbytes / (ms * 1e6) / HBM_PEAK_GBS, 4) if ms > 0 else 0.0, "traffic": None}
+    if pmc:
+        if "traffic" in pmc:
+            e["traffic"] = int(pmc["traffic"])
+        if "SQ_INSTS_VALU" in pmc and ms > 0:
+            e["valu_insts"] = int(pmc["SQ_INSTS_VALU"])
+            e["valu_issue_frac"] = round(pmc["SQ_INSTS_VALU"] * VALU_ISSUE_CYC / (SIMDS * CLOCK_HZ * ms * 1e-3), 4)
+    return e
 
 
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal knobs for a 1-GPU box (never set by the driver): every rank on
     # device 0, collectives over gloo staged through host memory.
     backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
@@ -168,139 +234,150 @@ def main():
 
     from gaussian_splat_amd import scene as S
     from gaussian_splat_amd.api import InstancedSplatRenderer, Options, default_camera
+    from gaussian_splat_amd.distributed import shard_bounds
 
-    W, H = args.width, args.height
-    # each rank generates its own shard (distinct seeds): weak scaling
-    scene = S.synthetic_scene(args.splats, seed=args.seed + 1000 * rank, sh_degree=args.sh, aspect=W / H)
+    W, H, N = args.width, args.height, args.splats
+    b, e = shard_bounds(N, world, rank)
+    # this rank's shard of the global scene (generated chunk-wise: the same
+    # splats whichever rank builds them)
+    scene = S.activate(S.synthetic_raw(N, seed=args.seed, aspect=W / H, rest=args.sh > 0, profile=args.profile,
+                                       start=b, stop=e), args.sh)
     cam = default_camera(W, H)
     view, proj = cam.getViewMatrix(), cam.getProjectionMatrix()
     timing = 0 if args.no_stage_timing else 2  # timed frames: dispatch-packet events only
     opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=timing,
                    frames_in_flight=args.frames_in_flight if world == 1 else 1)
 
+    def timed(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt * 1e3 / steps
+
+    schemes = {}
     if world == 1:
         r = InstancedSplatRenderer(scene, opts)
         r.initialize(local)
         out = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
         step = lambda: r.render(view, proj, W, H, out=out)
         rh = r
+        ms = timed(step, args.steps, args.warmup)
     else:
         from gaussian_splat_amd.distributed import HipShardBackend, HipSlabBackend, ShardedRenderer, SlabRenderer
 
-        if args.scheme == "slabs":
-            be = HipSlabBackend(scene, rank, world, rank * args.splats, opts, local)
-            sr = SlabRenderer(be, rank, world)
-        else:
-            be = HipShardBackend(scene, rank, world, rank * args.splats, opts, local)
-            sr = ShardedRenderer(be, rank, world)
-        step = lambda: sr.render(view, proj, W, H, gather=True)
-        rh = be.r
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    ms = dt * 1e3 / args.steps
-    total_splats = args.splats * world
-    value = total_splats / (ms * 1e-3) / 1e6
+        order = ["rows", "slabs"] if args.scheme == "both" else [args.scheme]
+        for sch in order:
+            if sch == "slabs":
+                be = HipSlabBackend(scene, rank, world, b, opts, local)
+                sr = SlabRenderer(be, rank, world)
+            else:
+                be = HipShardBackend(scene, rank, world, b, opts, local)
+                sr = ShardedRenderer(be, rank, world)
+            stp = (lambda s_=sr: s_.render(view, proj, W, H, gather=True))
+            schemes[sch] = {"ms": timed(stp, args.steps, args.warmup), "handle": be.r, "step": stp}
+        head = "rows" if "rows" in schemes else order[0]
+        ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
+    value = N / (ms * 1e-3) / 1e6
 
     s0 = rh.last_stats()
-    # the order the timed frames built their bin lists in (the default picks
-    # it per frame from the previous frame's pair count)
     binning = {1: "depth-first", 2: "bin-first"}.get(int(s0.get("binning", 0)), "?")
-    timed = {}
     pipelined = world == 1 and args.frames_in_flight >= 2
+    timed_k = {}
     if timing == 2:  # kernel times of the timed frames (last <= 64)
         pre, comp = rh.kernel_times(args.steps)
-        timed = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
-    # pipelined frames overlap the composite of frame k with the projection of
-    # frame k+1, so their kernel durations include the co-running kernel: the
-    # roofline takes the standalone kernels from extra unpipelined frames,
+        timed_k = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
+    # standalone kernels (the roofline's timing): extra unpipelined frames
     # timed by the same dispatch-packet events
-    standalone = {}
-    if timing == 2 and pipelined:
-        rh.set_frames_in_flight(1)
-        n_sa = min(max(args.steps, 3), 10)
+    standalone, n_sa = {}, min(max(args.steps, 3), 10)
+    if timing == 2:
+        if pipelined:
+            rh.set_frames_in_flight(1)
         for _ in range(n_sa):
             step()
         torch.cuda.synchronize()
         pre, comp = rh.kernel_times(n_sa)
         standalone = {"preprocess": float(np.mean(pre)), "composite": float(np.mean(comp))} if len(pre) else {}
-        rh.set_frames_in_flight(args.frames_in_flight)
+        sa_stats = rh.last_stats()  # (records the composite fetched in such a frame)
+        if pipelined:
+            rh.set_frames_in_flight(args.frames_in_flight)
     # full stage breakdown: extra untimed frames, an event between every stage
     st = {}
     if not args.no_stage_timing:
         rh.set_stage_timing(1)
         stats = []
-        for _ in range(min(max(args.steps, 3), 10)):
+        for _ in range(n_sa):
             step()
             stats.append(rh.last_stats())
         st = stage_summary(stats)
+        rh.set_stage_timing(timing)
 
     line = None
     if rank == 0:
-        rl = None
-        if st:
-            dom = max((k for k in st if k != "exchange"), key=lambda k: st[k]["ms"])
-            d = st[dom]
-            kms, src = d["ms"], "stage events, extra untimed frames"
-            if pipelined and dom in standalone:
-                kms = standalone[dom]
-                src = f"dispatch-packet events, {n_sa} extra unpipelined frames (standalone kernel)"
-            elif pipelined:
-                src = "stage events, extra untimed unpipelined frames (standalone kernel)"
-            elif dom in timed:
-                kms, src = timed[dom], f"dispatch-packet events, {min(args.steps, 64)} timed frames"
-            gbs = d["bytes"] / (kms * 1e6)
-            rl = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                  "kernel_ms": round(kms, 4), "bytes": int(d["bytes"]), "timing": src}
+        frame_bytes = sum(v["bytes"] for k, v in st.items() if k != "exchange") if st else 0.0
         line = {
-            "metric": "Msplats/sec (6M-splat scene @1080p, SH3, full frame)",
+            "metric": "Msplats/sec + achieved HBM GB/s (6M-splat scene @1080p, SH3, full frame)"
+            if args.config == "1080p" else f"Msplats/sec + achieved HBM GB/s ({args.label})",
             "value": round(value, 2), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded 3DGS-statistics scene; no garden .ply offline)",
-            "config": {"workload": f"{args.splats} splats/GPU @ {W}x{H}, SH{args.sh}, {args.mode} contract",
-                       "global_splats": total_splats, "width": W, "height": H, "sh_degree": args.sh,
-                       "parallelism": (f"splat-shard x{world}, 32-px bin-row ownership, all_to_all + gather, {backend}"
-                                       if args.scheme == "rows" else
-                                       f"splat-shard x{world}, depth slabs, all_to_all + T all_gather + RGBA "
-                                       f"reduce, {backend}") if world > 1 else
-                                      ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the "
-                                       "composite of frame k)" if args.frames_in_flight == 2 else "single GPU"),
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)",
+            "hbm_gbs": round(frame_bytes / (ms * 1e6), 1) if frame_bytes else None,
+            "config": {"workload": args.label, "global_splats": N, "width": W, "height": H, "sh_degree": args.sh,
+                       "parallelism": (f"{world} ranks, splat-index shards of one global scene; rows: 32-px bin-row "
+                                       f"ownership, all_to_all + band gather ({backend}, world {world})")
+                       if world > 1 else
+                       ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the composite of frame k)"
+                        if args.frames_in_flight == 2 else "single GPU"),
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning},
-            "roofline": rl,
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
-            "timed_kernel_ms": {k: round(v, 4) for k, v in timed.items()},
+            "timed_kernel_ms": {k: round(v, 4) for k, v in timed_k.items()},
             "standalone_kernel_ms": {k: round(v, 4) for k, v in standalone.items()},
-            "timed_kernel_note": ("timed frames, preprocess of frame k+1 co-running with the composite of frame k"
-                                  if pipelined else "timed frames"),
         }
-        if world == 1 and rl is not None and args.traffic:
-            kern = STAGE_KERNEL[rl["kernel"]]
-            if rl["kernel"] == "depth_sort" and binning == "bin-first":
-                kern = "bin_depth_sort_kernel"
-            traffic, why = pmc_traffic(args, kern)
-            rl["traffic"] = round(traffic) if traffic is not None else None
+        if world > 1:
+            line["comm"] = {"backend": dist.get_backend(), "ranks": dist.get_world_size()}
+            line["schemes"] = {k: {"ms_per_step": round(v["ms"], 4), "value": round(N / (v["ms"] * 1e-3) / 1e6, 2)}
+                               for k, v in schemes.items()}
+            if "slabs" in line["schemes"]:
+                line["schemes"]["slabs"]["note"] = ("depth slabs + transmittance all_gather + RGBA reduce "
+                                                    "(approximate: reassociated transmittance product)")
+        if st and standalone:
+            pmc, why = (pmc_passes(args) if (world == 1 and args.pmc) else (None, "pmc off"))
+            kern = {}
+            for k in ("preprocess", "composite"):
+                nbytes = sa_stats[f"bytes_{k}"]
+                kern[k] = kernel_entry(standalone[k], nbytes, (pmc or {}).get(k))
+            kern["composite"]["records_fetched"] = int(sa_stats["records_fetched"])
+            kern["composite"]["pairs"] = int(sa_stats["pairs"])
+            dom = max(kern, key=lambda k: kern[k]["ms"])
+            d = kern[dom]
+            line["roofline"] = {"bound": "hbm", "achieved": d["hbm_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": d["hbm_frac"], "traffic": d["traffic"], "kernel": dom, "kernel_ms": d["ms"],
+                                "bytes": d["bytes"], "valu_issue_frac": d.get("valu_issue_frac"),
+                                "timing": f"dispatch-packet events, {n_sa} extra unpipelined frames "
+                                          "(standalone kernel)",
+                                "kernels": kern}
             if why:
-                rl["traffic_note"] = why
+                line["roofline"]["pmc_note"] = why
         if world == 1 and args.cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(scene, view, proj, W, H, args.sh, args.cpu_sample,
-                                                args.cpu_seconds)
+            threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+            line["cpu_baseline"] = cpu_baseline(scene, view, proj, W, H, args.sh, threads, args.cpu_seconds)
+            sub = scene.subset(slice(0, min(scene.n, max(scene.n // 8, 1))))
+            line["cpu_baseline_1core"] = cpu_baseline(sub, view, proj, W, H, args.sh, 1, args.cpu_seconds,
+                                                      max_frames=20)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -36,7 +36,7 @@ class GsStats(C.Structure):
                 ("bytes_preprocess", C.c_int64), ("bytes_scan", C.c_int64), ("bytes_duplicate", C.c_int64),
                 ("bytes_sort", C.c_int64), ("bytes_ranges", C.c_int64), ("bytes_composite", C.c_int64),
                 ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
-                ("binning", C.c_int32), ("reserved_stats", C.c_int32)]
+                ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -106,6 +106,9 @@ struct gs_handle {
     bool bin_first_frame = false;       // the last frame used the bin-first order
     DevBuf seg_sample;                  // per-bin depth sort sample (launch_bin_depth_sort)
     DevBuf npairs;                      // P on the device (0 when it overflows the pair buffers)
+    DevBuf fetch;                       // per buffer set: records the composite fetched (u64)
+    int stats_set = -1;                 // buffer set of the frame in `stats` (its fetch counter)
+    int64_t stats_fixed_bytes = 0;      // composite bytes besides the records: range words + output
     hipEvent_t totals_ev = nullptr;     // P is in host_total
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
         int32_t w = 0, h = 0;
@@ -147,7 +150,7 @@ struct gs_handle {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
-                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs})
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -287,7 +290,7 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
     if (env && std::strcmp(env, "depth") == 0) b = GS_BINNING_DEPTH_FIRST;
     if (env && std::strcmp(env, "bin") == 0) b = GS_BINNING_BIN_FIRST;
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    if (b == GS_BINNING_DEPTH_FIRST || bits_for(T) + gs::kDepthBits > 32) return false;
+    if (b == GS_BINNING_DEPTH_FIRST || std::max(bits_for(T), 1) + gs::kDepthBits > 32) return false;
     if (b == GS_BINNING_BIN_FIRST) return true;
     auto& o = h->order;
     if (o.w != U.width || o.h != U.height) {  // new history
@@ -327,6 +330,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 16));
     }
     GS_HIP(h->npairs.reserve(4));
+    GS_HIP(h->fetch.reserve(16));
     if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
@@ -355,6 +359,10 @@ float elapsed(gs_handle* h, int a, int b) {
     if (h->opt.stage_timing == 1 && h->events) (void)hipEventElapsedTime(&ms, h->ev[a], h->ev[b]);
     return ms;
 }
+
+// The frame's composite fetch counter (one per buffer set; the preprocess of
+// the frame clears it).
+unsigned long long* fetch_counter(gs_handle* h) { return h->fetch.as<unsigned long long>() + h->set; }
 
 hipEvent_t kernel_event(gs_handle* h, int k) {
     return h->opt.stage_timing == 2 && h->events ? h->kev[h->kev_slot][k] : nullptr;
@@ -434,7 +442,9 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
                           const uint32_t* carry_dkey = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    const int bits = bits_for(T);
+    // at least one key bit: the bin ranges are written by the last sort pass,
+    // so a single-bin frame (W, H <= 32) still needs one pass
+    const int bits = std::max(bits_for(T), 1);
     GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
     if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
     // pair capacity of this buffer set: at least the last frame's P
@@ -581,6 +591,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
         GS_HIP(handoff());
+        ca.fetched = fetch_counter(h);
         GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
         mark(h, 7, sc);
         h->stats.pairs = (int64_t)P;
@@ -617,6 +628,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             ca.t_out = slab_t;
         }
         GS_HIP(handoff());
+        ca.fetched = fetch_counter(h);
         GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
         if (slab_t) {
             h->slab_ca = ca;
@@ -660,6 +672,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.t_out = slab_t;
     }
     GS_HIP(handoff());
+    ca.fetched = fetch_counter(h);
     GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
     if (slab_t) {
         h->slab_ca = ca;
@@ -681,7 +694,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     const int64_t bin = 56 + (h->opt.sh_degree > 0 ? 4 * 3 * sh_coeffs(h->opt.sh_degree) : 0);
     // Algorithmic bytes: what each stage must move at minimum.
     const int64_t Pi = (int64_t)P, dpass = gs::make_sort_plan(gs::kDepthBits).passes;
-    s.bytes_preprocess = N * (bin + 48 + 8);
+    s.bytes_preprocess = N * (bin + 48 + 12);  // record, depth key, rect lo/hi
     // reduce-then-scan LSD: per pass the count kernel reads the keys (4 B)
     // and the scatter moves key + values (read + write); the depth sort's
     // first pass generates the index values instead of reading them
@@ -700,7 +713,12 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     }
     s.bytes_sort = Pi * 20 * (int64_t)s.sort_passes;
     s.bytes_ranges = 0;  // ranges come out of the last sort pass
-    s.bytes_composite = T * 8 + Pi * (4 + 48) + (int64_t)U.width * U.height * 16;
+    // upper bound until the fetch counter is read (gs_last_stats): every tile
+    // of a bin reads the whole list; the early-out stops that short
+    h->stats_fixed_bytes = 4 * T * 8 + (int64_t)U.width * U.height * 16;
+    h->stats_set = h->set;
+    s.bytes_composite = h->stats_fixed_bytes + 4 * Pi * (4 + 48);
+    s.records_fetched = -1;
     // stage_timing 2: read lazily (gs_last_stats / gs_kernel_times), so a
     // frame never waits for itself
     if (h->opt.stage_timing == 2 && h->events) {
@@ -929,7 +947,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     begin_frame(h, sp);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
-                                 kernel_event(h, 1)));
+                                 kernel_event(h, 1), fetch_counter(h)));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
@@ -943,7 +961,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         GS_HIP(hipStreamSynchronize(st));
     }
     fill_stats(h, P, U);
-    if (bgra8) h->stats.bytes_composite -= (int64_t)W * H * 12;
+    if (bgra8) {
+        h->stats.bytes_composite -= (int64_t)W * H * 12;
+        h->stats_fixed_bytes -= (int64_t)W * H * 12;
+    }
     return GS_OK;
 }
 
@@ -964,6 +985,14 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
                                  &h->stats.ms_total);
         if (s != GS_OK) return s;
         h->kev_pending = false;
+    }
+    if (h->stats_set >= 0 && h->stats.records_fetched < 0) {  // the last frame's composite fetch counter
+        unsigned long long v = 0;
+        GS_HIP(hipSetDevice(h->device));
+        GS_HIP(hipEventSynchronize(h->set_free[h->stats_set]));
+        GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + h->stats_set, 8, hipMemcpyDeviceToHost));
+        h->stats.records_fetched = (int64_t)v;
+        h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
     }
     *out = h->stats;
     return GS_OK;
@@ -1105,7 +1134,7 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     begin_frame(h, st);
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, *U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
-                                 kernel_event(h, 1)));
+                                 kernel_event(h, 1), fetch_counter(h)));
     mark(h, 1, st);
     return GS_OK;
 }
@@ -1271,6 +1300,7 @@ gs_status gs_slab_composite(gs_handle* h, const float* t_all, float* out_rgba, v
     ca.slab_rank = h->rank;
     ca.t_all = t_all;
     ca.t_out = nullptr;
+    ca.fetched = nullptr;  // (records_fetched counts the transmittance pass)
     ca.out = reinterpret_cast<float4*>(out_rgba);
     GS_HIP(gs::launch_composite(ca, h->opt.mode, static_cast<hipStream_t>(stream)));
     GS_HIP(hipEventRecord(h->set_free[h->set], static_cast<hipStream_t>(stream)));

@@ -292,8 +292,16 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     }
     if (lane == 0) GS_CC(0, 1);
     if (tid == 0) GS_CC(6, rg.y - rg.x);
+    // records this workgroup fetched: the first batch, then one prefetched
+    // batch per batch it composites (the early-out stops both)
+    const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;  // (empty bins: {~0, 0})
+    uint32_t fetched = len < (uint32_t)kTileThreads ? len : (uint32_t)kTileThreads;
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
         if (__syncthreads_count(!finished()) == 0) break;
+        if (rg.y - b > (uint32_t)kTileThreads) {
+            const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
+            fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
+        }
         if (tid == 0) GS_CC(5, 1);
         if (b + tid < rg.y) {
             s0[tid] = r0;
@@ -409,6 +417,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         }
 #endif
     }
+    if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
     if (!inside) return;
     if constexpr (SLAB == 1) {
         a.t_out[(size_t)py * width + px] = MODE == 0 ? 1.0f - A : T;
@@ -446,7 +455,11 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
                               hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
     const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
-    if (nwg == 0) return hipSuccess;
+    if (nwg == 0) {  // no owned tiles: the timing events still mark the (empty) stage
+        if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
+        if (t1 && hipEventRecord(t1, st) != hipSuccess) return hipGetLastError();
+        return hipSuccess;
+    }
     // t0/t1 (optional) are recorded by the dispatch packet itself
     hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
                           nwg);

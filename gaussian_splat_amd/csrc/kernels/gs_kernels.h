@@ -14,9 +14,12 @@ namespace gs {
 // pixel rect (empty rect for culled splats).
 // t0/t1: optional events recorded by the kernel's own dispatch (timing
 // without extra packets).
+// zero8 (optional): a 64-bit word the kernel clears (the frame's composite
+// fetch counter, CompositeArgs::fetched), so no memset dispatch is needed.
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
-                             hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+                             hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr,
+                             unsigned long long* zero8 = nullptr);
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
@@ -137,6 +140,10 @@ struct CompositeArgs {
     int slab_rank;
     float* t_out;
     const float* t_all;
+    // optional: += the records the workgroups fetched (staged batches and the
+    // prefetched one; each of a bin's four tiles fetches its list itself),
+    // the early-out-aware basis of the composite's algorithmic bytes
+    unsigned long long* fetched;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals

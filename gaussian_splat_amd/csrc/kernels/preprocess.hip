@@ -170,8 +170,10 @@ template <int DEG>
 __global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
-                                                         uint32_t* __restrict__ rect_hi) {
+                                                         uint32_t* __restrict__ rect_hi,
+                                                         unsigned long long* __restrict__ zero8) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i == 0 && zero8) *zero8 = 0ull;
     if (i >= s.n) return;
     const float* V = U.V;
     const float* VP = U.VP;
@@ -343,16 +345,22 @@ __global__ __launch_bounds__(256, 8) void preprocess_kernel(SceneDev s, const Fr
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
-                             hipEvent_t t1) {
-    if (s.n == 0) return hipSuccess;
+                             hipEvent_t t1, unsigned long long* zero8) {
+    if (s.n == 0) {
+        // no dispatch: the timing events still mark the (empty) stage
+        if (zero8 && hipMemsetAsync(zero8, 0, 8, st) != hipSuccess) return hipGetLastError();
+        if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
+        if (t1 && hipEventRecord(t1, st) != hipSuccess) return hipGetLastError();
+        return hipSuccess;
+    }
     dim3 grid((s.n + 255) / 256), block(256);
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
     switch (sh_degree) {
-    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
-    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi); break;
+    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
+    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
+    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
+    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

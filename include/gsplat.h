@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 3
+#define GSPLAT_ABI_VERSION 4
 
 typedef enum {
     GS_OK = 0,
@@ -110,6 +110,12 @@ typedef struct gs_stats {
                               (ms_depth_sort = global depth sort) or GS_BINNING_BIN_FIRST
                               (ms_depth_sort = per-bin depth sort after the bin sort) */
     int32_t reserved_stats;
+    /* records the composite's workgroups fetched (each of a 32-px bin's four
+       16x16 tiles reads the bin's list itself; a tile stops fetching once its
+       pixels saturate): the basis of bytes_composite = 8 B per workgroup +
+       52 B per fetched record + the framebuffer.  gs_last_stats waits for the
+       last frame's composite to read it. */
+    int64_t records_fetched;
 } gs_stats;
 
 typedef struct gs_handle gs_handle;

@@ -59,3 +59,27 @@ def orbit_views(width, height, n=3):
             cam.orbit(0.35 * k, 0.1 * k)
         out.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
     return out
+
+
+# Depth-slab scheme tolerance.  The slab scheme is labelled
+# approximate: the colour pass of slab k starts from the product of the
+# farther slabs' transmittance, which differs from the sequential A / T
+# recurrence by fp32 reassociation (measured <= 5e-6).  Where the sequential
+# A lands within that rounding of the 0.99 break (T of the 0.01 break), the
+# slab frame can stop one fragment earlier or later: a flipped break adds or
+# drops at most 1 - 0.99 = 0.01 of alpha (and of colour, rgb <= 1), plus the
+# rounding.  So: every pixel within SLAB_FLIP_BOUND, and at most
+# SLAB_FLIP_SHARE of the pixels (at least 2) beyond the north star's 1e-4.
+NORTH_STAR_TOL = 1e-4
+SLAB_FLIP_BOUND = 0.0101
+SLAB_FLIP_SHARE = 1e-5
+
+
+def check_slab_frame(frame, ref):
+    """Returns (pixels beyond 1e-4, max error) after asserting the bound above."""
+    diff = np.abs(np.asarray(frame, np.float64) - np.asarray(ref, np.float64)).max(axis=-1)
+    over = int((diff > NORTH_STAR_TOL).sum())
+    worst = float(diff.max()) if diff.size else 0.0
+    assert worst <= SLAB_FLIP_BOUND, f"slab frame error {worst} beyond the flipped-break bound"
+    assert over <= max(2, int(SLAB_FLIP_SHARE * diff.size)), f"{over} pixels beyond 1e-4 (max {worst})"
+    return over, worst

@@ -3,9 +3,10 @@ slab bounds (gs_slab_bounds, host code of the product library), the oracle's
 slab decomposition against its own full composite, and the gloo protocol
 (histogram all-reduce, record all-to-all, transmittance all-gather, RGBA
 reduce).  The decomposition reassociates the transmittance product, so the
-bar is the north star's 1e-4 per channel on all but a handful of pixels that
-sit on the A >= 0.99 / T < 0.01 break (each of those is bounded by one
-fragment's contribution); world 1 is bit-exact."""
+scheme is approximate: the bar is the north star's 1e-4 per channel on all
+but a handful of pixels whose A >= 0.99 / T < 0.01 break flips, each bounded
+by the 0.01 left at the break (conftest.check_slab_frame); world 1 is
+bit-exact."""
 import os
 import socket
 
@@ -13,6 +14,8 @@ import numpy as np
 import pytest
 
 from oracle import oracle_py as O
+
+from conftest import SLAB_FLIP_BOUND, SLAB_FLIP_SHARE, check_slab_frame
 
 TOL = 1e-4
 
@@ -70,8 +73,7 @@ def test_oracle_slab_decomposition(mode):
             frame += O.composite_slab(r, k, w, h, 2, rank=d, t_all=ts, mode=mode)
         if world == 1:
             np.testing.assert_array_equal(frame.view(np.uint32), full.view(np.uint32))
-        bad, linf, npx = _flips_ok(frame, full)
-        assert bad <= max(2, npx // 10000), f"world {world}: {bad} pixels beyond 1e-4 (max {linf})"
+        check_slab_frame(frame, full)
 
 
 def _free_port():
@@ -125,4 +127,5 @@ def test_gloo_slab_frame(world, mode):
         assert p.exitcode == 0
     same_shape, bad, linf, npx = res
     assert same_shape
-    assert bad <= max(2, npx // 10000), f"{bad} pixels beyond 1e-4 (max {linf})"
+    assert linf <= SLAB_FLIP_BOUND, f"slab frame error {linf} beyond the flipped-break bound"
+    assert bad <= max(2, int(SLAB_FLIP_SHARE * npx)), f"{bad} pixels beyond 1e-4 (max {linf})"
