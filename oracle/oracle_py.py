@@ -27,6 +27,12 @@ class OraScene(C.Structure):
                 ("opacity", C.c_void_p), ("color", C.c_void_p), ("sh_rest", C.c_void_p), ("sh_degree", C.c_int)]
 
 
+class OraDebug(C.Structure):
+    _fields_ = [("zf", C.c_float), ("a", C.c_float), ("b", C.c_float), ("c", C.c_float), ("r1", C.c_float),
+                ("r2", C.c_float), ("e1x", C.c_float), ("e1y", C.c_float), ("dkey", C.c_uint32),
+                ("ntiles", C.c_uint32), ("visible", C.c_int)]
+
+
 class OraOptions(C.Structure):
     _fields_ = [("mode", C.c_int), ("cap", C.c_int), ("nthreads", C.c_int)]
 
@@ -53,6 +59,8 @@ def lib() -> C.CDLL:
         L.ora_perspective.argtypes = [C.c_float] * 4 + [C.c_void_p]
         L.ora_mat4_mul.argtypes = [C.c_void_p] * 3
         L.ora_camera_position.argtypes = [C.c_void_p] * 2
+        L.ora_project.argtypes = [C.POINTER(OraScene), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_int, C.c_int, C.c_void_p, C.POINTER(OraDebug)]
         L.ora_project_all.argtypes = [C.POINTER(OraScene), C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_int]
         L.ora_render.argtypes = [C.POINTER(OraScene), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
@@ -148,6 +156,26 @@ def project(scene, view, proj, width, height, sh_degree=0, nthreads=0):
     lib().ora_project_all(C.byref(s), V.ctypes.data, P.ctypes.data, int(width), int(height), rec.ctypes.data,
                           dk.ctypes.data, nt.ctypes.data, int(nthreads))
     return rec, dk, nt
+
+
+def project_debug(scene, view, proj, width, height, sh_degree=0):
+    """Per-splat K1-K5 intermediates (ora_project): records and a dict of
+    arrays zf, a, b, c, r1, r2, e1x, e1y, dkey, ntiles, visible."""
+    s, keep = _scene(scene, sh_degree)
+    V, P = _col16(view), _col16(proj)
+    VP = np.zeros(16, np.float32)
+    cam = np.zeros(3, np.float32)
+    lib().ora_mat4_mul(P.ctypes.data, V.ctypes.data, VP.ctypes.data)
+    lib().ora_camera_position(V.ctypes.data, cam.ctypes.data)
+    rec = np.zeros(s.n, RECORD_DTYPE)
+    dbg = {k: np.zeros(s.n, np.float32 if t is C.c_float else np.int64) for k, t in OraDebug._fields_}
+    d = OraDebug()
+    for i in range(s.n):
+        lib().ora_project(C.byref(s), i, V.ctypes.data, P.ctypes.data, VP.ctypes.data, cam.ctypes.data, int(width),
+                          int(height), rec[i:i + 1].ctypes.data, C.byref(d))
+        for k, _ in OraDebug._fields_:
+            dbg[k][i] = getattr(d, k)
+    return rec, dbg
 
 
 def render(scene, view, proj, width, height, sh_degree=0, mode="tile", cap=0, nthreads=0):

@@ -238,3 +238,30 @@ def test_config5_50m_4k_virtual_ranks(built, scene50m, frame50m):
     slabs = D.render_virtual_slabs(scene50m, 8, V, P, 3840, 2160)
     over, worst = check_slab_frame(slabs, img)
     print(f"config 5 slabs: {over} pixels beyond 1e-4, max error {worst:.3g}")
+
+
+def test_projection_pins_on_device(built):
+    """The HIP preprocess against the float64 pins of tile.metal:40-157
+    directly (not only through the oracle): every visible pin's record."""
+    import json
+    from pathlib import Path
+    from gaussian_splat_amd.api import Scene
+    kp = json.loads((Path(__file__).resolve().parent / "golden" / "known_answers.json").read_text())["k_pins"]
+    for camname, cam in kp["cameras"].items():
+        sps = [s for s in kp["splats"] if s["camera"] == camname]
+        sc = Scene(pos=np.array([s["pos"] for s in sps]), rot=np.array([s["rot"] for s in sps]),
+                   scale=np.array([s["scale"] for s in sps]), opacity=np.full(len(sps), 0.7),
+                   color=np.tile([0.2, 0.4, 0.6], (len(sps), 1)))
+        r = _renderer(sc)
+        V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+        rec, dk, nt = r.project_host(V, P, kp["width"], kp["height"])
+        for i, s in enumerate(sps):
+            e = s["expect"]
+            assert (nt[i] > 0) == e["visible"], s["name"]
+            if not e["visible"]:
+                continue
+            for k in ("cx", "cy"):
+                assert abs(float(rec[i][k]) - e[k]) <= 2e-5 * max(1.0, abs(e[k])), (s["name"], k)
+            na, nb = np.hypot(e["ax"], e["ay"]), np.hypot(e["bx"], e["by"])
+            assert np.allclose([rec[i]["ax"], rec[i]["ay"]], [e["ax"], e["ay"]], rtol=0, atol=2e-5 * na), s["name"]
+            assert np.allclose([rec[i]["bx"], rec[i]["by"]], [e["bx"], e["by"]], rtol=0, atol=2e-5 * nb), s["name"]

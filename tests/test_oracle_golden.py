@@ -146,3 +146,58 @@ def test_bgra8_conversion():
     x[0, :, :] = (np.arange(48 * 4, dtype=np.float32).reshape(48, 4) + 0.5) / np.float32(255)  # near-ties
     y = np.rint(np.clip(x, 0, 1) * np.float32(255)).astype(np.uint8)
     np.testing.assert_array_equal(O.to_bgra8(x), y[..., [2, 1, 0, 3]])
+
+
+def _pin_scene(sp, **kw):
+    from gaussian_splat_amd.api import Scene
+    return Scene(pos=np.array([sp["pos"]]), rot=np.array([sp["rot"]]), scale=np.array([sp["scale"]]),
+                 opacity=np.array([0.7]), color=np.array([[0.2, 0.4, 0.6]]), **kw)
+
+
+@pytest.mark.parametrize("name", [s["name"] for s in KA["k_pins"]["splats"]])
+def test_projection_pins(name):
+    """K1-K5 (tile.metal:40-157): the oracle's fp32 record and intermediates
+    against a float64 restatement written straight from the shader lines
+    (tools/make_golden.py ref64_vertex): rotated anisotropic off-axis splats
+    (the J z-column sign, :122-123, changes b), both eigen fallbacks and a
+    0 < |b| <= 1e-8 one (:77-81), the near / far clip and a splat behind the
+    eye.  Relative tolerance 2e-5 (fp32 rounding of well-conditioned cases)."""
+    kp = KA["k_pins"]
+    sp = next(s for s in kp["splats"] if s["name"] == name)
+    cam = kp["cameras"][sp["camera"]]
+    V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+    rec, dbg = O.project_debug(_pin_scene(sp), V, P, kp["width"], kp["height"])
+    e = sp["expect"]
+    assert bool(dbg["visible"][0]) == e["visible"], (name, e.get("cull"))
+    assert abs(float(dbg["zf"][0]) - e["zf"]) <= 2e-5 * max(1.0, abs(e["zf"]))
+    if not e["visible"]:  # culled before the covariance (the oracle stops there)
+        return
+    scale = max(abs(e["a"]), abs(e["c"]))
+    for k in ("a", "b", "c"):
+        assert abs(float(dbg[k][0]) - e[k]) <= 2e-5 * scale, (k, float(dbg[k][0]), e[k])
+    for k in ("r1", "r2"):
+        assert abs(float(dbg[k][0]) - e[k]) <= 2e-5 * e[k], k
+    np.testing.assert_allclose([dbg["e1x"][0], dbg["e1y"][0]], e["e1"], rtol=0, atol=2e-5)
+    r = rec[0]
+    for k in ("cx", "cy"):
+        assert abs(float(r[k]) - e[k]) <= 2e-5 * max(1.0, abs(e[k])), k
+    na, nb = np.hypot(e["ax"], e["ay"]), np.hypot(e["bx"], e["by"])
+    np.testing.assert_allclose([r["ax"], r["ay"]], [e["ax"], e["ay"]], rtol=0, atol=2e-5 * na)
+    np.testing.assert_allclose([r["bx"], r["by"]], [e["bx"], e["by"]], rtol=0, atol=2e-5 * nb)
+    assert int(dbg["dkey"][0]) == 0x7C00 - int(np.float16(np.float32(e["zf"])).view(np.uint16))
+
+
+def test_sh_basis_pins():
+    """N2 (no reference counterpart): SH degree 1-3 colours of the oracle
+    against the published 3DGS basis evaluated in float64 (make_golden.py
+    ref64_sh), including clamped channels."""
+    kp = KA["k_pins"]
+    cam = kp["cameras"]["default"]
+    V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+    from gaussian_splat_amd.api import Scene
+    for c in kp["sh"]:
+        sc = Scene(pos=np.array([c["pos"]]), rot=np.array([[1.0, 0.2, -0.1, 0.3]]), scale=np.array([[0.02] * 3]),
+                   opacity=np.array([0.5]), color=np.array([c["f_dc"]]), sh_rest=np.array([c["f_rest"]]))
+        rec, dbg = O.project_debug(sc, V, P, kp["width"], kp["height"], sh_degree=c["deg"])
+        assert dbg["visible"][0]
+        np.testing.assert_allclose([rec[0]["r"], rec[0]["g"], rec[0]["b"]], c["rgb"], rtol=2e-5, atol=2e-6)

@@ -6,7 +6,10 @@
    These pin row I1 on any machine, including the GPU box.
 2. known_answers.json: hand-derived known-answer vectors for C1/K*/S1/A1,
    each computed here in float64 from the cited reference lines, NOT by the
-   oracle (the oracle is checked against them).
+   oracle (the oracle is checked against them); `k_pins`: K1-K5 records of
+   rotated anisotropic off-axis splats, the eigen branches, the near/far clip
+   and N2 colours, from a float64 restatement of tile.metal:40-157 and the
+   published 3DGS SH basis (`--known-only` regenerates just this file).
 """
 from __future__ import annotations
 
@@ -168,10 +171,191 @@ def known_answers() -> dict:
     return ka
 
 
+# ---- K1-K5 and N2 pins: a float64 restatement written from the shader lines ----
+# Independent of oracle/gs_oracle.c and of DESIGN.md's fp32 contract: matrix
+# algebra in float64 straight from gaussian_splat_tile.metal:40-157 (Metal
+# matrices are column-major, float3x3(c0, c1, c2) takes COLUMNS, m[col][row]),
+# and the published 3DGS real-SH basis (Kerbl et al. 2023, utils/sh_utils.py).
+SH_C0 = 0.28209479177387814
+SH_C1 = 0.4886025119029199
+SH_C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+         1.445305721320277, -0.5900435899266435]
+
+
+def ref64_vertex(pos, rot, scale, V, P, W, H, jz_sign=-1.0):
+    """vertex_main (tile.metal:85-157) + the quad's closed form, float64.
+    V, P: 4x4 math-convention matrices (M[row, col]).  jz_sign: the sign of
+    the Jacobian's z column (-1 = the shader's :122-123; +1 only to show that
+    the pins depend on it)."""
+    V = np.asarray(V, np.float64)
+    P = np.asarray(P, np.float64)
+    p4 = np.append(np.asarray(pos, np.float64), 1.0)
+    vp = V @ p4                                       # :94  viewMatrix * float4(position, 1)
+    zf = -vp[2]                                       # :96-97
+    out = {"zf": zf, "visible": False}
+    if zf < 1e-4:                                     # :99-105
+        out["cull"] = "zfront"
+        return out
+    q = np.asarray(rot, np.float64)
+    w, x, y, z = q / np.linalg.norm(q)                # :41-42 normalize, w = q[0]
+    R = np.column_stack([[1 - 2 * (y * y + z * z), 2 * (x * y + w * z), 2 * (x * z - w * y)],
+                         [2 * (x * y - w * z), 1 - 2 * (x * x + z * z), 2 * (y * z + w * x)],
+                         [2 * (x * z + w * y), 2 * (y * z - w * x), 1 - 2 * (x * x + y * y)]])  # :44-48
+    M = R @ np.diag(np.asarray(scale, np.float64))    # :52-58 R * S
+    Sigma = M @ M.T                                   # :59
+    Wr = V[:3, :3]                                    # :109-113 float3x3(viewMatrix[0..2].xyz)
+    Sv = (Wr @ Sigma) @ Wr.T                          # :115
+    fx = P[0, 0] * (W * 0.5)                          # :117 projectionMatrix[0][0]
+    fy = P[1, 1] * (H * 0.5)                          # :118
+    J0 = np.array([fx / zf, 0.0, jz_sign * fx * vp[0] / zf ** 2])  # :120-122
+    J1 = np.array([0.0, fy / zf, jz_sign * fy * vp[1] / zf ** 2])  # :123
+    a = J0 @ Sv @ J0 + 1e-4                           # :125, :129-130
+    b = J0 @ Sv @ J1                                  # :126
+    c = J1 @ Sv @ J1 + 1e-4                           # :127, :131
+    tr, det = a + c, a * c - b * b                    # eigenSym2x2 :62-83
+    s = math.sqrt(max(0.0, 0.25 * tr * tr - det))
+    l1, l2 = 0.5 * tr + s, 0.5 * tr - s
+    if abs(b) > 1e-8:
+        e1 = np.array([l1 - c, b]) / math.hypot(l1 - c, b)
+    else:
+        e1 = np.array([1.0, 0.0]) if a >= c else np.array([0.0, 1.0])
+    e2 = np.array([-e1[1], e1[0]])
+    r1, r2 = 3 * math.sqrt(max(l1, 0.0)), 3 * math.sqrt(max(l2, 0.0))  # :133-140
+    clip = (P @ V) @ p4                               # :145 viewProjectionMatrix (= P V, .mm:453)
+    ndc = clip[:3] / clip[3]                          # :146-147, z = clip.z * invW (:152)
+    out.update(a=a, b=b, c=c, r1=r1, r2=r2, e1=e1.tolist(), z_ndc=ndc[2])
+    # Metal clips to 0 <= z_ndc <= 1; the fragment stage drops depth < 0.001 (:187)
+    if not (0.0 <= ndc[2] <= 1.0):
+        out["cull"] = "zclip"
+        return out
+    if zf < 0.001 or not (r1 > 0 and r2 > 0):
+        out["cull"] = "depth/area"
+        return out
+    # window position of the centre (viewport y down) and the quad's uv = 3 q
+    # as a linear function of the pixel offset d = (x - cx, cy - y):
+    # uv = (3 d.e1 / r1, 3 d.e2 / r2)  (offsetPx = q.x r1 e1 + q.y r2 e2, :143)
+    cx, cy = (ndc[0] + 1) * W / 2, (1 - ndc[1]) * H / 2
+    A, B = e1 * 3 / r1, e2 * 3 / r2
+    out.update(visible=True, cx=cx, cy=cy, ax=A[0], ay=A[1], bx=B[0], by=B[1])
+    return out
+
+
+def ref64_sh(pos, campos, f_dc, f_rest, deg):
+    """eval_sh of the published 3DGS basis, dir = normalize(pos - campos),
+    f_rest channel-major (ply f_rest_{ch*15+k}); +0.5 and the loader's [0,1]
+    clamp (ply_loader.cpp:11-20; the reference has no SH > 0)."""
+    d = np.asarray(pos, np.float64) - np.asarray(campos, np.float64)
+    x, y, z = d / np.linalg.norm(d)
+    fr = np.asarray(f_rest, np.float64).reshape(3, 15)
+    out = []
+    for ch in range(3):
+        sh = np.concatenate([[f_dc[ch]], fr[ch]])
+        r = SH_C0 * sh[0]
+        if deg > 0:
+            r = r - SH_C1 * y * sh[1] + SH_C1 * z * sh[2] - SH_C1 * x * sh[3]
+        if deg > 1:
+            xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+            r = (r + SH_C2[0] * xy * sh[4] + SH_C2[1] * yz * sh[5] + SH_C2[2] * (2 * zz - xx - yy) * sh[6]
+                 + SH_C2[3] * xz * sh[7] + SH_C2[4] * (xx - yy) * sh[8])
+        if deg > 2:
+            r = (r + SH_C3[0] * y * (3 * xx - yy) * sh[9] + SH_C3[1] * xy * z * sh[10]
+                 + SH_C3[2] * y * (4 * zz - xx - yy) * sh[11] + SH_C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[12]
+                 + SH_C3[4] * x * (4 * zz - xx - yy) * sh[13] + SH_C3[5] * z * (xx - yy) * sh[14]
+                 + SH_C3[6] * x * (xx - 3 * yy) * sh[15])
+        out.append(min(max(r + 0.5, 0.0), 1.0))
+    return out
+
+
+def _f32(a):
+    return np.asarray(a, np.float32).astype(np.float64)
+
+
+def k_pins() -> dict:
+    """Splats whose K1-K5 outputs the oracle must reproduce (within fp32
+    rounding of these float64 values), by camera."""
+    def look_at(eye, tgt, up):
+        e, t = np.asarray(eye, np.float64), np.asarray(tgt, np.float64)
+        f = (t - e) / np.linalg.norm(t - e)
+        s = np.cross(f, up)
+        s /= np.linalg.norm(s)
+        u = np.cross(s, f)
+        V = np.eye(4)
+        V[0, :3], V[1, :3], V[2, :3] = s, u, -f
+        V[:3, 3] = [-s @ e, -u @ e, f @ e]
+        return V
+
+    def persp(fov, aspect, n, fr):
+        ys = 1 / math.tan(math.radians(fov) / 2)
+        P = np.zeros((4, 4))
+        P[0, 0], P[1, 1] = ys / aspect, ys
+        P[2, 2], P[2, 3], P[3, 2] = -(fr + n) / (fr - n), -2 * fr * n / (fr - n), -1
+        return P
+
+    W, H = 1920, 1080
+    cams = {"default": (_f32(look_at([0, 2, 5], [0, 0, 0], [0, -1, 0])), _f32(persp(45, W / H, 0.1, 1000))),
+            "axis": (_f32(np.eye(4)), _f32(persp(45, W / H, 0.1, 1000)))}  # eye at 0 looking down -z
+    cases = [
+        # rotated, anisotropic, off-axis (vx, vy != 0: the J z-column sign matters)
+        ("rot_aniso_1", "default", (0.8, -0.5, 1.2), (0.9, 0.3, -0.2, 0.25), (0.05, 0.01, 0.002)),
+        ("rot_aniso_2", "default", (-1.5, 0.7, -0.3), (0.2, -0.7, 0.5, 0.4), (0.02, 0.08, 0.01)),
+        ("rot_aniso_3", "default", (0.3, 1.1, 2.0), (-0.5, 0.5, 0.5, 0.5), (0.004, 0.03, 0.06)),
+        ("rot_aniso_4", "default", (-0.9, -1.2, 0.5), (0.1, 0.2, 0.9, -0.3), (0.1, 0.02, 0.05)),
+        ("rot_aniso_5", "default", (1.7, 0.2, -1.0), (0.6, -0.1, -0.6, 0.5), (0.015, 0.015, 0.2)),
+        ("rot_aniso_6", "default", (0.05, 0.4, 3.0), (0.3, 0.3, -0.3, 0.85), (0.03, 0.005, 0.012)),
+        ("unnormalised_quat", "default", (-0.4, 0.9, -1.6), (2.0, -1.0, 0.6, 1.4), (0.03, 0.012, 0.04)),
+        ("edge_straddle", "default", (2.95, -0.2, 0.4), (0.7, 0.1, 0.7, -0.1), (0.4, 0.1, 0.2)),
+        # b == 0 exactly (vx = 0, axis-aligned): eigen fallback e1 = (0, 1) if a < c, (1, 0) if a >= c (:77-81)
+        ("b0_a_lt_c", "axis", (0.0, 0.7, -5.0), (1.0, 0.0, 0.0, 0.0), (0.01, 0.03, 0.02)),
+        ("b0_a_ge_c", "axis", (0.0, 0.7, -5.0), (1.0, 0.0, 0.0, 0.0), (0.03, 0.01, 0.02)),
+        # 0 < |b| <= 1e-8 (vx = -6e-9): still the fallback branch
+        ("b_tiny_a_lt_c", "axis", (-6e-9, 0.7, -5.0), (1.0, 0.0, 0.0, 0.0), (0.01, 0.03, 0.02)),
+        # near plane: Metal's z-clip keeps z_ndc >= 0, i.e. zF >= 2fn/(f+n) = 0.19998
+        ("near_in", "axis", (0.01, 0.02, -0.2005), (0.9, 0.2, 0.3, 0.25), (0.001, 0.002, 0.0015)),
+        ("near_out", "axis", (0.01, 0.02, -0.1995), (0.9, 0.2, 0.3, 0.25), (0.001, 0.002, 0.0015)),
+        ("behind", "axis", (0.0, 0.0, 0.5), (1.0, 0.0, 0.0, 0.0), (0.01, 0.01, 0.01)),
+        ("beyond_far", "axis", (0.0, 0.0, -1001.0), (1.0, 0.0, 0.0, 0.0), (1.0, 1.0, 1.0)),
+    ]
+    out = {"width": W, "height": H, "cameras": {k: {"view": v.tolist(), "proj": p.tolist()} for k, (v, p) in cams.items()},
+           "splats": []}
+    for name, cam, pos, rot, scale in cases:
+        V, P = cams[cam]
+        pos, rot, scale = _f32(pos), _f32(rot), _f32(scale)
+        r = ref64_vertex(pos, rot, scale, V, P, W, H)
+        if name.startswith("rot_aniso"):  # the pin must see the shader's J z-column sign
+            alt = ref64_vertex(pos, rot, scale, V, P, W, H, jz_sign=+1.0)
+            assert abs(alt["b"] - r["b"]) > 1e-3 * max(abs(r["a"]), abs(r["c"])), name
+        out["splats"].append({"name": name, "camera": cam, "pos": pos.tolist(), "rot": rot.tolist(),
+                              "scale": scale.tolist(), "expect": r})
+    # N2: SH degree 1-3 colours from the published basis
+    V, P = cams["default"]
+    campos = -(V[:3, :3].T @ V[:3, 3])
+    rng = np.random.default_rng(2024)
+    sh = []
+    for deg in (1, 2, 3):
+        for k in range(4):
+            pos = _f32(rng.uniform(-1.5, 1.5, 3))
+            f_dc = _f32(rng.normal(0, 0.5, 3) if k < 3 else [4.0, -4.0, 0.1])  # k = 3: clamps at 1 and 0
+            f_rest = _f32(rng.normal(0, 0.3, 45))
+            sh.append({"deg": deg, "pos": pos.tolist(), "f_dc": f_dc.tolist(), "f_rest": f_rest.tolist(),
+                       "rgb": ref64_sh(pos, campos, f_dc, f_rest, deg)})
+    out["sh"] = sh
+    return out
+
+
 if __name__ == "__main__":
+    if "--known-only" in sys.argv:  # the float64 pins need no reference build
+        ka = json.loads((GOLD / "known_answers.json").read_text()) if (GOLD / "known_answers.json").exists() else {}
+        ka.update(known_answers())
+        ka["k_pins"] = k_pins()
+        (GOLD / "known_answers.json").write_text(json.dumps(ka, indent=1))
+        print("wrote", GOLD / "known_answers.json")
+        sys.exit(0)
     if not O.ref_available():
         sys.exit("oracle/_ref/libref_ply.so missing: run `make -C oracle` where /root/reference exists")
     GOLD.mkdir(parents=True, exist_ok=True)
     print(ply_fixtures())
-    (GOLD / "known_answers.json").write_text(json.dumps(known_answers(), indent=1))
+    ka = known_answers()
+    ka["k_pins"] = k_pins()
+    (GOLD / "known_answers.json").write_text(json.dumps(ka, indent=1))
     print("wrote", GOLD)
