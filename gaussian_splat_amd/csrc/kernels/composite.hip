@@ -25,13 +25,6 @@
 
 namespace gs {
 
-#ifndef GS_COMP_MASKSTEP  // A/B knob (tools/build_variant.py): 0 = the branch-free update
-#define GS_COMP_MASKSTEP 1
-#endif
-#ifndef GS_COMP_QMASK  // A/B knob: per-record quadrant mask computed once at staging
-#define GS_COMP_QMASK 1
-#endif
-
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
 __device__ unsigned long long g_cc[8];
@@ -116,14 +109,33 @@ struct KBuf {
 // only fragments with id <= thr[pixel] (the first a.cap in arrival order).
 // SLAB (depth-slab multi-GPU): 1 = transmittance pass, 2 =
 // colour pass from the earlier slabs' transmittance product.
+//
+// Staged record (per tile): the conic scaled by kConicScale
+// and its offset at the tile origin, so a lane's coverage is four fmas on
+// its tile-local pixel centre (lx, ly) = (px - tx0 + 1/2, py - ty0 + 1/2):
+//   u' = fma(Ax', lx, fma(-Ay', ly, U0)),  U0 = fma(Ax', tx0 - cx, Ay' (cy - ty0))
+// and likewise v' from (Bx', By', V0).
+// One 48-B LDS slot per staged record:
+//   a = (U0, V0, Ax', -Ay')   b = (Bx', -By', opacity, r)   c = (g, b)   id   half(zF)
+// and the wave lists hold slot byte offsets (u16), so a record's reads take
+// one address VGPR.
+struct StagedRec {
+    float4 a, b;
+    float2 c;
+    uint32_t id;  // splat id (cap modes)
+    uint32_t hd;  // MLAB: half(zF) bits
+};
+static_assert(sizeof(StagedRec) == 48, "staged record slot");
+__device__ __forceinline__ const StagedRec& staged_at(const StagedRec* base, uint32_t off) {
+    return *reinterpret_cast<const StagedRec*>(reinterpret_cast<const char*>(base) + off);
+}
+
 template <int MODE, bool CAP, int SLAB = 0>
 __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
-    __shared__ float4 s0[kTileThreads], s1[kTileThreads], s2[kTileThreads];
-    __shared__ uint32_t sid[kIds ? kTileThreads : 1];
-    __shared__ _Float16 shd[MODE == 3 ? kTileThreads : 1];  // MLAB: half depth of each record
-    __shared__ uint8_t wlist[4][kTileThreads];
-    __shared__ uint8_t sqm[GS_COMP_QMASK ? kTileThreads : 1];  // per staged record: quadrants it may reach
+    __shared__ StagedRec srec[kTileThreads];
+    __shared__ uint16_t wlist[4][kTileThreads];  // per wave: slot byte offsets
+    __shared__ uint8_t sqm[kTileThreads];  // per staged record: the quadrants it may reach
 
     // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
     // residue class a contiguous run of tiles (cdna_hip_programming.md §5, T1).
@@ -143,25 +155,23 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     const int tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
-    // this wave's quadrant: pixels [qx0, qx0+7] x [qy0, qy0+7]
+    // this wave's quadrant: pixels [tx0 + ox, +7] x [ty0 + oy, +7]
     const uint32_t tx0 = (uint32_t)(tx * kTile), ty0 = (uint32_t)(ty * kTile);
-    const uint32_t qx0 = tx0 + (wave & 1u) * 8u;
-    const uint32_t qy0 = ty0 + (wave >> 1) * 8u;
-    const int px = (int)qx0 + (int)(lane & 7u);
-    const int py = (int)qy0 + (int)(lane >> 3);
+    const uint32_t lxi = (wave & 1u) * 8u + (lane & 7u), lyi = (wave >> 1) * 8u + (lane >> 3);
+    const int px = (int)(tx0 + lxi);
+    const int py = (int)(ty0 + lyi);
     const bool inside = px < width && py < height;
-    const float fx = (float)px + 0.5f;
-    const float fy = (float)py + 0.5f;
+    const float lx = (float)lxi + 0.5f;  // tile-local pixel centre (exact)
+    const float ly = (float)lyi + 0.5f;
+    const float ftx0 = (float)tx0, fty0 = (float)ty0;
 
     const uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
-    // Pixels outside the frame start finished (A = 1 / T = 0): for the tile and
-    // live50 rules "finished" is then just the break test on A / T itself, so
-    // no separate per-lane flag is carried through the loop.
-    float A = inside ? 0.0f : 1.0f;  // tile rule: accumulated alpha
-    float T = inside ? 1.0f : 0.0f;  // live50 rule: transmittance
+    // Pixels outside the frame start finished (T = 0): for the tile and live50
+    // rules "finished" is then just the break test on T itself, so no
+    // separate per-lane flag is carried through the loop.
+    float T = inside ? 1.0f : 0.0f;  // transmittance (tile rule: T = 1 - A)
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     bool done = !inside;  // MODE 2 / 3
-    bool any = false;
     uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
     int cnt = 0;                 // MODE 2: covering fragments seen
     if constexpr (CAP) {
@@ -169,110 +179,74 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     }
     // slab colour pass: the state the earlier (farther) slabs leave, exactly
     // the ordered product of their transmittance, rank order = depth order
-    float A0 = 0.0f, T0 = 1.0f;
+    float T0 = 1.0f;
     mlab::KBuf kb;
     if constexpr (MODE == 3) kb.clear();
     if constexpr (SLAB == 2) {
         float ts = 1.0f;
         if (inside)
             for (int j = 0; j < a.slab_rank; ++j) ts *= a.t_all[((size_t)j * height + py) * width + px];
-        // saturated before this slab (A >= 0.99 / T < 0.01): the loop broke earlier
-        if constexpr (MODE == 0) {
-            if (inside) A = 1.0f - ts;
-            A0 = A;
-        } else {
-            if (inside) T = ts;
-            T0 = T;
-        }
+        // saturated before this slab (T <= 0.01 / T < 0.01): the loop broke earlier
+        if (inside) T = ts;
+        T0 = T;
     }
     auto finished = [&]() -> bool {
-        if constexpr (MODE == 0) return A >= kSat;
+        if constexpr (MODE == 0) return T <= kTSat;
         else if constexpr (MODE == 1) return T < kTMin;
         else return done;
     };
 
-    // Composite update of one fragment (covered = box test and 0.01 cutoff).
-    auto step = [&](bool covered, float alpha, float r, float g, float bl, uint32_t id) {
-        bool in = !finished() && covered;
-        if constexpr (CAP) in = in && id <= thr;
-        any |= in;
-#if GS_COMP_MASKSTEP
-        if constexpr (MODE == 0) {
-            // skipping a lane is bit-identical to adding its exact zero; the
-            // update shares the gaussian's exec-masked block
-            if (in) {
-                const float sa = alpha * (1.0f - A);
-                C0 = __builtin_fmaf(r, sa, C0);
-                C1 = __builtin_fmaf(g, sa, C1);
-                C2 = __builtin_fmaf(bl, sa, C2);
-                A = A + sa;
-            }
-        } else if constexpr (MODE == 1) {
-            if (in) {
-                C0 = __builtin_fmaf(r, T, C0);
-                C1 = __builtin_fmaf(g, T, C1);
-                C2 = __builtin_fmaf(bl, T, C2);
-                T = T * (1.0f - alpha);
-            }
-        } else {
-#else
-        if constexpr (MODE == 0) {
-            // out-of-support lanes add an exact zero: bit-identical to skipping
-            const float sa = in ? alpha * (1.0f - A) : 0.0f;
-            C0 = __builtin_fmaf(r, sa, C0);
-            C1 = __builtin_fmaf(g, sa, C1);
-            C2 = __builtin_fmaf(bl, sa, C2);
-            A = A + sa;
-        } else {
-#endif
-            const float tw = in ? T : 0.0f;
-            C0 = __builtin_fmaf(r, tw, C0);
-            C1 = __builtin_fmaf(g, tw, C1);
-            C2 = __builtin_fmaf(bl, tw, C2);
-            T = in ? T * (1.0f - alpha) : T;
-        }
-    };
-
-    auto body_v = [&](const float4 aa, const float4 bb, const float4 cc, uint32_t id) {
-        const float dx = fx - aa.x;
-        const float dy = aa.y - fy;
-        const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
-        const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
+    // One record at this lane's pixel: coverage (K6 closed form: the quad box
+    // |uv| <= 3 and the 0.01 cutoff, tile.metal:142-156,191-195), then the
+    // gaussian alpha (:197) and the composite update (A1).  Skipping a lane is
+    // bit-identical to adding its exact zero, so the update sits in the
+    // gaussian's exec-masked block.
+    auto body_v = [&](const float4 aa, const float4 bb, const float2 cc, uint32_t id, _Float16 hd) {
+        const float u = __builtin_fmaf(aa.z, lx, __builtin_fmaf(aa.w, ly, aa.x));
+        const float v = __builtin_fmaf(bb.x, lx, __builtin_fmaf(bb.y, ly, aa.y));
         const float qq = __builtin_fmaf(v, v, u * u);
-        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
-#ifdef GS_COMPOSITE_COUNTERS
-        {
-            const uint64_t m = __ballot(covered && !finished());
-            if (lane == 0 && m) GS_CC(4, 1);
-            if (lane == 0) GS_CC(7, __popcll(m));
-        }
-#endif
-        step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, id);
-    };
-
-    auto body = [&](uint32_t k) {
-        const float4 aa = s0[k];
-        const float4 bb = s1[k];
-        const float4 cc = s2[k];
-        const float dx = fx - aa.x;
-        const float dy = aa.y - fy;
-        const float u = __builtin_fmaf(dy, aa.w, dx * aa.z);
-        const float v = __builtin_fmaf(dy, bb.y, dx * bb.x);
-        const float qq = __builtin_fmaf(v, v, u * u);
-        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= 3.0f && qq <= kQMax;
+        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= kBoxS && qq <= kQMaxS;
         if constexpr (MODE == 2) {
             // arrival order: the a.cap-th covering fragment fixes the threshold
             const bool in = !done && covered;
             cnt += in ? 1 : 0;
             if (in && cnt == a.cap) {
-                thr = sid[k];
+                thr = id;
                 done = true;
             }
         } else if constexpr (MODE == 3) {
-            if (!done && covered) kb.insert(bb.w, cc.x, cc.y, bb.z * gs_gauss(qq), shd[k]);
+            if (!done && covered) kb.insert(bb.w, cc.x, cc.y, bb.z * gs_gauss2(qq), hd);
         } else {
-            step(covered, bb.z * gs_gauss(qq), bb.w, cc.x, cc.y, kIds ? sid[k] : 0u);
+            bool in = !finished() && covered;
+            if constexpr (CAP) in = in && id <= thr;
+#ifdef GS_COMPOSITE_COUNTERS
+            {
+                const uint64_t m = __ballot(in);
+                if (lane == 0 && m) GS_CC(4, 1);
+                if (lane == 0) GS_CC(7, __popcll(m));
+            }
+#endif
+            if (in) {
+                const float alpha = bb.z * gs_gauss2(qq);
+                if constexpr (MODE == 0) {
+                    const float sa = alpha * T;
+                    C0 = __builtin_fmaf(bb.w, sa, C0);
+                    C1 = __builtin_fmaf(cc.x, sa, C1);
+                    C2 = __builtin_fmaf(cc.y, sa, C2);
+                    T = T - sa;
+                } else {
+                    C0 = __builtin_fmaf(bb.w, T, C0);
+                    C1 = __builtin_fmaf(cc.x, T, C1);
+                    C2 = __builtin_fmaf(cc.y, T, C2);
+                    T = T * (1.0f - alpha);
+                }
+            }
         }
+    };
+    auto body = [&](uint32_t off) {
+        const StagedRec& r = staged_at(srec, off);
+        body_v(r.a, r.b, r.c, kIds ? r.id : 0u,
+               MODE == 3 ? __builtin_bit_cast(_Float16, (uint16_t)r.hd) : (_Float16)0.0f);
     };
 
     // Software pipeline: while batch b is composited, batch b+1's records are
@@ -304,10 +278,15 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         }
         if (tid == 0) GS_CC(5, 1);
         if (b + tid < rg.y) {
-            s0[tid] = r0;
-            s1[tid] = r1;
-            s2[tid] = r2;
-#if GS_COMP_QMASK
+            // record (cx, cy, ax, ay) (bx, by, op, r) (g, b, rect_lo, rect_hi)
+            // staged for this tile (scaled conic, offsets at the tile origin)
+            const float ax = r0.z * kConicScale, ay = r0.w * kConicScale;
+            const float bxs = r1.x * kConicScale, bys = r1.y * kConicScale;
+            const float ex = ftx0 - r0.x, ey = r0.y - fty0;
+            StagedRec& st = srec[tid];
+            st.a = make_float4(__builtin_fmaf(ax, ex, ay * ey), __builtin_fmaf(bxs, ex, bys * ey), ax, -ay);
+            st.b = make_float4(bxs, -bys, r1.z, r1.w);
+            st.c = make_float2(r2.x, r2.y);
             {
                 // which of the tile's 8x8 quadrants (wave w: column w & 1, row
                 // w >> 1) the record's rect reaches and its cell mask does not
@@ -329,10 +308,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 }
                 sqm[tid] = (uint8_t)qm;
             }
-#endif
-            if constexpr (kIds) sid[tid] = id_cur;
+            if constexpr (kIds) st.id = id_cur;
             if constexpr (MODE == 3)  // half(zF) from the depth key (dkey = 0x7C00 - half bits)
-                shd[tid] = __builtin_bit_cast(_Float16, (uint16_t)(kDepthInf - a.dkey[id_cur]));
+                st.hd = kDepthInf - a.dkey[id_cur];
         }
         __syncthreads();
         {
@@ -352,95 +330,52 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         if (__ballot(!finished()) != 0) {
             for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
                 const uint32_t k = k0 + lane;
-                bool hit = false;
-#if GS_COMP_QMASK
-                if (k < cnt_b) hit = (sqm[k] >> wave) & 1u;
-#else
-                if (k < cnt_b) {
-                    const float4 c = s2[k];
-                    const uint32_t wlo = __float_as_uint(c.z), whi = __float_as_uint(c.w);
-                    const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
-                    hit = !((hi >> 16) < qy0 || (lo >> 16) > qy0 + 7u || (hi & 0xFFFFu) < qx0 ||
-                            (lo & 0xFFFFu) > qx0 + 7u);
-                    if (hit && a.cell_mask) {
-                        // skip the quadrant when the ellipse provably misses it
-                        const uint32_t dcx = (qx0 >> 3) - ((lo & 0xFFFFu) >> 3), dcy = (qy0 >> 3) - ((lo >> 16) >> 3);
-                        if (dcx < 4u && dcy < 4u) hit = !((rect_cell_mask(wlo, whi) >> (dcy * 4u + dcx)) & 1u);
-                    }
-                }
-#endif
+                const bool hit = k < cnt_b && ((sqm[k] >> wave) & 1u);
                 const uint64_t m = __ballot(hit);
-                if (hit) wlist[wave][nl + mbcnt(m)] = (uint8_t)k;
+                if (hit) wlist[wave][nl + mbcnt(m)] = (uint16_t)(k * sizeof(StagedRec));
                 nl += (uint32_t)__popcll(m);
             }
         }
         wave_lds_sync();  // wlist[wave] is only touched by this wave
         uint32_t i = 0;
-        for (; i + 1 < nl; i += 2) {
-            if (__ballot(!finished()) == 0) break;
-            const uint32_t k0 = wlist[wave][i], k1 = wlist[wave][i + 1];
-            if constexpr (MODE == 2 || MODE == 3) {
-                body(k0);
-                body(k1);
-            } else {
-                // both records' LDS reads issue before either update
-                const float4 a0 = s0[k0], b0 = s1[k0], c0 = s2[k0];
-                const float4 a1 = s0[k1], b1 = s1[k1], c1 = s2[k1];
-                const uint32_t i0 = kIds ? sid[k0] : 0u, i1 = kIds ? sid[k1] : 0u;
-                body_v(a0, b0, c0, i0);
-                body_v(a1, b1, c1, i1);
+        if constexpr (MODE == 2 || MODE == 3) {
+            for (; i < nl; ++i) {
+                if (__ballot(!done) == 0) break;
+                body(wlist[wave][i]);
             }
+        } else {
+            // two records per step, both records' LDS reads issued before
+            // either body; the next pair's slot offsets are read one step ahead
+            const uint32_t* wl2 = reinterpret_cast<const uint32_t*>(wlist[wave]);
+            uint32_t w2 = nl >= 2 ? wl2[0] : 0u;
+            for (; i + 1 < nl; i += 2) {
+                if (__ballot(!finished()) == 0) break;
+                const StagedRec& p0 = staged_at(srec, w2 & 0xFFFFu);
+                const StagedRec& p1 = staged_at(srec, w2 >> 16);
+                const float4 a0 = p0.a, b0 = p0.b;
+                const float2 c0 = p0.c;
+                const float4 a1 = p1.a, b1 = p1.b;
+                const float2 c1 = p1.c;
+                const uint32_t i0 = kIds ? p0.id : 0u, i1 = kIds ? p1.id : 0u;
+                if (i + 3 < nl) w2 = wl2[(i >> 1) + 1];
+                body_v(a0, b0, c0, i0, (_Float16)0.0f);
+                body_v(a1, b1, c1, i1, (_Float16)0.0f);
+            }
+            if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         }
-        if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         if (lane == 0) GS_CC(3, i);
-#ifdef GS_COMPOSITE_COUNTERS
-        {  // iterations a split quadrant would need: max over 8x4 halves / 4x4 quarters
-            uint32_t h[2] = {0, 0}, qc[4] = {0, 0, 0, 0};
-            for (uint32_t j = 0; j < i; ++j) {
-                const float4 c = s2[wlist[wave][j]];
-                const uint32_t lo = rect_coords(__float_as_uint(c.z), a.cell_mask);
-                const uint32_t hi = rect_coords(__float_as_uint(c.w), a.cell_mask);
-                const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
-                for (uint32_t sy = 0; sy < 2; ++sy) {
-                    const bool oy = !(y1 < qy0 + 4 * sy || y0 > qy0 + 4 * sy + 3);
-                    h[sy] += oy;
-                    for (uint32_t sx = 0; sx < 2; ++sx) {
-                        const bool ox = !(x1 < qx0 + 4 * sx || x0 > qx0 + 4 * sx + 3);
-                        qc[sy * 2 + sx] += (oy && ox);
-                    }
-                }
-            }
-            if (lane == 0) {
-                GS_CC(1, h[0] > h[1] ? h[0] : h[1]);
-                GS_CC(2, max(max(qc[0], qc[1]), max(qc[2], qc[3])));
-            }
-        }
-#endif
     }
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
     if (!inside) return;
     if constexpr (SLAB == 1) {
-        a.t_out[(size_t)py * width + px] = MODE == 0 ? 1.0f - A : T;
+        a.t_out[(size_t)py * width + px] = T;
     } else if constexpr (SLAB == 2) {
         // contributions: colour and the alpha this slab adds (sum over slabs)
-        a.out[(size_t)py * width + px] =
-            make_float4(C0, C1, C2, MODE == 0 ? A - A0 : (any ? T0 - T : 0.0f));
+        a.out[(size_t)py * width + px] = make_float4(C0, C1, C2, T0 - T);
     } else if constexpr (MODE == 2) {
         a.thr_out[(size_t)py * width + px] = thr;
-    } else if constexpr (MODE == 3) {
-        const float4 o = kb.resolve();
-        const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
-        if (a.out_bgra8)
-            a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
-        else
-            a.out[(size_t)orow * width + px] = o;
     } else {
-        float4 o;
-        if constexpr (MODE == 0) {
-            o = make_float4(C0, C1, C2, A);
-        } else {
-            o = make_float4(C0, C1, C2, any ? 1.0f - T : 0.0f);
-        }
+        const float4 o = MODE == 3 ? kb.resolve() : make_float4(C0, C1, C2, 1.0f - T);
         // compact = owned bin rows stacked (multi-GPU band buffer)
         const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
         if (a.out_bgra8)

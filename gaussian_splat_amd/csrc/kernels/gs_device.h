@@ -22,8 +22,18 @@ constexpr int kBinThreads = 1024;
 constexpr int kDepthBits = 15;            // positive half bit patterns are < 0x7C01
 constexpr uint32_t kDepthInf = 0x7C00u;
 constexpr float kQMax = 9.21034037197618f;  // 2 ln 100: exp(-q/2) >= 0.01 (tile.metal:193)
-constexpr float kSat = 0.99f;             // tile.metal:261
 constexpr float kTMin = 0.01f;            // 50layer.metal:219
+// Composite contract.  The conic is scaled by
+// kConicScale = sqrt(log2(e)/2) when a record is staged for a tile, so that
+// q' = u'^2 + v'^2 = q log2(e)/2 and the gaussian is 2^-q' with no scale op:
+//   box test |u| <= 3 (the quad, tile.metal:142-156)  ->  |u'| <= kBoxS,
+//   cutoff exp(-q/2) >= 0.01 (tile.metal:191-195)      ->  q' <= log2(100).
+// The tile rule (tile.metal:251-266) tracks T = 1 - A: sa = a*T, C += rgb*sa,
+// T -= sa, break once T <= kTSat (A >= 0.99, :261); alpha out = 1 - T.
+constexpr float kConicScale = 0.8493217825889587f;
+constexpr float kBoxS = 2.5479652881622314f;   // float(3 * sqrt(log2(e)/2))
+constexpr float kQMaxS = 6.643856048583984f;   // float(log2(100))
+constexpr float kTSat = 0.01f;
 
 // Uniforms of one frame (tile.metal:16-21 plus derived values).
 struct FrameUniforms {
@@ -88,8 +98,21 @@ __device__ __forceinline__ float gs_exp2_poly(float t) {
     return __builtin_ldexpf(p, (int)n);
 }
 
-// F1 gaussian exp(-q/2) = 2^(q * -log2(e)/2) (oracle ora_gauss).
-__device__ __forceinline__ float gs_gauss(float q) { return gs_exp2_poly(q * -0.72134752044448170f); }
+// F1 gaussian on the scaled conic: exp(-q/2) = 2^-q' (oracle ora_gauss2, op
+// for op): n = rint(-q'), f = -q' - n (exact), a degree-5 minimax polynomial
+// of 2^f on [-1/2, 1/2] (relative error 1.7e-7 in f32), scaled by 2^n.
+__device__ __forceinline__ float gs_gauss2(float qs) {
+    const float t = -qs;
+    const float n = __builtin_rintf(t);
+    const float f = t - n;
+    float p = 1.3267117319628596e-3f;
+    p = __builtin_fmaf(p, f, 9.6715930849313736e-3f);
+    p = __builtin_fmaf(p, f, 5.5507261306047440e-2f);
+    p = __builtin_fmaf(p, f, 2.4022240936756134e-1f);
+    p = __builtin_fmaf(p, f, 6.9314700365066528e-1f);
+    p = __builtin_fmaf(p, f, 1.0f);
+    return __builtin_ldexpf(p, (int)n);
+}
 
 // IEEE half bits, round to nearest even (v_cvt_f16_f32).
 __device__ __forceinline__ uint32_t half_bits(float f) {

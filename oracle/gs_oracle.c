@@ -20,9 +20,17 @@
 #define OWN_ROW 32 /* multi-GPU ownership unit: 32-px bin rows, owner[by] */
 /* 2*ln(100): exp(-q/2) < 0.01 <=> q > 2 ln 100 (tile.metal:191-195). */
 #define ORA_QMAX 9.21034037197618f
-/* 0.99 saturation (tile.metal:261), 0.01 transmittance (50layer.metal:219). */
-#define ORA_SAT 0.99f
+/* 0.01 transmittance (50layer.metal:219). */
 #define ORA_TMIN 0.01f
+/* Composite contract: the record's conic is scaled by
+ * sqrt(log2(e)/2) per tile, so q' = q log2(e)/2 and the gaussian is 2^-q';
+ * box |u| <= 3 -> |u'| <= ORA_BOXS, cutoff exp(-q/2) >= 0.01 -> q' <= log2 100.
+ * The tile rule tracks T = 1 - A and breaks at T <= 0.01 (A >= 0.99,
+ * tile.metal:261). */
+#define ORA_CONIC_S 0.8493217825889587f
+#define ORA_BOXS 2.5479652881622314f
+#define ORA_QMAXS 6.643856048583984f
+#define ORA_TSAT 0.01f
 
 static const float SH_C0 = 0.28209479177387814f; /* ply_loader.cpp:9 */
 static const float SH_C1 = 0.4886025119029199f;
@@ -87,6 +95,23 @@ float ora_expf(float x) { return ora_exp2_poly(x * 1.44269504088896341f); }
  * tile.metal evaluates exp in relaxed math and stores alpha as half, so this
  * is far inside the reference's own precision. */
 float ora_gauss(float q) { return ora_exp2_poly(q * -0.72134752044448170f); }
+
+/* The composite's gaussian on the scaled conic: 2^-qs = exp(-q/2) with
+ * n = rint(-qs), f = -qs - n (exact), a degree-5 minimax polynomial of 2^f
+ * on [-1/2, 1/2] (relative error 1.7e-7 in f32) and ldexp; op for op the
+ * kernel's gs_gauss2. */
+float ora_gauss2(float qs) {
+    float t = -qs;
+    float n = rintf(t);
+    float f = t - n;
+    float p = 1.3267117319628596e-3f;
+    p = fmaf(p, f, 9.6715930849313736e-3f);
+    p = fmaf(p, f, 5.5507261306047440e-2f);
+    p = fmaf(p, f, 2.4022240936756134e-1f);
+    p = fmaf(p, f, 6.9314700365066528e-1f);
+    p = fmaf(p, f, 1.0f);
+    return ldexpf(p, (int)n);
+}
 
 static uint8_t ora_unorm8(float x) {
     if (!(x > 0.0f)) return 0; /* also NaN */
@@ -598,16 +623,23 @@ void ora_project_all(const ora_scene *s, const float V[16], const float P[16], i
 /* F1 + S1 + A1: per-pixel composite                                        */
 /* ------------------------------------------------------------------------ */
 
-/* Coverage + gaussian of record j at pixel (px,py): returns alpha or -1. */
+/* Coverage + gaussian of record j at pixel (px,py): returns alpha or -1.
+ * The conic is staged per 16x16 tile (the composite kernel's workgroup):
+ * scaled by sqrt(log2(e)/2), offset at the tile origin (tx0, ty0); the pixel
+ * centre enters tile-local, (lx, ly) = (px - tx0 + 1/2, py - ty0 + 1/2). */
 static float frag_alpha(const ora_record *r, int px, int py) {
-    float dx = ((float)px + 0.5f) - r->cx;
-    float dy = r->cy - ((float)py + 0.5f);
-    float u = fmaf(dy, r->ay, dx * r->ax);
-    float v = fmaf(dy, r->by, dx * r->bx);
-    if (!(fabsf(u) <= 3.0f && fabsf(v) <= 3.0f)) return -1.0f; /* K6 quad coverage */
+    int tx0 = px & ~(TILE - 1), ty0 = py & ~(TILE - 1);
+    float ax = r->ax * ORA_CONIC_S, ay = r->ay * ORA_CONIC_S;
+    float bx = r->bx * ORA_CONIC_S, by = r->by * ORA_CONIC_S;
+    float ex = (float)tx0 - r->cx, ey = r->cy - (float)ty0;
+    float u0 = fmaf(ax, ex, ay * ey), v0 = fmaf(bx, ex, by * ey);
+    float lx = (float)(px - tx0) + 0.5f, ly = (float)(py - ty0) + 0.5f;
+    float u = fmaf(ax, lx, fmaf(-ay, ly, u0));
+    float v = fmaf(bx, lx, fmaf(-by, ly, v0));
+    if (!(fmaxf(fabsf(u), fabsf(v)) <= ORA_BOXS)) return -1.0f; /* K6 quad coverage |uv| <= 3 */
     float q = fmaf(v, v, u * u);
-    if (!(q <= ORA_QMAX)) return -1.0f; /* g < 0.01 discard, tile.metal:193 */
-    return r->opacity * ora_gauss(q); /* tile.metal:197 */
+    if (!(q <= ORA_QMAXS)) return -1.0f; /* g < 0.01 discard, tile.metal:193 */
+    return r->opacity * ora_gauss2(q); /* tile.metal:197 */
 }
 
 typedef struct {
@@ -705,17 +737,17 @@ static void mlab_resolve(const mlab_kbuf *k, float out[4]) {
 /* Composite `cnt` fragments given in S1 order (dkey asc, index asc). */
 static void composite(int mode, const float *frag_rgb_a, int cnt, float out[4]) {
     if (mode == ORA_MODE_TILE) { /* tile.metal:251-266 */
-        float A = 0.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+        float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f; /* T = 1 - A */
         for (int k = 0; k < cnt; ++k) {
             const float *f = frag_rgb_a + k * 4;
-            float sa = f[3] * (1.0f - A);
+            float sa = f[3] * T;
             C0 = fmaf(f[0], sa, C0);
             C1 = fmaf(f[1], sa, C1);
             C2 = fmaf(f[2], sa, C2);
-            A = A + sa;
-            if (A >= ORA_SAT) break;
+            T = T - sa;
+            if (T <= ORA_TSAT) break; /* A >= 0.99 */
         }
-        out[0] = C0; out[1] = C1; out[2] = C2; out[3] = A;
+        out[0] = C0; out[1] = C1; out[2] = C2; out[3] = 1.0f - T;
     } else { /* 50layer.metal:208-222 */
         float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
         for (int k = 0; k < cnt; ++k) {
@@ -866,63 +898,55 @@ static int composite_records_impl(const ora_record *rec, const uint32_t *dkey, i
                         float ts = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
                         if (slab == 2)
                             for (int j = 0; j < slab_rank; ++j) ts *= t_all[((size_t)j * H + py) * W + px];
+                        float T = slab == 2 ? ts : 1.0f, T0 = T;
                         if (mode == ORA_MODE_TILE) {
-                            float A = slab == 2 ? 1.0f - ts : 0.0f, A0 = A;
-                            if (!(A >= ORA_SAT))
+                            if (!(T <= ORA_TSAT))
                                 for (int64_t k = 0; k < m; ++k) {
                                     const ora_record *r = &rec[ord[k].idx];
                                     float al = frag_alpha(r, px, py);
                                     if (al < 0.0f) continue;
-                                    float sa = al * (1.0f - A);
+                                    float sa = al * T;
                                     C0 = fmaf(r->r, sa, C0);
                                     C1 = fmaf(r->g, sa, C1);
                                     C2 = fmaf(r->b, sa, C2);
-                                    A = A + sa;
-                                    if (A >= ORA_SAT) break;
+                                    T = T - sa;
+                                    if (T <= ORA_TSAT) break;
                                 }
-                            if (slab == 1) {
-                                o[0] = 1.0f - A;
-                            } else {
-                                o[0] = C0; o[1] = C1; o[2] = C2; o[3] = A - A0;
-                            }
                         } else {
-                            float T = slab == 2 ? ts : 1.0f, T0 = T;
-                            int any = 0;
                             if (!(T < ORA_TMIN))
                                 for (int64_t k = 0; k < m; ++k) {
                                     const ora_record *r = &rec[ord[k].idx];
                                     float al = frag_alpha(r, px, py);
                                     if (al < 0.0f) continue;
-                                    any = 1;
                                     C0 = fmaf(r->r, T, C0);
                                     C1 = fmaf(r->g, T, C1);
                                     C2 = fmaf(r->b, T, C2);
                                     T = T * (1.0f - al);
                                     if (T < ORA_TMIN) break;
                                 }
-                            if (slab == 1) {
-                                o[0] = T;
-                            } else {
-                                o[0] = C0; o[1] = C1; o[2] = C2; o[3] = any ? T0 - T : 0.0f;
-                            }
+                        }
+                        if (slab == 1) {
+                            o[0] = T;
+                        } else {
+                            o[0] = C0; o[1] = C1; o[2] = C2; o[3] = T0 - T;
                         }
                         continue;
                     }
                     if (cap == 0) {
                         if (mode == ORA_MODE_TILE) { /* fused early-break walk */
-                            float A = 0.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+                            float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f; /* T = 1 - A */
                             for (int64_t k = 0; k < m; ++k) {
                                 const ora_record *r = &rec[ord[k].idx];
                                 float al = frag_alpha(r, px, py);
                                 if (al < 0.0f) continue;
-                                float sa = al * (1.0f - A);
+                                float sa = al * T;
                                 C0 = fmaf(r->r, sa, C0);
                                 C1 = fmaf(r->g, sa, C1);
                                 C2 = fmaf(r->b, sa, C2);
-                                A = A + sa;
-                                if (A >= ORA_SAT) break;
+                                T = T - sa;
+                                if (T <= ORA_TSAT) break;
                             }
-                            o[0] = C0; o[1] = C1; o[2] = C2; o[3] = A;
+                            o[0] = C0; o[1] = C1; o[2] = C2; o[3] = 1.0f - T;
                             continue;
                         }
                         for (int64_t k = 0; k < m; ++k) {

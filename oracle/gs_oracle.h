@@ -153,7 +153,8 @@ void ora_composite_list(const float *frags, int n, int mode, int cap, float out[
 /* Helpers exposed for tests. */
 uint16_t ora_f32_to_f16_bits(float f);
 float ora_expf(float x);
-float ora_gauss(float q); /* exp(-q/2) as used by F1 */
+float ora_gauss(float q); /* exp(-q/2) (round-1 form, test helper) */
+float ora_gauss2(float qs); /* 2^-qs: the composite gaussian on the scaled conic (F1) */
 /* fp32 RGBA -> BGRA8Unorm (metal_renderer.mm:58, instanced_splat_renderer.mm:269-271):
  * per channel clamp to [0,1], x255, round half to even; bytes B,G,R,A.
  * Parity unpinned (Metal's conversion cannot run here). */

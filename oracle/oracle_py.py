@@ -80,6 +80,8 @@ def lib() -> C.CDLL:
         L.ora_expf.restype = C.c_float
         L.ora_gauss.argtypes = [C.c_float]
         L.ora_gauss.restype = C.c_float
+        L.ora_gauss2.argtypes = [C.c_float]
+        L.ora_gauss2.restype = C.c_float
         L.ora_to_bgra8.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
         L.ora_to_bgra8.restype = None
         _lib = L
@@ -239,6 +241,11 @@ def expf(x: float) -> float:
 
 def gauss(q: float) -> float:
     return float(lib().ora_gauss(float(q)))
+
+
+def gauss2(qs: float) -> float:
+    """2^-qs, the composite's gaussian on the scaled conic."""
+    return float(lib().ora_gauss2(float(qs)))
 
 
 def to_bgra8(rgba: np.ndarray) -> np.ndarray:

@@ -115,6 +115,11 @@ def test_expf_accuracy():
     g = np.array([O.gauss(float(q)) for q in qs], np.float64)
     assert np.abs(g / np.exp(-0.5 * qs.astype(np.float64)) - 1).max() < 5e-7
     assert O.gauss(0.0) == 1.0
+    # the composite's gaussian on the scaled conic: 2^-q' = exp(-q/2), q' = q log2(e)/2
+    qs = np.linspace(0.0, 6.6439, 40001, dtype=np.float32)
+    g2 = np.array([O.gauss2(float(q)) for q in qs], np.float64)
+    assert np.abs(g2 / np.exp2(-qs.astype(np.float64)) - 1).max() < 2e-7
+    assert O.gauss2(0.0) == 1.0 and O.gauss2(1.0) == 0.5 and O.gauss2(6.0) == 2.0 ** -6
 
 
 def test_oracle_render_invariants():
