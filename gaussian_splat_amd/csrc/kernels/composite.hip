@@ -32,6 +32,30 @@ __device__ unsigned long long g_cc[8];
 #else
 #define GS_CC(i, v) (void)0
 #endif
+#ifdef GS_COMPOSITE_TIMERS
+// Debug build only (-DGS_COMPOSITE_TIMERS): shader-clock cycles per wave
+// spent in each phase of the batch loop, summed over waves (tools/composite_counters.py).
+__device__ unsigned long long g_ct[8];
+#define GS_CT_DECL unsigned long long ct_acc[6] = {0, 0, 0, 0, 0, 0}, ct_t = clock64(), ct_t0 = ct_t
+#define GS_CT(i)                                   \
+    do {                                           \
+        const unsigned long long ct_n = clock64(); \
+        ct_acc[i] += ct_n - ct_t;                  \
+        ct_t = ct_n;                               \
+    } while (0)
+#define GS_CT_FLUSH()                                                                            \
+    do {                                                                                         \
+        if (lane == 0) {                                                                         \
+            for (int ci = 0; ci < 6; ++ci) (void)atomicAdd(&g_ct[ci], ct_acc[ci]);               \
+            (void)atomicAdd(&g_ct[6], clock64() - ct_t0);                                        \
+            (void)atomicAdd(&g_ct[7], 1ull);                                                     \
+        }                                                                                        \
+    } while (0)
+#else
+#define GS_CT_DECL (void)0
+#define GS_CT(i) (void)0
+#define GS_CT_FLUSH() (void)0
+#endif
 
 // MLAB k-buffer (gaussian_splat.metal:201-361): six premultiplied half
 // layers + half depths per pixel in registers, updated per covering fragment
@@ -115,15 +139,12 @@ struct KBuf {
 // its tile-local pixel centre (lx, ly) = (px - tx0 + 1/2, py - ty0 + 1/2):
 //   u' = fma(Ax', lx, fma(-Ay', ly, U0)),  U0 = fma(Ax', tx0 - cx, Ay' (cy - ty0))
 // and likewise v' from (Bx', By', V0).
-// One 48-B LDS slot per staged record:
-//   a = (U0, V0, Ax', -Ay')   b = (Bx', -By', opacity, r)   c = (g, b)   id   half(zF)
-// and the wave lists hold slot byte offsets (u16), so a record's reads take
-// one address VGPR.
+// One 48-B LDS slot per staged record (first the raw gathered record):
+//   a = (U0, V0, Ax', -Ay')   b = (Bx', -By', opacity, r)   c = (g, b, id, half(zF))
+// (id: the splat id, cap modes; half(zF) bits: MLAB), and the wave lists hold
+// slot byte offsets (u16), so a record's reads take one address VGPR.
 struct StagedRec {
-    float4 a, b;
-    float2 c;
-    uint32_t id;  // splat id (cap modes)
-    uint32_t hd;  // MLAB: half(zF) bits
+    float4 a, b, c;
 };
 static_assert(sizeof(StagedRec) == 48, "staged record slot");
 __device__ __forceinline__ const StagedRec& staged_at(const StagedRec* base, uint32_t off) {
@@ -245,24 +266,43 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     };
     auto body = [&](uint32_t off) {
         const StagedRec& r = staged_at(srec, off);
-        body_v(r.a, r.b, r.c, kIds ? r.id : 0u,
-               MODE == 3 ? __builtin_bit_cast(_Float16, (uint16_t)r.hd) : (_Float16)0.0f);
+        body_v(r.a, r.b, make_float2(r.c.x, r.c.y), kIds ? __float_as_uint(r.c.z) : 0u,
+               MODE == 3 ? __builtin_bit_cast(_Float16, (uint16_t)__float_as_uint(r.c.w)) : (_Float16)0.0f);
     };
 
     // Software pipeline: while batch b is composited, batch b+1's records are
     // in flight into registers and batch b+2's ids are being loaded.
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    // Coalesced gathers: wave w stages records 64w..64w+63 of a batch, and
+    // their 192 16-B chunks are loaded by its 64 lanes three apiece (chunk
+    // c = lane + 64i is part c % 3 of record c / 3), so adjacent lanes read
+    // adjacent bytes of one record; the owner lane of each record collects
+    // its chunks through LDS.  Every lane loads, its list position clamped to
+    // the last entry: a conditional load joins the old and the loaded
+    // registers, and the copy the compiler then emits waits for the load it
+    // was meant to overlap.
+    const uint32_t last = rg.y > rg.x ? rg.y - 1u : rg.x;
+    uint32_t ck[3], cp[3];  // this lane's chunks: record (in the wave's 64) and part
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t c = lane + 64u * (uint32_t)i;
+        ck[i] = c / 3u;
+        cp[i] = c - 3u * ck[i];
+    }
+    float4 rc[3] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f),
+                    make_float4(0.f, 0.f, 0.f, 0.f)};
     uint32_t id_cur = 0, id_next = 0;
-    {
-        const uint32_t j = rg.x + tid;
-        if (j < rg.y) {
-            id_cur = a.vals[j];
-            const float4* rp = a.rec + (size_t)a.rec_stride * id_cur;
-            r0 = rp[0];
-            r1 = rp[1];
-            r2 = rp[2];
+    auto gather = [&](uint32_t own_id) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t idk = (uint32_t)__shfl((int)own_id, (int)ck[i], 64);
+            rc[i] = a.rec[(size_t)a.rec_stride * idk + cp[i]];
         }
-        if (j + kTileThreads < rg.y) id_next = a.vals[j + kTileThreads];
+    };
+    if (rg.y > rg.x) {
+        const uint32_t j = rg.x + tid;
+        id_cur = a.vals[j < last ? j : last];
+        gather(id_cur);
+        id_next = a.vals[j + kTileThreads < last ? j + kTileThreads : last];
     }
     if (lane == 0) GS_CC(0, 1);
     if (tid == 0) GS_CC(6, rg.y - rg.x);
@@ -270,23 +310,36 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     // batch per batch it composites (the early-out stops both)
     const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;  // (empty bins: {~0, 0})
     uint32_t fetched = len < (uint32_t)kTileThreads ? len : (uint32_t)kTileThreads;
+    GS_CT_DECL;
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
+        GS_CT(5);
         if (__syncthreads_count(!finished()) == 0) break;
+        GS_CT(0);
         if (rg.y - b > (uint32_t)kTileThreads) {
             const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
             fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
         }
         if (tid == 0) GS_CC(5, 1);
+        // the wave's gathered chunks into their records' slots (raw layout)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            (cp[i] == 0 ? srec[64u * wave + ck[i]].a : cp[i] == 1 ? srec[64u * wave + ck[i]].b
+                                                                   : srec[64u * wave + ck[i]].c) = rc[i];
+        wave_lds_sync();  // the wave's 64 slots are only touched by this wave until the barrier
         if (b + tid < rg.y) {
             // record (cx, cy, ax, ay) (bx, by, op, r) (g, b, rect_lo, rect_hi)
             // staged for this tile (scaled conic, offsets at the tile origin)
+            StagedRec& st = srec[tid];
+            const float4 r0 = st.a, r1 = st.b, r2 = st.c;
             const float ax = r0.z * kConicScale, ay = r0.w * kConicScale;
             const float bxs = r1.x * kConicScale, bys = r1.y * kConicScale;
             const float ex = ftx0 - r0.x, ey = r0.y - fty0;
-            StagedRec& st = srec[tid];
             st.a = make_float4(__builtin_fmaf(ax, ex, ay * ey), __builtin_fmaf(bxs, ex, bys * ey), ax, -ay);
             st.b = make_float4(bxs, -bys, r1.z, r1.w);
-            st.c = make_float2(r2.x, r2.y);
+            uint32_t sid = 0, shd = 0;
+            if constexpr (kIds) sid = id_cur;
+            if constexpr (MODE == 3) shd = kDepthInf - a.dkey[id_cur];  // half(zF) (dkey = 0x7C00 - half bits)
+            st.c = make_float4(r2.x, r2.y, __uint_as_float(sid), __uint_as_float(shd));
             {
                 // which of the tile's 8x8 quadrants (wave w: column w & 1, row
                 // w >> 1) the record's rect reaches and its cell mask does not
@@ -308,21 +361,15 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 }
                 sqm[tid] = (uint8_t)qm;
             }
-            if constexpr (kIds) st.id = id_cur;
-            if constexpr (MODE == 3)  // half(zF) from the depth key (dkey = 0x7C00 - half bits)
-                st.hd = kDepthInf - a.dkey[id_cur];
         }
+        GS_CT(1);
         __syncthreads();
+        GS_CT(2);
         {
-            const uint32_t j = b + kTileThreads + tid;
-            if (j < rg.y) {
-                id_cur = id_next;
-                const float4* rp = a.rec + (size_t)a.rec_stride * id_cur;
-                r0 = rp[0];
-                r1 = rp[1];
-                r2 = rp[2];
-            }
-            if (j + kTileThreads < rg.y) id_next = a.vals[j + kTileThreads];
+            const uint32_t j = b + 2u * kTileThreads + tid;
+            id_cur = id_next;
+            gather(id_cur);
+            id_next = a.vals[j < last ? j : last];
         }
         const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
         // wave-level compaction of the splats reaching this quadrant (index order kept)
@@ -337,6 +384,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             }
         }
         wave_lds_sync();  // wlist[wave] is only touched by this wave
+        GS_CT(3);
         uint32_t i = 0;
         if constexpr (MODE == 2 || MODE == 3) {
             for (; i < nl; ++i) {
@@ -353,10 +401,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 const StagedRec& p0 = staged_at(srec, w2 & 0xFFFFu);
                 const StagedRec& p1 = staged_at(srec, w2 >> 16);
                 const float4 a0 = p0.a, b0 = p0.b;
-                const float2 c0 = p0.c;
+                const float2 c0 = make_float2(p0.c.x, p0.c.y);
                 const float4 a1 = p1.a, b1 = p1.b;
-                const float2 c1 = p1.c;
-                const uint32_t i0 = kIds ? p0.id : 0u, i1 = kIds ? p1.id : 0u;
+                const float2 c1 = make_float2(p1.c.x, p1.c.y);
+                const uint32_t i0 = kIds ? __float_as_uint(p0.c.z) : 0u, i1 = kIds ? __float_as_uint(p1.c.z) : 0u;
                 if (i + 3 < nl) w2 = wl2[(i >> 1) + 1];
                 body_v(a0, b0, c0, i0, (_Float16)0.0f);
                 body_v(a1, b1, c1, i1, (_Float16)0.0f);
@@ -364,7 +412,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         }
         if (lane == 0) GS_CC(3, i);
+        GS_CT(4);
     }
+    GS_CT_FLUSH();
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
     if (!inside) return;
     if constexpr (SLAB == 1) {
@@ -423,6 +473,13 @@ hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {
 
 }  // namespace gs
 
+#ifdef GS_COMPOSITE_TIMERS
+extern "C" int gs_debug_composite_timers(unsigned long long* out) {
+    unsigned long long zero[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_ct), sizeof zero) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_ct), zero, sizeof zero) != hipSuccess;
+}
+#endif
 #ifdef GS_COMPOSITE_COUNTERS
 extern "C" int gs_debug_composite_counters(unsigned long long* out) {
     unsigned long long zero[8] = {};

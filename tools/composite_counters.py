@@ -33,6 +33,22 @@ V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
 r = InstancedSplatRenderer(scene, Options(mode="tile", sh_degree=args.sh, crop=False))
 r.initialize(0)
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
+if hasattr(lib(), "gs_debug_composite_timers"):  # -DGS_COMPOSITE_TIMERS build: phase cycles per wave
+    f = lib().gs_debug_composite_timers
+    f.argtypes = [C.POINTER(C.c_uint64)]
+    buf = (C.c_uint64 * 8)()
+    for _ in range(2):
+        r.render(V, P, W, H, out=out)
+        torch.cuda.synchronize()
+        f(buf)
+    c = list(buf)
+    nw = max(c[7], 1)
+    tot = c[6] / nw
+    names = ["barrier_count", "staging", "barrier2", "compaction", "walk", "loop tail/prefetch issue"]
+    for n, v in zip(names, c[:6]):
+        print(f"{n:>26}: {v / nw:10.0f} cyc/wave  {100 * v / nw / tot:5.1f} %")
+    print(f"{'wave lifetime':>26}: {tot:10.0f} cyc/wave ({nw} waves)")
+    sys.exit(0)
 f = lib().gs_debug_composite_counters
 f.argtypes = [C.POINTER(C.c_uint64)]
 buf = (C.c_uint64 * 8)()
