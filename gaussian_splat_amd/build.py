@@ -94,6 +94,20 @@ def build_lib(verbose: bool = False, extra: list[str] | None = None, build_dir: 
     return lib
 
 
+DROPIN_SRC = ROOT / "tests" / "cpp" / "dropin_app.cpp"
+DROPIN_BIN = ROOT / "tests" / "cpp" / "dropin_app"
+
+
+def build_dropin_app(lib: Path = LIB) -> Path:
+    """The reference's call sites (main.mm) as a plain C++ program against the
+    drop-in headers and libgsplat.so; run by the GPU tests."""
+    deps = [DROPIN_SRC, lib, *_headers()]
+    if _stale(DROPIN_BIN, deps):
+        _run([_hipcc(), "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(DROPIN_SRC), f"-L{lib.parent}", "-lgsplat",
+              "-Wl,-rpath,$ORIGIN/../../gaussian_splat_amd", "-o", str(DROPIN_BIN)])
+    return DROPIN_BIN
+
+
 def build_oracle() -> None:
     """Test infrastructure: the C oracle and, when /root/reference exists, oracle/_ref."""
     _run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"])
@@ -101,6 +115,7 @@ def build_oracle() -> None:
 
 def build_all(verbose: bool = False) -> Path:
     lib = build_lib(verbose)
+    build_dropin_app(lib)
     build_oracle()
     return lib
 
