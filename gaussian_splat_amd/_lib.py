@@ -53,6 +53,8 @@ SIGNATURES = {
     "gs_create": (C.c_int, [C.c_char_p, C.POINTER(GsOptions), C.POINTER(_P)]),
     "gs_create_from_soa": (C.c_int, [C.POINTER(GsSceneSoa), C.POINTER(GsOptions), C.POINTER(_P)]),
     "gs_create_from_points": (C.c_int, [_P, C.c_int64, C.POINTER(GsOptions), C.POINTER(_P)]),
+    "gs_create_subset": (C.c_int, [_P, C.c_int64, C.c_int64, C.POINTER(_P)]),
+    "gs_get_scene": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "gs_initialize": (C.c_int, [_P, C.c_int32]),
     "gs_point_count": (C.c_int64, [_P]),
     "gs_destroy": (None, [_P]),
@@ -77,6 +79,16 @@ SIGNATURES = {
     "gs_slab_pack": (C.c_int, [_P, _P, _P, C.c_int64, _I64P, _P]),
     "gs_slab_render": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
     "gs_slab_composite": (C.c_int, [_P, _P, _P, _P]),
+    "gs_create_sharded": (C.c_int, [C.c_char_p, C.POINTER(GsOptions), C.c_int32, C.POINTER(_P)]),
+    "gs_create_sharded_from_handle": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
+    "gs_group_initialize": (C.c_int, [_P, _P, C.c_int32]),
+    "gs_group_set_scheme": (C.c_int, [_P, C.c_int32]),
+    "gs_group_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
+    "gs_group_point_count": (C.c_int64, [_P]),
+    "gs_group_size": (C.c_int32, [_P]),
+    "gs_group_transport": (C.c_int32, [_P]),
+    "gs_group_last_stats": (C.c_int, [_P, C.c_int32, C.POINTER(GsStats)]),
+    "gs_group_destroy": (None, [_P]),
     "gs_ply_load": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(_FP), _I64P]),
     "gs_ply_free": (None, [_FP]),
     "gs_look_at": (None, [_FP, _FP, _FP, _FP]),

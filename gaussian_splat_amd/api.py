@@ -322,6 +322,25 @@ class InstancedSplatRenderer:
               "gs_sorted_pairs_host")
         return k, v
 
+    def scene(self) -> Scene:
+        """The loaded (post-crop) scene as host SoA arrays (gs_get_scene)."""
+        n = self.getPointCount()
+        a = {k: np.empty(shape, np.float32) for k, shape in
+             (("pos", (n, 3)), ("rot", (n, 4)), ("scale", (n, 3)), ("opacity", (n,)), ("color", (n, 3)),
+              ("sh_rest", (n, 45)))}
+        check(lib().gs_get_scene(self._h, *(a[k].ctypes.data for k in ("pos", "rot", "scale", "opacity", "color",
+                                                                         "sh_rest"))), "gs_get_scene")
+        return Scene(**a)
+
+    def subset(self, begin: int, end: int) -> "InstancedSplatRenderer":
+        """A renderer over splats [begin, end) of this one's scene (gs_create_subset)."""
+        r = InstancedSplatRenderer.__new__(InstancedSplatRenderer)
+        r.options = Options(**vars(self.options))
+        r._h = C.c_void_p()
+        r.device = None
+        check(lib().gs_create_subset(self._h, int(begin), int(end), C.byref(r._h)), "gs_create_subset")
+        return r
+
     def close(self):
         if self._h:
             lib().gs_destroy(self._h)
@@ -347,3 +366,86 @@ def radix_sort_pairs(keys, vals, bits: int, stream=None):
                                     C.c_void_p(tk.data_ptr()), C.c_void_p(tv.data_ptr()), n, int(bits),
                                     C.c_void_p(stream)), "gs_radix_sort_pairs")
     return keys, vals
+
+
+SCHEMES = {"rows": 0, "slabs": 1}          # gs_scheme
+TRANSPORTS = {"auto": 0, "rccl": 1, "copy": 2}  # gs_transport
+
+
+class ShardedGroup:
+    """Multi-GPU frames from one process (gs_create_sharded):
+    one contiguous splat-index shard per device, frames into devices[0] by
+    the bin-row scheme (bit-identical to one GPU) or the depth-slab scheme;
+    RCCL when every rank has its own device, peer copies otherwise."""
+
+    def __init__(self, source, num_gpus: int, options: Optional[Options] = None):
+        self.options = options or Options()
+        self._g = C.c_void_p()
+        if isinstance(source, InstancedSplatRenderer):
+            check(lib().gs_create_sharded_from_handle(source._h, int(num_gpus), C.byref(self._g)),
+                  "gs_create_sharded_from_handle")
+        else:
+            opt = self.options.to_c()
+            check(lib().gs_create_sharded(str(source).encode(), C.byref(opt), int(num_gpus), C.byref(self._g)),
+                  "gs_create_sharded")
+        self.device = None
+
+    def initialize(self, devices=None, transport: str = "auto") -> bool:
+        arr = None
+        if devices is not None:
+            d = np.ascontiguousarray(devices, np.int32)
+            assert d.shape == (self.size,)
+            arr = d.ctypes.data
+            self._devices = d
+        check(lib().gs_group_initialize(self._g, arr, TRANSPORTS[transport]), "gs_group_initialize")
+        self.device = int(devices[0]) if devices is not None else 0
+        return True
+
+    @property
+    def size(self) -> int:
+        return int(lib().gs_group_size(self._g))
+
+    @property
+    def transport(self) -> str:
+        t = int(lib().gs_group_transport(self._g))
+        return {v: k for k, v in TRANSPORTS.items()}.get(t, "none")
+
+    def getPointCount(self) -> int:
+        return int(lib().gs_group_point_count(self._g))
+
+    def set_scheme(self, scheme: str):
+        check(lib().gs_group_set_scheme(self._g, SCHEMES[scheme]), "gs_group_set_scheme")
+
+    def render(self, view, proj, width: int, height: int, out=None, stream=None):
+        import torch
+
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.float32, device=f"cuda:{self.device or 0}")
+        assert out.is_cuda and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == width * height * 4
+        if stream is None:
+            stream = torch.cuda.current_stream(out.device).cuda_stream
+        check(lib().gs_group_render(self._g, _mat16(view), _mat16(proj), int(width), int(height),
+                                    C.c_void_p(out.data_ptr()), 1, C.c_void_p(stream)), "gs_group_render")
+        return out
+
+    def render_host(self, view, proj, width: int, height: int) -> np.ndarray:
+        out = np.empty((height, width, 4), np.float32)
+        check(lib().gs_group_render(self._g, _mat16(view), _mat16(proj), int(width), int(height), out.ctypes.data,
+                                    0, None), "gs_group_render")
+        return out
+
+    def last_stats(self, rank: int = 0) -> dict:
+        s = GsStats()
+        check(lib().gs_group_last_stats(self._g, int(rank), C.byref(s)), "gs_group_last_stats")
+        return s.as_dict()
+
+    def close(self):
+        if self._g:
+            lib().gs_group_destroy(self._g)
+            self._g = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -21,8 +21,8 @@ BUILD = ROOT / "build" / "gsplat"
 LIB = PKG / "libgsplat.so"
 ARCH = os.environ.get("GSPLAT_ARCH", "gfx950")
 
-HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "host" / "renderer.cpp"]
-CXX_SOURCES = [CSRC / "host" / "ply_loader.cpp", CSRC / "host" / "camera.cpp",
+HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "host" / "renderer.cpp", CSRC / "host" / "group.cpp"]
+CXX_SOURCES = [CSRC / "host" / "ply_loader.cpp", CSRC / "host" / "scene_io.cpp", CSRC / "host" / "camera.cpp",
                CSRC / "host" / "instanced_splat_renderer.cpp", CSRC / "host" / "renderable.cpp"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
@@ -90,7 +90,7 @@ def build_lib(verbose: bool = False, extra: list[str] | None = None, build_dir: 
     if jobs or _stale(lib, objs):
         lib.parent.mkdir(parents=True, exist_ok=True)
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
-              "-lpthread"])
+              "-lpthread", "-ldl"])
     return lib
 
 

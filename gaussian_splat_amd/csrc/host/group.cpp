@@ -1,0 +1,634 @@
+// group.cpp — multi-GPU frames from one host process (gs_create_sharded,
+// SURVEY §8(b)/(e)).  No reference counterpart: the reference renders on one
+// Metal device.
+//
+// A group owns one shard handle per GPU: contiguous splat-index ranges of the
+// (cropped) scene, made with gs_create_subset.  A frame runs the same per-rank
+// C-ABI steps as the one-process-per-GPU path (gaussian_splat_amd/
+// distributed.py), driven here by one worker thread per rank:
+//
+//   rows  (default; the frame is bit-identical to one GPU's)
+//     gs_shard_project -> all-to-all of exchange records -> gs_shard_render
+//     -> each rank's band of bin rows into the frame on devices[0]
+//   slabs (the north star's depth slabs + RGBA reduce)
+//     gs_slab_project -> all-reduce of the depth histogram -> gs_slab_pack
+//     -> all-to-all -> gs_slab_render -> all-gather of the transmittance
+//     -> gs_slab_composite -> reduce (SUM) of the contributions on devices[0]
+//
+// Transport: RCCL over xGMI (ncclCommInitAll, grouped ncclSend/ncclRecv,
+// ncclAllReduce / ncclAllGather / ncclReduce) when every rank has its own
+// device, loaded at gs_group_initialize; GS_TRANSPORT_COPY moves the same
+// bytes with peer copies (hipMemcpyPeerAsync) and sums slab contributions
+// on devices[0] in rank order — the only choice when ranks share a device
+// (virtual ranks on one GPU, the tests' configuration).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../kernels/gs_kernels.h"
+#include "gs_internal.h"
+#include "gsplat.h"
+
+namespace {
+
+gs_status gfail(gs_status s, const std::string& msg) {
+    gs_set_last_error(msg);
+    return s;
+}
+
+#define GG_HIP(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return gfail(e_ == hipErrorOutOfMemory ? GS_ERR_OOM : GS_ERR_DEVICE,                   \
+                         std::string(#expr) + ": " + hipGetErrorString(e_));                       \
+    } while (0)
+
+// RCCL entry points, resolved at gs_group_initialize (no link-time
+// dependency: a process that never builds an RCCL group never loads it).
+struct Rccl {
+    void* so = nullptr;
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool load(std::string* why) {
+        if (so) return true;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            so = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (so) break;
+        }
+        if (!so) {
+            *why = std::string("RCCL not loadable: ") + dlerror();
+            return false;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(so, name));
+            ok = ok && fn != nullptr;
+        };
+        sym(comm_init_all, "ncclCommInitAll");
+        sym(comm_destroy, "ncclCommDestroy");
+        sym(group_start, "ncclGroupStart");
+        sym(group_end, "ncclGroupEnd");
+        sym(send, "ncclSend");
+        sym(recv, "ncclRecv");
+        sym(all_reduce, "ncclAllReduce");
+        sym(all_gather, "ncclAllGather");
+        sym(reduce, "ncclReduce");
+        sym(error_string, "ncclGetErrorString");
+        if (!ok) *why = "RCCL: missing symbols";
+        return ok;
+    }
+};
+Rccl g_rccl;
+
+#define GG_NCCL(expr)                                                                                \
+    do {                                                                                             \
+        ncclResult_t r_ = (expr);                                                                    \
+        if (r_ != ncclSuccess)                                                                       \
+            return gfail(GS_ERR_COMM, std::string(#expr) + ": " + g_rccl.error_string(r_));          \
+    } while (0)
+
+// One worker thread per rank; run(f) executes f(rank) on every worker and
+// returns once all are done.
+class Pool {
+public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(const std::function<void(int)>& f) {
+        std::unique_lock<std::mutex> l(mu_);
+        job_ = &f;
+        pending_ = (int)th_.size();
+        ++gen_;
+        cv_.notify_all();
+        done_.wait(l, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                job = job_;
+            }
+            (*job)(i);
+            std::lock_guard<std::mutex> l(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool quit_ = false;
+};
+
+struct DevMem {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    int dev = -1;
+    void release() {
+        if (ptr) {
+            (void)hipSetDevice(dev);
+            (void)hipFree(ptr);
+        }
+        ptr = nullptr;
+        bytes = 0;
+    }
+    hipError_t reserve(int device, size_t want) {
+        if (want <= bytes && device == dev) return hipSuccess;
+        release();
+        dev = device;
+        size_t b = std::max<size_t>(want + want / 8, 256);
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipMalloc(&ptr, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(ptr); }
+};
+
+struct Rank {
+    gs_handle* h = nullptr;
+    int dev = 0;
+    int64_t base = 0;
+    hipStream_t st = nullptr;  // rank 0: the caller's stream during a frame
+    bool own_stream = false;
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    DevMem send, recv, band, hist, tloc, tall, contrib, stage;
+    std::vector<int64_t> counts;  // records to each rank
+    gs_status status = GS_OK;
+    std::string error;
+};
+
+}  // namespace
+
+struct gs_group {
+    gs_options opt{};
+    int world = 1;
+    int64_t n = 0;
+    int scheme = GS_SCHEME_ROWS;
+    int transport = GS_TRANSPORT_COPY;
+    bool initialized = false;
+    std::vector<Rank> r;
+    std::vector<ncclComm_t> comms;
+    Pool* pool = nullptr;
+    hipEvent_t frame_done = nullptr;  // on devices[0]: everything of the last frame
+    DevMem fb;                        // host-output frames
+    gs_stats stats{};
+    ~gs_group() {
+        delete pool;
+        for (auto& k : r) {
+            if (k.dev >= 0) (void)hipSetDevice(k.dev);
+            for (DevMem* m : {&k.send, &k.recv, &k.band, &k.hist, &k.tloc, &k.tall, &k.contrib, &k.stage}) m->release();
+            if (k.own_stream && k.st) (void)hipStreamDestroy(k.st);
+            if (k.ev_ready) (void)hipEventDestroy(k.ev_ready);
+            if (k.ev_done) (void)hipEventDestroy(k.ev_done);
+            gs_destroy(k.h);
+        }
+        for (ncclComm_t c : comms)
+            if (c) (void)g_rccl.comm_destroy(c);
+        if (frame_done) (void)hipEventDestroy(frame_done);
+        fb.release();
+    }
+};
+
+namespace {
+
+// f(rank) on every rank's worker (device set); the first failure's status and
+// gs_last_error text are passed to the caller's thread.
+gs_status run_ranks(gs_group* g, const std::function<gs_status(Rank&, int)>& f) {
+    std::function<void(int)> job = [&](int i) {
+        Rank& k = g->r[(size_t)i];
+        if (hipSetDevice(k.dev) != hipSuccess) {
+            k.status = GS_ERR_DEVICE;
+            k.error = "hipSetDevice";
+            return;
+        }
+        k.status = f(k, i);
+        k.error = k.status == GS_OK ? std::string() : std::string(gs_last_error());
+    };
+    g->pool->run(job);
+    for (auto& k : g->r)
+        if (k.status != GS_OK) return gfail(k.status, "rank: " + k.error);
+    return GS_OK;
+}
+
+// Row ownership of the default table (gs_shard_set_rows not used by groups):
+// rank d owns bin rows [d*R/world, (d+1)*R/world).
+void owned_rows(int H, int world, int d, int* row0, int* nrows) {
+    const int R = (H + gs::kBin - 1) / gs::kBin;
+    *row0 = (int)((int64_t)d * R / world);
+    *nrows = (int)((int64_t)(d + 1) * R / world) - *row0;
+}
+
+// All-to-all of the exchange records: rank d receives, in source-rank order,
+// the records every rank packed for it.  Returns the received counts.
+gs_status exchange(gs_group* g, std::vector<int64_t>* nrec) {
+    const int W = g->world;
+    const int64_t xb = gs_exchange_record_bytes();
+    nrec->assign((size_t)W, 0);
+    for (int d = 0; d < W; ++d)
+        for (int s = 0; s < W; ++s) (*nrec)[(size_t)d] += g->r[(size_t)s].counts[(size_t)d];
+    for (int d = 0; d < W; ++d) GG_HIP(g->r[(size_t)d].recv.reserve(g->r[(size_t)d].dev, (size_t)std::max<int64_t>((*nrec)[(size_t)d], 1) * xb));
+    auto soff = [&](int s, int d) {  // offset (records) of s's group for d in its send buffer
+        int64_t o = 0;
+        for (int j = 0; j < d; ++j) o += g->r[(size_t)s].counts[(size_t)j];
+        return o;
+    };
+    auto roff = [&](int d, int s) {  // offset of s's records in d's receive buffer
+        int64_t o = 0;
+        for (int j = 0; j < s; ++j) o += g->r[(size_t)j].counts[(size_t)d];
+        return o;
+    };
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int s = 0; s < W; ++s) {
+            Rank& k = g->r[(size_t)s];
+            for (int d = 0; d < W; ++d) {
+                const int64_t cs = k.counts[(size_t)d], cr = g->r[(size_t)d].counts[(size_t)s];
+                if (cs > 0)
+                    GG_NCCL(g_rccl.send(k.send.as<char>() + soff(s, d) * xb, (size_t)(cs * xb), ncclUint8, d,
+                                        g->comms[(size_t)s], k.st));
+                if (cr > 0)
+                    GG_NCCL(g_rccl.recv(k.recv.as<char>() + roff(s, d) * xb, (size_t)(cr * xb), ncclUint8, d,
+                                        g->comms[(size_t)s], k.st));
+            }
+        }
+        GG_NCCL(g_rccl.group_end());
+        return GS_OK;
+    }
+    for (int d = 0; d < W; ++d) {
+        Rank& k = g->r[(size_t)d];
+        GG_HIP(hipSetDevice(k.dev));
+        for (int s = 0; s < W; ++s) {
+            const int64_t c = g->r[(size_t)s].counts[(size_t)d];
+            if (c <= 0) continue;
+            GG_HIP(hipStreamWaitEvent(k.st, g->r[(size_t)s].ev_ready, 0));
+            GG_HIP(hipMemcpyPeerAsync(k.recv.as<char>() + roff(d, s) * xb, k.dev,
+                                      g->r[(size_t)s].send.as<char>() + soff(s, d) * xb, g->r[(size_t)s].dev,
+                                      (size_t)(c * xb), k.st));
+        }
+    }
+    return GS_OK;
+}
+
+gs_status render_rows(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out) {
+    const int W = g->world;
+    const int64_t xb = gs_exchange_record_bytes();
+    gs_status s = run_ranks(g, [&](Rank& k, int) -> gs_status {
+        const size_t cap = (size_t)std::max<int64_t>(gs_point_count(k.h), 1) * (size_t)W * (size_t)xb;
+        GG_HIP(k.send.reserve(k.dev, cap));
+        k.counts.assign((size_t)W, 0);
+        gs_status st = gs_shard_project(k.h, V, P, Wd, Ht, k.send.ptr, (int64_t)k.send.bytes, k.counts.data(), k.st);
+        if (st != GS_OK) return st;
+        GG_HIP(hipEventRecord(k.ev_ready, k.st));
+        return GS_OK;
+    });
+    if (s != GS_OK) return s;
+    std::vector<int64_t> nrec;
+    if ((s = exchange(g, &nrec)) != GS_OK) return s;
+    if ((s = run_ranks(g, [&](Rank& k, int d) -> gs_status {
+             int row0, nrows;
+             owned_rows(Ht, W, d, &row0, &nrows);
+             GG_HIP(k.band.reserve(k.dev, (size_t)std::max(nrows, 1) * gs::kBin * Wd * 16));
+             gs_status st = gs_shard_render(k.h, k.recv.ptr, nrec[(size_t)d], Wd, Ht, k.band.as<float>(), k.st);
+             if (st != GS_OK) return st;
+             GG_HIP(hipEventRecord(k.ev_done, k.st));
+             return GS_OK;
+         })) != GS_OK)
+        return s;
+    // bands (owned rows stacked, contiguous under the default table) into the frame
+    Rank& r0 = g->r[0];
+    auto span = [&](int d, size_t* off, size_t* bytes) {
+        int row0, nrows;
+        owned_rows(Ht, W, d, &row0, &nrows);
+        const int y0 = row0 * gs::kBin, y1 = std::min(Ht, (row0 + nrows) * gs::kBin);
+        *off = (size_t)y0 * Wd * 4;
+        *bytes = y1 > y0 ? (size_t)(y1 - y0) * Wd * 16 : 0;
+    };
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int d = 1; d < W; ++d) {
+            size_t off, bytes;
+            span(d, &off, &bytes);
+            if (!bytes) continue;
+            GG_NCCL(g_rccl.send(g->r[(size_t)d].band.ptr, bytes, ncclUint8, 0, g->comms[(size_t)d], g->r[(size_t)d].st));
+            GG_NCCL(g_rccl.recv(out + off, bytes, ncclUint8, d, g->comms[0], r0.st));
+        }
+        GG_NCCL(g_rccl.group_end());
+        size_t off, bytes;
+        span(0, &off, &bytes);
+        GG_HIP(hipSetDevice(r0.dev));
+        if (bytes) GG_HIP(hipMemcpyAsync(out + off, r0.band.ptr, bytes, hipMemcpyDeviceToDevice, r0.st));
+        for (int d = 1; d < W; ++d) {  // the senders' streams are done with their bands
+            GG_HIP(hipSetDevice(g->r[(size_t)d].dev));
+            GG_HIP(hipEventRecord(g->r[(size_t)d].ev_done, g->r[(size_t)d].st));
+        }
+        GG_HIP(hipSetDevice(r0.dev));
+        for (int d = 1; d < W; ++d) GG_HIP(hipStreamWaitEvent(r0.st, g->r[(size_t)d].ev_done, 0));
+        return GS_OK;
+    }
+    GG_HIP(hipSetDevice(r0.dev));
+    for (int d = 0; d < W; ++d) {
+        size_t off, bytes;
+        span(d, &off, &bytes);
+        if (!bytes) continue;
+        GG_HIP(hipStreamWaitEvent(r0.st, g->r[(size_t)d].ev_done, 0));
+        GG_HIP(hipMemcpyPeerAsync(out + off, r0.dev, g->r[(size_t)d].band.ptr, g->r[(size_t)d].dev, bytes, r0.st));
+    }
+    return GS_OK;
+}
+
+gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out) {
+    const int W = g->world;
+    const int64_t xb = gs_exchange_record_bytes();
+    const size_t npx = (size_t)Wd * Ht;
+    gs_status s = run_ranks(g, [&](Rank& k, int) -> gs_status {
+        GG_HIP(k.hist.reserve(k.dev, GS_SLAB_BINS * 8));
+        gs_status st = gs_slab_project(k.h, V, P, Wd, Ht, k.hist.as<uint64_t>(), k.st);
+        if (st != GS_OK) return st;
+        GG_HIP(hipEventRecord(k.ev_ready, k.st));
+        return GS_OK;
+    });
+    if (s != GS_OK) return s;
+    // histogram all-reduce -> the same slab bounds on every rank
+    std::vector<uint64_t> hsum(GS_SLAB_BINS, 0), hk(GS_SLAB_BINS);
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int i = 0; i < W; ++i)
+            GG_NCCL(g_rccl.all_reduce(g->r[(size_t)i].hist.ptr, g->r[(size_t)i].hist.ptr, GS_SLAB_BINS, ncclUint64, ncclSum,
+                                      g->comms[(size_t)i], g->r[(size_t)i].st));
+        GG_NCCL(g_rccl.group_end());
+        GG_HIP(hipSetDevice(g->r[0].dev));
+        GG_HIP(hipMemcpyAsync(hsum.data(), g->r[0].hist.ptr, GS_SLAB_BINS * 8, hipMemcpyDeviceToHost, g->r[0].st));
+        GG_HIP(hipStreamSynchronize(g->r[0].st));
+    } else {
+        for (int i = 0; i < W; ++i) {
+            GG_HIP(hipSetDevice(g->r[(size_t)i].dev));
+            GG_HIP(hipMemcpyAsync(hk.data(), g->r[(size_t)i].hist.ptr, GS_SLAB_BINS * 8, hipMemcpyDeviceToHost,
+                                  g->r[(size_t)i].st));
+            GG_HIP(hipStreamSynchronize(g->r[(size_t)i].st));
+            for (int b = 0; b < GS_SLAB_BINS; ++b) hsum[(size_t)b] += hk[(size_t)b];
+        }
+    }
+    std::vector<uint32_t> bounds((size_t)W + 1);
+    if ((s = gs_slab_bounds(hsum.data(), W, bounds.data())) != GS_OK) return s;
+    if ((s = run_ranks(g, [&](Rank& k, int) -> gs_status {
+             const size_t cap = (size_t)std::max<int64_t>(gs_point_count(k.h), 1) * (size_t)xb;
+             GG_HIP(k.send.reserve(k.dev, cap));
+             k.counts.assign((size_t)W, 0);
+             gs_status st = gs_slab_pack(k.h, bounds.data(), k.send.ptr, (int64_t)k.send.bytes, k.counts.data(), k.st);
+             if (st != GS_OK) return st;
+             GG_HIP(hipEventRecord(k.ev_ready, k.st));
+             return GS_OK;
+         })) != GS_OK)
+        return s;
+    std::vector<int64_t> nrec;
+    if ((s = exchange(g, &nrec)) != GS_OK) return s;
+    if ((s = run_ranks(g, [&](Rank& k, int d) -> gs_status {
+             GG_HIP(k.tloc.reserve(k.dev, npx * 4));
+             GG_HIP(k.tall.reserve(k.dev, npx * 4 * (size_t)W));
+             GG_HIP(k.contrib.reserve(k.dev, npx * 16));
+             gs_status st = gs_slab_render(k.h, k.recv.ptr, nrec[(size_t)d], Wd, Ht, k.tloc.as<float>(), k.st);
+             if (st != GS_OK) return st;
+             GG_HIP(hipEventRecord(k.ev_ready, k.st));
+             return GS_OK;
+         })) != GS_OK)
+        return s;
+    // all-gather of the slabs' transmittance, rank-major
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int i = 0; i < W; ++i)
+            GG_NCCL(g_rccl.all_gather(g->r[(size_t)i].tloc.ptr, g->r[(size_t)i].tall.ptr, npx, ncclFloat32,
+                                      g->comms[(size_t)i], g->r[(size_t)i].st));
+        GG_NCCL(g_rccl.group_end());
+    } else {
+        for (int d = 0; d < W; ++d) {
+            Rank& k = g->r[(size_t)d];
+            GG_HIP(hipSetDevice(k.dev));
+            for (int j = 0; j < W; ++j) {
+                GG_HIP(hipStreamWaitEvent(k.st, g->r[(size_t)j].ev_ready, 0));
+                GG_HIP(hipMemcpyPeerAsync(k.tall.as<float>() + (size_t)j * npx, k.dev, g->r[(size_t)j].tloc.ptr,
+                                          g->r[(size_t)j].dev, npx * 4, k.st));
+            }
+        }
+    }
+    if ((s = run_ranks(g, [&](Rank& k, int) -> gs_status {
+             gs_status st = gs_slab_composite(k.h, k.tall.as<float>(), k.contrib.as<float>(), k.st);
+             if (st != GS_OK) return st;
+             GG_HIP(hipEventRecord(k.ev_done, k.st));
+             return GS_OK;
+         })) != GS_OK)
+        return s;
+    // RGBA + weight reduce (SUM) into the frame on devices[0]
+    Rank& r0 = g->r[0];
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int i = 0; i < W; ++i)
+            GG_NCCL(g_rccl.reduce(g->r[(size_t)i].contrib.ptr, i == 0 ? (void*)out : g->r[(size_t)i].contrib.ptr,
+                                  npx * 4, ncclFloat32, ncclSum, 0, g->comms[(size_t)i], g->r[(size_t)i].st));
+        GG_NCCL(g_rccl.group_end());
+        for (int d = 1; d < W; ++d) {
+            GG_HIP(hipSetDevice(g->r[(size_t)d].dev));
+            GG_HIP(hipEventRecord(g->r[(size_t)d].ev_done, g->r[(size_t)d].st));
+        }
+        GG_HIP(hipSetDevice(r0.dev));
+        for (int d = 1; d < W; ++d) GG_HIP(hipStreamWaitEvent(r0.st, g->r[(size_t)d].ev_done, 0));
+        return GS_OK;
+    }
+    // rank order: frame = c0, frame += c1, ... (the virtual-slab reference's order)
+    GG_HIP(hipSetDevice(r0.dev));
+    GG_HIP(r0.stage.reserve(r0.dev, npx * 16));
+    GG_HIP(hipMemcpyAsync(out, r0.contrib.ptr, npx * 16, hipMemcpyDeviceToDevice, r0.st));
+    for (int d = 1; d < W; ++d) {
+        GG_HIP(hipStreamWaitEvent(r0.st, g->r[(size_t)d].ev_done, 0));
+        GG_HIP(hipMemcpyPeerAsync(r0.stage.ptr, r0.dev, g->r[(size_t)d].contrib.ptr, g->r[(size_t)d].dev, npx * 16,
+                                  r0.st));
+        GG_HIP(gs::launch_accumulate(reinterpret_cast<float4*>(out), r0.stage.as<const float4>(), npx, r0.st));
+    }
+    return GS_OK;
+}
+
+gs_status make_group(gs_handle* scene, int32_t num_gpus, gs_group** out) {
+    if (num_gpus < 1 || num_gpus > gs::kMaxWorld) return gfail(GS_ERR_INVALID_ARG, "num_gpus must be 1..32");
+    gs_group* g = new gs_group();
+    g->world = num_gpus;
+    g->n = gs_point_count(scene);
+    g->r.resize((size_t)num_gpus);
+    for (int i = 0; i < num_gpus; ++i) {
+        Rank& k = g->r[(size_t)i];
+        k.dev = -1;
+        k.base = g->n * i / num_gpus;
+        const int64_t e = g->n * (i + 1) / num_gpus;
+        gs_status s = gs_create_subset(scene, k.base, e, &k.h);
+        if (s == GS_OK) s = gs_shard_configure(k.h, i, num_gpus, k.base);
+        if (s != GS_OK) {
+            delete g;
+            return s;
+        }
+    }
+    *out = g;
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gs_status gs_create_sharded_from_handle(const gs_handle* scene, int32_t num_gpus, gs_group** out) {
+    if (!out || !scene) return gfail(GS_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return make_group(const_cast<gs_handle*>(scene), num_gpus, out);
+}
+
+gs_status gs_create_sharded(const char* ply_path, const gs_options* opt, int32_t num_gpus, gs_group** out) {
+    if (!out || !ply_path) return gfail(GS_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    gs_handle* scene = nullptr;
+    gs_status s = gs_create(ply_path, opt, &scene);
+    if (s != GS_OK) return s;
+    s = make_group(scene, num_gpus, out);
+    gs_destroy(scene);
+    return s;
+}
+
+gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t transport) {
+    if (!g) return gfail(GS_ERR_INVALID_ARG, "null group");
+    if (g->initialized) return gfail(GS_ERR_STATE, "group already initialized");
+    int count = 0;
+    GG_HIP(hipGetDeviceCount(&count));
+    std::vector<int> dev((size_t)g->world);
+    for (int i = 0; i < g->world; ++i) {
+        dev[(size_t)i] = devices ? devices[i] : i;
+        if (dev[(size_t)i] < 0 || dev[(size_t)i] >= count)
+            return gfail(GS_ERR_DEVICE, "no HIP device " + std::to_string(dev[(size_t)i]));
+    }
+    std::vector<int> sorted = dev;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (transport == GS_TRANSPORT_AUTO) transport = (distinct && g->world > 1) ? GS_TRANSPORT_RCCL : GS_TRANSPORT_COPY;
+    if (transport != GS_TRANSPORT_RCCL && transport != GS_TRANSPORT_COPY)
+        return gfail(GS_ERR_INVALID_ARG, "bad transport");
+    if (transport == GS_TRANSPORT_RCCL && !distinct)
+        return gfail(GS_ERR_INVALID_ARG, "RCCL needs one device per rank (GS_TRANSPORT_COPY for shared devices)");
+    for (int i = 0; i < g->world; ++i) {
+        Rank& k = g->r[(size_t)i];
+        k.dev = dev[(size_t)i];
+        gs_status s = gs_initialize(k.h, k.dev);
+        if (s != GS_OK) return s;
+        GG_HIP(hipSetDevice(k.dev));
+        if (i > 0) {
+            GG_HIP(hipStreamCreateWithFlags(&k.st, hipStreamNonBlocking));
+            k.own_stream = true;
+        }
+        GG_HIP(hipEventCreateWithFlags(&k.ev_ready, hipEventDisableTiming));
+        GG_HIP(hipEventCreateWithFlags(&k.ev_done, hipEventDisableTiming));
+    }
+    if (transport == GS_TRANSPORT_COPY && distinct) {  // direct peer access over xGMI where the devices allow it
+        for (int a = 0; a < g->world; ++a)
+            for (int b = 0; b < g->world; ++b) {
+                int can = 0;
+                if (a == b || hipDeviceCanAccessPeer(&can, dev[(size_t)a], dev[(size_t)b]) != hipSuccess || !can) continue;
+                GG_HIP(hipSetDevice(dev[(size_t)a]));
+                hipError_t e = hipDeviceEnablePeerAccess(dev[(size_t)b], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GG_HIP(e);
+                (void)hipGetLastError();
+            }
+    }
+    if (transport == GS_TRANSPORT_RCCL) {
+        std::string why;
+        if (!g_rccl.load(&why)) return gfail(GS_ERR_COMM, why);
+        g->comms.assign((size_t)g->world, nullptr);
+        GG_NCCL(g_rccl.comm_init_all(g->comms.data(), g->world, dev.data()));
+    }
+    GG_HIP(hipSetDevice(dev[0]));
+    GG_HIP(hipEventCreateWithFlags(&g->frame_done, hipEventDisableTiming));
+    g->transport = transport;
+    g->pool = new Pool(g->world);
+    g->initialized = true;
+    return GS_OK;
+}
+
+gs_status gs_group_set_scheme(gs_group* g, int32_t scheme) {
+    if (!g || (scheme != GS_SCHEME_ROWS && scheme != GS_SCHEME_SLABS))
+        return gfail(GS_ERR_INVALID_ARG, "scheme must be GS_SCHEME_ROWS or GS_SCHEME_SLABS");
+    g->scheme = scheme;
+    return GS_OK;
+}
+
+int64_t gs_group_point_count(const gs_group* g) { return g ? g->n : 0; }
+int32_t gs_group_size(const gs_group* g) { return g ? g->world : 0; }
+int32_t gs_group_transport(const gs_group* g) { return g && g->initialized ? g->transport : -1; }
+
+gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int32_t width, int32_t height,
+                          float* out_rgba, int32_t out_is_device, void* hip_stream) {
+    if (!g || !g->initialized) return gfail(GS_ERR_STATE, "gs_group_initialize not called");
+    if (!view || !proj || !out_rgba || width <= 0 || height <= 0)
+        return gfail(GS_ERR_INVALID_ARG, "gs_group_render: bad arguments");
+    Rank& r0 = g->r[0];
+    GG_HIP(hipSetDevice(r0.dev));
+    r0.st = static_cast<hipStream_t>(hip_stream);
+    float* out = out_rgba;
+    const size_t bytes = (size_t)width * height * 16;
+    if (!out_is_device) {
+        GG_HIP(g->fb.reserve(r0.dev, bytes));
+        out = g->fb.as<float>();
+    }
+    // the last frame is done everywhere (its gather waited for every rank)
+    GG_HIP(hipEventSynchronize(g->frame_done));
+    gs_status s = g->world == 1 ? gs_render(r0.h, view, proj, width, height, out, 1, r0.st)
+                 : g->scheme == GS_SCHEME_SLABS ? render_slabs(g, view, proj, width, height, out)
+                                                : render_rows(g, view, proj, width, height, out);
+    if (s != GS_OK) return s;
+    GG_HIP(hipSetDevice(r0.dev));
+    GG_HIP(hipEventRecord(g->frame_done, r0.st));
+    if (!out_is_device) {
+        GG_HIP(hipMemcpyAsync(out_rgba, out, bytes, hipMemcpyDeviceToHost, r0.st));
+        GG_HIP(hipStreamSynchronize(r0.st));
+    }
+    return gs_last_stats(r0.h, &g->stats);
+}
+
+gs_status gs_group_last_stats(gs_group* g, int32_t rank, gs_stats* out) {
+    if (!g || !out || rank < 0 || rank >= g->world) return gfail(GS_ERR_INVALID_ARG, "gs_group_last_stats: bad arguments");
+    return gs_last_stats(g->r[(size_t)rank].h, out);
+}
+
+void gs_group_destroy(gs_group* g) { delete g; }
+
+}  // extern "C"

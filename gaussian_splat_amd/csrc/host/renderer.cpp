@@ -22,6 +22,8 @@
 #include "../kernels/gs_kernels.h"
 #include "gsplat.h"
 #include "gsplat/ply_loader.h"
+#include "gs_internal.h"
+#include "scene_io.h"
 
 namespace {
 
@@ -62,16 +64,18 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(ptr); }
 };
 
-int sh_coeffs(int deg) { return deg <= 0 ? 0 : (deg == 1 ? 3 : (deg == 2 ? 8 : 15)); }
+using gsio::sh_coeffs;
 
 }  // namespace
 
+// (gs_internal.h) the calling thread's gs_last_error() text
+void gs_set_last_error(const std::string& msg) { g_last_error = msg; }
+
 struct gs_handle {
     gs_options opt{};
-    // host SoA (post-crop)
+    // host copy of the scene (post-crop) in the HBM plane layout (scene_io.h)
     int64_t n = 0;
-    std::vector<float> pos, rot, scale, opacity, color, sh_rest;
-    bool has_sh = false;
+    gsio::HostPlanes hp;
     // device
     int device = -1;
     bool initialized = false;
@@ -181,10 +185,7 @@ struct gs_handle {
 
 namespace {
 
-// Crop (instanced_splat_renderer.mm:382-386) and store SoA.
-gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& opt) {
-    if (!sc || sc->n < 0 || (sc->n > 0 && (!sc->pos || !sc->rot || !sc->scale || !sc->opacity || !sc->color)))
-        return fail(GS_ERR_INVALID_ARG, "gs_scene_soa: null array");
+gs_status check_options(const gs_options& opt) {
     if (opt.sh_degree < 0 || opt.sh_degree > 3) return fail(GS_ERR_INVALID_ARG, "sh_degree must be 0..3");
     if (opt.cap < 0) return fail(GS_ERR_INVALID_ARG, "cap must be >= 0");
     if (opt.mode != GS_MODE_TILE && opt.mode != GS_MODE_LIVE50 && opt.mode != GS_MODE_MLAB)
@@ -192,57 +193,36 @@ gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& op
     if (opt.frames_in_flight < 0 || opt.frames_in_flight > 2)
         return fail(GS_ERR_INVALID_ARG, "frames_in_flight must be 1 or 2");
     if (opt.binning < 0 || opt.binning > 2) return fail(GS_ERR_INVALID_ARG, "binning must be 0, 1 or 2");
-    if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
-    if (sc->n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
-    h->opt = opt;
-    h->has_sh = opt.sh_degree > 0;
-    std::vector<int64_t> keep;
-    keep.reserve((size_t)sc->n);
-    const float r = opt.crop_radius;
-    for (int64_t i = 0; i < sc->n; ++i) {
-        const float* p = sc->pos + i * 3;
-        if (!opt.crop || (std::fabs(p[0]) < r && std::fabs(p[1]) < r && std::fabs(p[2]) < r)) keep.push_back(i);
-    }
-    const int64_t m = (int64_t)keep.size();
-    h->n = m;
-    h->pos.resize(m * 3);
-    h->rot.resize(m * 4);
-    h->scale.resize(m * 3);
-    h->opacity.resize(m);
-    h->color.resize(m * 3);
-    if (h->has_sh) h->sh_rest.resize(m * 45);
-    for (int64_t k = 0; k < m; ++k) {
-        int64_t i = keep[k];
-        std::memcpy(&h->pos[k * 3], sc->pos + i * 3, 12);
-        std::memcpy(&h->rot[k * 4], sc->rot + i * 4, 16);
-        std::memcpy(&h->scale[k * 3], sc->scale + i * 3, 12);
-        h->opacity[k] = sc->opacity[i];
-        std::memcpy(&h->color[k * 3], sc->color + i * 3, 12);
-        if (h->has_sh) std::memcpy(&h->sh_rest[k * 45], sc->sh_rest + i * 45, 45 * 4);
-    }
     return GS_OK;
+}
+
+gs_status adopt_planes(gs_handle* h, gs_status built, const gs_options& opt) {
+    if (built == GS_ERR_OOM) return fail(GS_ERR_OOM, "host scene planes");
+    if (built != GS_OK) return built;
+    if (h->hp.n >= (int64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
+    h->opt = opt;
+    h->n = h->hp.n;
+    return GS_OK;
+}
+
+// Crop (instanced_splat_renderer.mm:382-386) into the host planes.
+gs_status build_scene(gs_handle* h, const gs_scene_soa* sc, const gs_options& opt) {
+    if (!sc || sc->n < 0 || (sc->n > 0 && (!sc->pos || !sc->rot || !sc->scale || !sc->opacity || !sc->color)))
+        return fail(GS_ERR_INVALID_ARG, "gs_scene_soa: null array");
+    gs_status s = check_options(opt);
+    if (s != GS_OK) return s;
+    if (opt.sh_degree > 0 && !sc->sh_rest) return fail(GS_ERR_INVALID_ARG, "sh_degree > 0 needs sh_rest");
+    if (sc->n >= (int64_t)UINT32_MAX && !opt.crop) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 splats");
+    return adopt_planes(h, gsio::planes_from_soa(*sc, opt.crop_radius, opt.crop != 0, opt.sh_degree, &h->hp), opt);
 }
 
 gs_status scene_from_points(const PointData* pts, int64_t n, const std::vector<float>* raw_dc,
                             const gs_options& opt, gs_handle* h) {
-    std::vector<float> pos(n * 3), rot(n * 4), scale(n * 3), op(n), col(n * 3), rest;
-    const bool sh = opt.sh_degree > 0;
-    if (sh) rest.resize(n * 45);
-    for (int64_t i = 0; i < n; ++i) {
-        const PointData& p = pts[i];
-        pos[i * 3 + 0] = p.x; pos[i * 3 + 1] = p.y; pos[i * 3 + 2] = p.z;
-        rot[i * 4 + 0] = p.rot_0; rot[i * 4 + 1] = p.rot_1; rot[i * 4 + 2] = p.rot_2; rot[i * 4 + 3] = p.rot_3;
-        scale[i * 3 + 0] = p.scale_x; scale[i * 3 + 1] = p.scale_y; scale[i * 3 + 2] = p.scale_z;
-        op[i] = p.opacity;
-        if (sh && raw_dc) {
-            for (int c = 0; c < 3; ++c) col[i * 3 + c] = (*raw_dc)[i * 3 + c];
-        } else {
-            col[i * 3 + 0] = p.r; col[i * 3 + 1] = p.g; col[i * 3 + 2] = p.b;
-        }
-        if (sh) std::memcpy(&rest[i * 45], p.sh_rest, 45 * 4);
-    }
-    gs_scene_soa sc{n, pos.data(), rot.data(), scale.data(), op.data(), col.data(), sh ? rest.data() : nullptr};
-    return build_scene(h, &sc, opt);
+    gs_status s = check_options(opt);
+    if (s != GS_OK) return s;
+    return adopt_planes(h, gsio::planes_from_points(pts, n, raw_dc ? raw_dc->data() : nullptr, opt.crop_radius,
+                                                    opt.crop != 0, opt.sh_degree, &h->hp),
+                        opt);
 }
 
 // Host-side frame uniforms; VP = P·V with the contract's summation order.
@@ -801,17 +781,79 @@ gs_status gs_create(const char* ply_path, const gs_options* opt, gs_handle** out
     gs_options o;
     gs_default_options(&o);
     if (opt) o = *opt;
-    std::vector<PointData> pts;
-    std::vector<float> dc;
-    if (!PLYLoader::load(ply_path, pts, &dc, true))
-        return fail(GS_ERR_IO, std::string("failed to load PLY: ") + ply_path);
+    gs_status s = check_options(o);
+    if (s != GS_OK) return s;
     gs_handle* h = new gs_handle();
-    gs_status s = scene_from_points(pts.data(), (int64_t)pts.size(), &dc, o, h);
+    // binary files: mapped and converted in parallel straight into the HBM
+    // plane layout (scene_io.h); anything else through the PLYLoader drop-in.
+    // GS_PLY_DIRECT=0 takes the PLYLoader path for every file (A/B).
+    static const char* direct_env = std::getenv("GS_PLY_DIRECT");
+    bool handled = false;
+    if (!(direct_env && direct_env[0] == '0')) {
+        s = adopt_planes(h, gsio::planes_from_ply(ply_path, o.crop_radius, o.crop != 0, o.sh_degree, &h->hp, &handled),
+                         o);
+        if (s != GS_OK) {
+            delete h;
+            return s;
+        }
+    }
+    if (!handled) {
+        std::vector<PointData> pts;
+        std::vector<float> dc;
+        if (!PLYLoader::load(ply_path, pts, &dc, true)) {
+            delete h;
+            return fail(GS_ERR_IO, std::string("failed to load PLY: ") + ply_path);
+        }
+        s = scene_from_points(pts.data(), (int64_t)pts.size(), &dc, o, h);
+    }
     if (s != GS_OK) {
         delete h;
         return s;
     }
     *out = h;
+    return GS_OK;
+}
+
+gs_status gs_create_subset(const gs_handle* src, int64_t begin, int64_t end, gs_handle** out) {
+    if (!out) return fail(GS_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    if (!src || begin < 0 || end < begin || end > src->n) return fail(GS_ERR_INVALID_ARG, "gs_create_subset: bad range");
+    gs_handle* h = new gs_handle();
+    try {
+        gsio::planes_subset(src->hp, begin, end, &h->hp);
+    } catch (const std::bad_alloc&) {
+        delete h;
+        return fail(GS_ERR_OOM, "gs_create_subset: host planes");
+    }
+    h->opt = src->opt;
+    h->n = h->hp.n;
+    *out = h;
+    return GS_OK;
+}
+
+gs_status gs_get_scene(const gs_handle* h, float* pos, float* rot, float* scale, float* opacity, float* color,
+                       float* sh_rest) {
+    if (!h) return fail(GS_ERR_INVALID_ARG, "null handle");
+    const gsio::HostPlanes& hp = h->hp;
+    const int K = sh_coeffs(hp.sh_degree), NF = 3 * K, NP4 = hp.np4();
+    const size_t n = (size_t)hp.n;
+    for (size_t i = 0; i < n; ++i) {
+        const float *a = hp.p0.data() + 4 * i, *b = hp.p1.data() + 4 * i, *c = hp.p2.data() + 4 * i,
+                    *d = hp.p3.data() + 2 * i;
+        if (pos) std::memcpy(pos + 3 * i, a, 12);
+        if (opacity) opacity[i] = a[3];
+        if (rot) std::memcpy(rot + 4 * i, b, 16);
+        if (scale) std::memcpy(scale + 3 * i, c, 12);
+        if (color) color[3 * i] = c[3], color[3 * i + 1] = d[0], color[3 * i + 2] = d[1];
+        if (sh_rest) {
+            float* r = sh_rest + 45 * i;
+            std::memset(r, 0, 45 * 4);
+            for (int j = 0; j < NF; ++j) {  // flat j = 3k + ch <- f_rest[ch*15 + k]
+                const float v = j / 4 < NP4 ? hp.sh4.data()[((size_t)(j / 4) * n + i) * 4 + j % 4] : hp.sh1.data()[i];
+                r[(j % 3) * 15 + j / 3] = v;
+            }
+        }
+    }
     return GS_OK;
 }
 
@@ -822,41 +864,24 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
     if (device < 0 || device >= count) return fail(GS_ERR_DEVICE, "no such HIP device");
     GS_HIP(hipSetDevice(device));
     h->device = device;
-    const size_t n = (size_t)std::max<int64_t>(h->n, 1);
-    // HBM layout: four SoA float4/float2 planes, optional SH planes.
-    std::vector<float> a((size_t)n * 4), b((size_t)n * 4), c((size_t)n * 4), d((size_t)n * 2);
-    for (int64_t i = 0; i < h->n; ++i) {
-        a[i * 4 + 0] = h->pos[i * 3 + 0]; a[i * 4 + 1] = h->pos[i * 3 + 1];
-        a[i * 4 + 2] = h->pos[i * 3 + 2]; a[i * 4 + 3] = h->opacity[i];
-        std::memcpy(&b[i * 4], &h->rot[i * 4], 16);
-        c[i * 4 + 0] = h->scale[i * 3 + 0]; c[i * 4 + 1] = h->scale[i * 3 + 1];
-        c[i * 4 + 2] = h->scale[i * 3 + 2]; c[i * 4 + 3] = h->color[i * 3 + 0];
-        d[i * 2 + 0] = h->color[i * 3 + 1]; d[i * 2 + 1] = h->color[i * 3 + 2];
-    }
+    // HBM layout: the host planes are already in it, one copy each
+    const size_t n = (size_t)std::max<int64_t>(h->n, 1), m = (size_t)h->n;
+    const gsio::HostPlanes& hp = h->hp;
     GS_HIP(h->p0.reserve(n * 16));
     GS_HIP(h->p1.reserve(n * 16));
     GS_HIP(h->p2.reserve(n * 16));
     GS_HIP(h->p3.reserve(n * 8));
-    GS_HIP(hipMemcpy(h->p0.ptr, a.data(), n * 16, hipMemcpyHostToDevice));
-    GS_HIP(hipMemcpy(h->p1.ptr, b.data(), n * 16, hipMemcpyHostToDevice));
-    GS_HIP(hipMemcpy(h->p2.ptr, c.data(), n * 16, hipMemcpyHostToDevice));
-    GS_HIP(hipMemcpy(h->p3.ptr, d.data(), n * 8, hipMemcpyHostToDevice));
-    if (h->has_sh) {
-        // k-major, rgb-interleaved coefficient stream: flat j = 3k + ch
-        // (k = 0..K-1) <- f_rest[ch*15 + k] (PLY channel-major order).
-        const int K = sh_coeffs(h->opt.sh_degree), NF = 3 * K, NP4 = NF / 4;
-        std::vector<float> planes((size_t)std::max(NP4, 1) * n * 4), tail(n);
-        for (int64_t i = 0; i < h->n; ++i) {
-            float flat[45];
-            for (int k = 0; k < K; ++k)
-                for (int ch = 0; ch < 3; ++ch) flat[3 * k + ch] = h->sh_rest[i * 45 + ch * 15 + k];
-            for (int m = 0; m < NP4; ++m) std::memcpy(&planes[((size_t)m * n + i) * 4], &flat[4 * m], 16);
-            if (NF % 4) tail[i] = flat[NF - 1];
-        }
-        GS_HIP(h->sh4.reserve(planes.size() * 4));
-        GS_HIP(hipMemcpy(h->sh4.ptr, planes.data(), planes.size() * 4, hipMemcpyHostToDevice));
+    if (m) {
+        GS_HIP(hipMemcpy(h->p0.ptr, hp.p0.data(), m * 16, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(h->p1.ptr, hp.p1.data(), m * 16, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(h->p2.ptr, hp.p2.data(), m * 16, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(h->p3.ptr, hp.p3.data(), m * 8, hipMemcpyHostToDevice));
+    }
+    if (h->opt.sh_degree > 0) {
+        GS_HIP(h->sh4.reserve((size_t)std::max(hp.np4(), 1) * n * 16));
         GS_HIP(h->sh1.reserve(n * 4));
-        GS_HIP(hipMemcpy(h->sh1.ptr, tail.data(), n * 4, hipMemcpyHostToDevice));
+        if (m && hp.np4()) GS_HIP(hipMemcpy(h->sh4.ptr, hp.sh4.data(), (size_t)hp.np4() * m * 16, hipMemcpyHostToDevice));
+        if (m && hp.tail()) GS_HIP(hipMemcpy(h->sh1.ptr, hp.sh1.data(), m * 4, hipMemcpyHostToDevice));
     }
     // frames_in_flight 2: the side stream (projection .. per-bin sort, the
     // frame's critical path, HBM- and latency-bound) runs at the highest queue

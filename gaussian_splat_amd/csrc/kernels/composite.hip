@@ -16,8 +16,8 @@
 // The per-pixel body is branch-free (a non-covering splat contributes an
 // exact zero), a wave leaves the batch once all 64 of its pixels are
 // saturated, and the workgroup stops fetching once all 256 are.
-// Bins are dealt to workgroups XCD-aware: consecutive bins of a row share
-// many of their splats, so they are placed on one XCD's L2.
+// Bins are dealt to workgroups XCD-aware: the four tiles of a bin run on
+// one XCD and share the bin's list through its L2.
 #include <hip/hip_ext.h>
 
 #include "gs_kernels.h"
@@ -55,6 +55,25 @@ __device__ unsigned long long g_ct[8];
 #define GS_CT_DECL (void)0
 #define GS_CT(i) (void)0
 #define GS_CT_FLUSH() (void)0
+#endif
+#ifdef GS_COMPOSITE_TRACE
+// Debug build only (-DGS_COMPOSITE_TRACE): per wave {start, end} realtime
+// (100 MHz), HW_ID and XCC_ID, for the occupancy / tail analysis of
+// tools/composite_trace.py.
+constexpr uint32_t kTraceMax = 1u << 18;
+__device__ uint4 g_trace[kTraceMax];
+#define GS_TR_DECL const uint32_t tr_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime()
+#define GS_TR_FLUSH()                                                                                    \
+    do {                                                                                                 \
+        const uint32_t tr_t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();                              \
+        const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);                                      \
+        if ((threadIdx.x & 63u) == 0 && slot < kTraceMax)                                                \
+            g_trace[slot] = make_uint4(tr_t0, tr_t1, __builtin_amdgcn_s_getreg((31 << 11) | 4),          \
+                                       __builtin_amdgcn_s_getreg((31 << 11) | 20));                      \
+    } while (0)
+#else
+#define GS_TR_DECL (void)0
+#define GS_TR_FLUSH() (void)0
 #endif
 
 // MLAB k-buffer (gaussian_splat.metal:201-361): six premultiplied half
@@ -157,12 +176,25 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     __shared__ StagedRec srec[kTileThreads];
     __shared__ uint16_t wlist[4][kTileThreads];  // per wave: slot byte offsets
     __shared__ uint8_t sqm[kTileThreads];  // per staged record: the quadrants it may reach
+    __shared__ uint32_t sopen;             // byte per wave: pixels still open after its last walk
 
-    // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each
-    // residue class a contiguous run of tiles (cdna_hip_programming.md §5, T1).
+    // XCD-aware bijective remap (blocks b and b+8 share an XCD,
+    // cdna_hip_programming.md §5, T1).
+    GS_TR_DECL;
     const uint32_t orig = blockIdx.x;
+#if defined(GS_XCD_MAP) && GS_XCD_MAP == 0
+    // A/B: each XCD a contiguous run of tiles (a band of bin rows)
     const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
     const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+#else
+    // Bins dealt round-robin over the XCDs, a bin's 4 tiles on one XCD (they
+    // share its list through that L2).  Measured against giving each XCD a
+    // contiguous band of bin rows: -2 % composite, since the bands' costs
+    // differ and the launch ends with the slowest XCD.
+    const uint32_t full = nwg & ~31u;
+    const uint32_t kk = orig >> 3;
+    const uint32_t wg = orig < full ? 32u * (kk >> 2) + 4u * (orig & 7u) + (kk & 3u) : orig;
+#endif
 
     // Grid covers only the owned bin rows.  The four 16x16
     // tiles of a bin are consecutive workgroups (same XCD / L2).
@@ -313,7 +345,17 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     GS_CT_DECL;
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
         GS_CT(5);
+#ifdef GS_AB_SYNC_COUNT
         if (__syncthreads_count(!finished()) == 0) break;
+#else
+        // every wave published at the end of its last walk whether it still
+        // has open pixels; one LDS barrier both orders that and frees the
+        // slots of the last batch (__syncthreads_count takes three)
+        if (b != rg.x) {
+            block_lds_sync();
+            if (sopen == 0u) break;
+        }
+#endif
         GS_CT(0);
         if (rg.y - b > (uint32_t)kTileThreads) {
             const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
@@ -412,9 +454,14 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         }
         if (lane == 0) GS_CC(3, i);
+        {
+            const bool open = __ballot(!finished()) != 0;
+            if (lane == 0) reinterpret_cast<volatile uint8_t*>(&sopen)[wave] = open ? 1u : 0u;
+        }
         GS_CT(4);
     }
     GS_CT_FLUSH();
+    GS_TR_FLUSH();
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
     if (!inside) return;
     if constexpr (SLAB == 1) {
@@ -478,6 +525,12 @@ extern "C" int gs_debug_composite_timers(unsigned long long* out) {
     unsigned long long zero[8] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_ct), sizeof zero) != hipSuccess) return 1;
     return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_ct), zero, sizeof zero) != hipSuccess;
+}
+#endif
+#ifdef GS_COMPOSITE_TRACE
+extern "C" int gs_debug_composite_trace(void* out, unsigned n) {  // n uint4 entries
+    if (n > gs::kTraceMax) n = gs::kTraceMax;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_trace), (size_t)n * 16) != hipSuccess;
 }
 #endif
 #ifdef GS_COMPOSITE_COUNTERS

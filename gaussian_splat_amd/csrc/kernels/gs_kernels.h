@@ -190,4 +190,6 @@ hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint
 // Unpack dkey and packed rect of every received exchange record.
 hipError_t launch_recv_unpack(float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
                               uint32_t* rect_hi, hipStream_t st);
+// dst[i] += src[i] for n4 float4s.
+hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStream_t st);
 }  // namespace gs

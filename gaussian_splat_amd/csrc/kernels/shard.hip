@@ -8,6 +8,8 @@
 // holds its key.  Either way received records arrive in source-rank order,
 // i.e. in global index order, so the receiving rank's stable sort reproduces
 // the single-GPU order of its bins (rows) or of its depth range (slabs).
+#include <algorithm>
+
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -212,6 +214,23 @@ hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint
                              uint32_t nblocks, float4* send, hipStream_t st) {
     if (nblocks == 0) return hipSuccess;
     shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, dkey, dest_mask, n, world, counts, dest_total, nblocks, send);
+    return hipGetLastError();
+}
+
+// dst[i] += src[i] over float4s (the depth-slab RGBA reduce of a transport
+// without collectives: contributions summed on one device in rank order).
+__global__ __launch_bounds__(256) void accumulate_kernel(float4* __restrict__ dst, const float4* __restrict__ src,
+                                                         size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        const float4 a = dst[i], b = src[i];
+        dst[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+}
+
+hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStream_t st) {
+    if (n4 == 0) return hipSuccess;
+    const size_t blocks = std::min<size_t>((n4 + 255) / 256, 8192);
+    accumulate_kernel<<<(unsigned)blocks, 256, 0, st>>>(dst, src, n4);
     return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 4
+#define GSPLAT_ABI_VERSION 5
 
 typedef enum {
     GS_OK = 0,
@@ -130,6 +130,14 @@ gs_status gs_create(const char *ply_path, const gs_options *opt, gs_handle **out
 gs_status gs_create_from_soa(const gs_scene_soa *scene, const gs_options *opt, gs_handle **out);
 /* PointData array (62 floats per point, src/ply_loader.h:7-28), sh_degree 0. */
 gs_status gs_create_from_points(const float *points, int64_t n, const gs_options *opt, gs_handle **out);
+/* A handle over splats [begin, end) of a loaded (cropped) scene, same options:
+ * a shard without re-reading the file (no reference counterpart). */
+gs_status gs_create_subset(const gs_handle *scene, int64_t begin, int64_t end, gs_handle **out);
+/* The loaded (post-crop) scene back as host SoA arrays in gs_scene_soa layout
+ * (n = gs_point_count; any pointer may be NULL; sh_rest: n*45 in PLY order,
+ * zero beyond the handle's SH degree). */
+gs_status gs_get_scene(const gs_handle *h, float *pos, float *rot, float *scale, float *opacity, float *color,
+                       float *sh_rest);
 gs_status gs_initialize(gs_handle *h, int32_t device_ordinal); /* uploads the scene to HBM */
 int64_t gs_point_count(const gs_handle *h);
 void gs_destroy(gs_handle *h);
@@ -235,6 +243,34 @@ gs_status gs_slab_pack(gs_handle *h, const uint32_t *bounds, void *send, int64_t
 gs_status gs_slab_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height, float *t_local,
                          void *hip_stream);
 gs_status gs_slab_composite(gs_handle *h, const float *t_all, float *out_rgba, void *hip_stream);
+
+/* ---- multi-GPU from one process (gs_create_sharded) ------ */
+/* A group splits the (cropped) scene into num_gpus contiguous splat-index
+ * shards, one per device, and renders whole frames into devices[0] with the
+ * bin-row scheme (bit-identical to one GPU) or the depth-slab
+ * scheme.  One worker thread per rank drives the gs_shard_* /
+ * gs_slab_* steps above; collectives run over RCCL (xGMI) when every rank has
+ * its own device (GS_TRANSPORT_AUTO), or as peer copies (GS_TRANSPORT_COPY,
+ * required when ranks share a device).  Drop-in use: replace
+ * gs_create/gs_initialize/gs_render by their gs_group counterparts. */
+typedef struct gs_group gs_group;
+typedef enum { GS_SCHEME_ROWS = 0, GS_SCHEME_SLABS = 1 } gs_scheme;
+typedef enum { GS_TRANSPORT_AUTO = 0, GS_TRANSPORT_RCCL = 1, GS_TRANSPORT_COPY = 2 } gs_transport;
+gs_status gs_create_sharded(const char *ply_path, const gs_options *opt, int32_t num_gpus, gs_group **out);
+gs_status gs_create_sharded_from_handle(const gs_handle *scene, int32_t num_gpus, gs_group **out);
+/* devices: num_gpus ordinals (NULL = 0 .. num_gpus-1; repeats allowed with
+ * GS_TRANSPORT_COPY); transport: gs_transport. */
+gs_status gs_group_initialize(gs_group *g, const int32_t *devices, int32_t transport);
+gs_status gs_group_set_scheme(gs_group *g, int32_t scheme);
+/* The frame (fp32 RGBA, W*H*16 B) on devices[0]: out_is_device = 1 async on
+ * hip_stream (a stream of devices[0]); 0 = host memory, the call syncs. */
+gs_status gs_group_render(gs_group *g, const float view[16], const float proj[16], int32_t width, int32_t height,
+                          float *out_rgba, int32_t out_is_device, void *hip_stream);
+int64_t gs_group_point_count(const gs_group *g);
+int32_t gs_group_size(const gs_group *g);
+int32_t gs_group_transport(const gs_group *g); /* the transport in use, -1 before initialize */
+gs_status gs_group_last_stats(gs_group *g, int32_t rank, gs_stats *out);
+void gs_group_destroy(gs_group *g);
 
 /* ---- PLY loader (PLYLoader::load drop-in) ----------------------------- */
 /* Loads into a malloc'd PointData array (62 floats/point).  compat = 1

@@ -35,6 +35,12 @@ public:
     static bool load(const std::string& filepath, std::vector<PointData>& points, std::vector<float>* raw_dc,
                      bool compat = true);
 
+    // Header of a binary PLY as load() reads it (properties of every element,
+    // 4 bytes each): vertex count, property names and the payload offset.
+    // False for ASCII files and headers load() rejects.
+    static bool scanBinary(const std::string& filepath, int& vertexCount, std::vector<std::string>& names,
+                           long long& dataOffset);
+
 private:
     struct PropertyInfo {
         std::string name;

@@ -1,0 +1,115 @@
+"""GPU tests of the one-process multi-GPU group (gs_create_sharded, SURVEY
+§8(b)/(e)).  On a one-GPU box the ranks are virtual (devices [0, 0, ...],
+peer-copy transport): the same gs_shard_* / gs_slab_* steps and buffers as
+on 8 GPUs, with hipMemcpyPeerAsync in place of RCCL.  The RCCL transport
+runs when the box has two or more GPUs.
+
+Bar: the bin-row scheme is bit-identical to the 1-GPU frame; the depth-slab
+scheme is bit-identical to the Python virtual-slab path (same passes, same
+summation order) and within the slab bound (conftest.check_slab_frame) of
+the 1-GPU frame."""
+import numpy as np
+import pytest
+
+from conftest import check_slab_frame, orbit_views
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(n, seed, sh, aspect):
+    from gaussian_splat_amd import scene as S
+    return S.activate(S.synthetic_raw(n, seed=seed, aspect=aspect, rest=sh > 0), sh)
+
+
+def _group(r, world, devices=None, transport="copy", scheme="rows"):
+    from gaussian_splat_amd import ShardedGroup
+    g = ShardedGroup(r, world)
+    g.initialize(devices if devices is not None else [0] * world, transport)
+    g.set_scheme(scheme)
+    return g
+
+
+@pytest.mark.parametrize("world,mode,sh,W,H", [(2, "tile", 3, 640, 400), (3, "live50", 0, 640, 400),
+                                               (4, "tile", 3, 1920, 1080), (1, "tile", 0, 256, 256)])
+def test_group_rows_bitexact(built, world, mode, sh, W, H):
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    n = 200000 if W > 1000 else 60000
+    sc = _scene(n, 51 + world, sh, W / H)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    g = _group(r, world)
+    assert g.transport == "copy" and g.size == world
+    for V, P in orbit_views(W, H, 2):
+        ref = r.render_host(V, P, W, H)
+        got = g.render_host(V, P, W, H)
+        assert int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))) == 0
+        dev = g.render(V, P, W, H).cpu().numpy()  # device output, caller's stream
+        np.testing.assert_array_equal(dev.view(np.uint32), ref.view(np.uint32))
+    st = g.last_stats(0)
+    assert st["width"] == W and st["height"] == H
+
+
+@pytest.mark.parametrize("world,mode,sh", [(2, "tile", 3), (3, "live50", 0)])
+def test_group_slabs(built, world, mode, sh):
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd import distributed as D
+    W, H = 640, 400
+    sc = _scene(60000, 61 + world, sh, W / H)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    g = _group(r, world, scheme="slabs")
+    V, P = orbit_views(W, H, 2)[1]
+    got = g.render_host(V, P, W, H)
+    virt = D.render_virtual_slabs(sc, world, V, P, W, H, sh_degree=sh, mode=mode)
+    np.testing.assert_array_equal(got.view(np.uint32), virt.view(np.uint32))
+    check_slab_frame(got, r.render_host(V, P, W, H))
+
+
+def test_group_from_ply_with_crop(built, tmp_path):
+    """gs_create_sharded(path): the crop applies to the global scene before
+    sharding, so the group's frame is the 1-GPU frame of the same file."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options, ShardedGroup
+    from gaussian_splat_amd import scene as S
+    raw = S.synthetic_raw(80000, seed=71, aspect=16 / 9, rest=True)
+    raw.pos[::5] *= 2.0  # some outside the crop box
+    p = S.write_ply(tmp_path / "s.ply", raw)
+    W, H = 960, 540
+    opt = Options(sh_degree=3, crop=True)
+    r = InstancedSplatRenderer(p, opt)
+    r.initialize(0)
+    g = ShardedGroup(p, 3, opt)
+    g.initialize([0, 0, 0], "copy")
+    assert g.getPointCount() == r.getPointCount() < 80000
+    V, P = orbit_views(W, H, 1)[0]
+    np.testing.assert_array_equal(g.render_host(V, P, W, H).view(np.uint32), r.render_host(V, P, W, H).view(np.uint32))
+
+
+def test_group_rccl_two_gpus(built):
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL transport needs two GPUs (this box has one)")
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    W, H = 640, 400
+    sc = _scene(60000, 81, 0, W / H)
+    r = InstancedSplatRenderer(sc, Options(crop=False))
+    r.initialize(0)
+    for scheme in ("rows", "slabs"):
+        g = _group(r, 2, devices=[0, 1], transport="auto", scheme=scheme)
+        assert g.transport == "rccl"
+        V, P = orbit_views(W, H, 1)[0]
+        ref = r.render_host(V, P, W, H)
+        got = g.render_host(V, P, W, H)
+        if scheme == "rows":
+            np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+        else:
+            check_slab_frame(got, ref)
+        g.close()
+
+
+def test_group_rejects_rccl_on_shared_device(built):
+    from gaussian_splat_amd import GsError, InstancedSplatRenderer, Options, ShardedGroup
+    sc = _scene(1000, 5, 0, 1.0)
+    r = InstancedSplatRenderer(sc, Options(crop=False))
+    g = ShardedGroup(r, 2)
+    with pytest.raises(GsError):
+        g.initialize([0, 0], "rccl")
