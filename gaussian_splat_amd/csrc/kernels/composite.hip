@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     __shared__ StagedRec srec[kTileThreads];
     __shared__ uint16_t wlist[4][kTileThreads];  // per wave: slot byte offsets
     __shared__ uint8_t sqm[kTileThreads];  // per staged record: the quadrants it may reach
-    __shared__ uint32_t sopen;             // byte per wave: pixels still open after its last walk
+    __shared__ uint32_t sopen[4];          // per wave: pixels still open after its last walk
 
     // XCD-aware bijective remap (blocks b and b+8 share an XCD,
     // cdna_hip_programming.md §5, T1).
@@ -218,7 +218,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     const float ly = (float)lyi + 0.5f;
     const float ftx0 = (float)tx0, fty0 = (float)ty0;
 
-    const uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
+    // (a tile wholly outside the frame, the last bin row's lower half, has
+    // nothing to composite)
+    uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
+    if (tx0 >= (uint32_t)width || ty0 >= (uint32_t)height) rg.y = rg.x;
     // Pixels outside the frame start finished (T = 0): for the tile and live50
     // rules "finished" is then just the break test on T itself, so no
     // separate per-lane flag is carried through the loop.
@@ -348,12 +351,15 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
 #ifdef GS_AB_SYNC_COUNT
         if (__syncthreads_count(!finished()) == 0) break;
 #else
-        // every wave published at the end of its last walk whether it still
-        // has open pixels; one LDS barrier both orders that and frees the
-        // slots of the last batch (__syncthreads_count takes three)
+        // every wave publishes whether it still has open pixels; one LDS
+        // barrier both orders that and frees the slots of the last batch
+        // (__syncthreads_count takes three)
         if (b != rg.x) {
+            const bool open = __ballot(!finished()) != 0;
+            if (lane == 0) sopen[wave] = open ? 1u : 0u;
             block_lds_sync();
-            if (sopen == 0u) break;
+            const uint4 o = *reinterpret_cast<const uint4*>(sopen);
+            if ((o.x | o.y | o.z | o.w) == 0u) break;
         }
 #endif
         GS_CT(0);
@@ -454,10 +460,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         }
         if (lane == 0) GS_CC(3, i);
-        {
-            const bool open = __ballot(!finished()) != 0;
-            if (lane == 0) reinterpret_cast<volatile uint8_t*>(&sopen)[wave] = open ? 1u : 0u;
-        }
         GS_CT(4);
     }
     GS_CT_FLUSH();
