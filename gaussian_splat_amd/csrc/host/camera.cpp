@@ -155,5 +155,8 @@ simd_quatf TrackballCamera::rotationBetweenVectors(simd_float3 start, simd_float
     simd_float3 axis = simd_cross(start, dest);
     float s = std::sqrt((1.0f + cosT) * 2.0f);
     float inv = 1.0f / s;
-    return simd_quaternion(axis.x * inv, axis.y * inv, axis.z * inv, s * 0.5f);
+    // Argument order as the reference passes it (trackball_camera.mm:187):
+    // simd_quaternion(ix, iy, iz, r) receives (s/2, axis/s), so the real part
+    // lands in ix.  Kept for behaviour-identical drags (drop-in contract).
+    return simd_quaternion(s * 0.5f, axis.x * inv, axis.y * inv, axis.z * inv);
 }

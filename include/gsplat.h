@@ -227,10 +227,12 @@ int32_t gs_exchange_record_bytes(void);
  *                     ranks' (farther slabs') transmittance; out_rgba (device,
  *                     W*H*4 f32) = (C, delta alpha) contributions
  *   (reduce SUM of out_rgba = the frame)
- * Rank order is composite (far-to-near) order.  The result equals the 1-GPU
- * frame up to fp32 reassociation of the transmittance product;
- * the row scheme above is bit-identical.  No fragment cap.  `recv` must stay
- * alive until gs_slab_composite returns. */
+ * Rank order is composite (far-to-near) order.  APPROXIMATE: the frame equals
+ * the 1-GPU frame up to fp32 reassociation of the transmittance product, and a
+ * pixel within rounding of the 0.99 / 0.01 break may stop one fragment
+ * earlier or later; the row scheme above is the bit-identical
+ * one.  No fragment cap.  `recv` must stay alive until gs_slab_composite
+ * returns. */
 #define GS_SLAB_BINS 2048   /* histogram bins ... */
 #define GS_SLAB_BIN_KEYS 16 /* ... of 16 depth keys: slab bounds are multiples of 16 */
 gs_status gs_slab_project(gs_handle *h, const float view[16], const float proj[16], int32_t width, int32_t height,
