@@ -35,14 +35,15 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
                                                           uint64_t* __restrict__ partials,
                                                           uint2* __restrict__ fill, uint32_t nfill,
                                                           uint32_t* __restrict__ zero, uint32_t nzero) {
-    __shared__ uint64_t tmp[4];
+    __shared__ uint2 tmp[4];
     // the frame's bin ranges start empty and the first sort pass's digit
     // counts at zero (saves two fill dispatches)
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nfill; i += gridDim.x * 256u)
         fill[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
     const uint32_t base = blockIdx.x * kScanItems;
-    uint64_t s = 0, vis = 0;
+    // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
+    uint32_t s = 0, vis = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         uint32_t i = base + k * 256 + threadIdx.x;
@@ -52,12 +53,15 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
             vis += c > 0;
         }
     }
-    uint64_t total, vtotal;
-    block256_exclusive_scan<uint64_t>(s, tmp, &total);
-    block256_exclusive_scan<uint64_t>(vis, tmp, &vtotal);
+    // block sums: wave reductions (DPP), then one barrier
+    s = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(s), 63);
+    vis = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(vis), 63);
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) tmp[wave] = make_uint2(s, vis);
+    __syncthreads();
     if (threadIdx.x == 0) {
-        partials[blockIdx.x] = total;
-        partials[gridDim.x + blockIdx.x] = vtotal;
+        partials[blockIdx.x] = (uint64_t)tmp[0].x + tmp[1].x + tmp[2].x + tmp[3].x;
+        partials[gridDim.x + blockIdx.x] = (uint64_t)tmp[0].y + tmp[1].y + tmp[2].y + tmp[3].y;
     }
 }
 
