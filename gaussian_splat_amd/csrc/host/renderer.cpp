@@ -463,8 +463,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                         h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
                                         h->npairs.as<uint32_t>(), cap, pc.C, pc.C ? (pc.mask + 1) * pc.ntiles : 0u,
-                                        st));
-    GS_HIP(hipEventRecord(h->totals_ev, st));
+                                        st, h->totals_ev));
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
     // bin id), then a stable sort by bin id only; the last pass also writes
@@ -530,9 +529,10 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     // lists are ready on st.  A pointer, since the caller's stream may be the
     // null stream.
     const hipStream_t sc = composite_stream ? *composite_stream : st;
-    auto handoff = [&]() -> hipError_t {
+    // (recorded = the last list kernel's dispatch packet carried sorted_ev)
+    auto handoff = [&](bool recorded = false) -> hipError_t {
         if (sc == st) return hipSuccess;
-        hipError_t e = hipEventRecord(h->sorted_ev, st);
+        hipError_t e = recorded ? hipSuccess : hipEventRecord(h->sorted_ev, st);
         return e != hipSuccess ? e : hipStreamWaitEvent(sc, h->sorted_ev, 0);
     };
     Ownership own;
@@ -601,13 +601,14 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         // (one sample word pair per buffer set)
         GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
                                          h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
-                                         h->seg_sample.as<uint32_t>() + 2 * h->set, sd));
+                                         h->seg_sample.as<uint32_t>() + 2 * h->set, sd,
+                                         sc != st ? h->sorted_ev : nullptr));
         mark(h, 6, sd);
         if (slab_t) {
             ca.slab = 1;
             ca.t_out = slab_t;
         }
-        GS_HIP(handoff());
+        GS_HIP(handoff(true));
         ca.fetched = fetch_counter(h);
         GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
         if (slab_t) {
@@ -963,7 +964,9 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         h->swap_sets();
         if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     }
-    GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
+    // (a wait packet only when that composite may still run: each costs a
+    // few us of stream bubble)
+    if (hipEventQuery(h->set_free[h->set]) != hipSuccess) GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
     if (pipe && !h->last_pipe) {  // the side stream starts after everything the caller's stream holds
         GS_HIP(hipEventRecord(h->sorted_ev, st));
         GS_HIP(hipStreamWaitEvent(sp, h->sorted_ev, 0));

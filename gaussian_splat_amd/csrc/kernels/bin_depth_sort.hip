@@ -24,6 +24,8 @@
 // its bucket-rank loop costs the largest bucket of the wave.)
 // Longer lists (a hot bin of a dense scene) take a chunked LSD over global
 // memory, one workgroup per bin, through the bin sort's spare buffers.
+#include <hip/hip_ext.h>
+
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -312,13 +314,13 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
 
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
-                                 hipStream_t st) {
-    if (nbins == 0) return hipSuccess;
+                                 hipStream_t st, hipEvent_t done) {
+    if (nbins == 0) return done ? hipEventRecord(done, st) : hipSuccess;
     if (bin_bits < 0 || bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     // one workgroup per bin
     static_assert(GS_SEG_NT * GS_SEG_IPT == kSegLdsMax, "gs_kernels.h");
-    bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>
-        <<<nbins, GS_SEG_NT, 0, st>>>(ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample);
+    hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>), dim3(nbins), dim3(GS_SEG_NT), 0,
+                          st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample);
     return hipGetLastError();
 }
 

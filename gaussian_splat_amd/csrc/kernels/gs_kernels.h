@@ -38,7 +38,9 @@ constexpr int kScanItems = 4096;  // per block
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st);
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr);
+// (done: recorded by the totals kernel's own dispatch packet, not a separate
+// marker packet, which would leave a ~6 us bubble in the stream.)
 // The first LSD pass's digit counts of the pairs, C[digit][tile] with
 // `ntiles` columns, tiles of `tile` pairs, digit = bin & mask: the index-order
 // duplicate adds them up as it writes (C zeroed before), so the sort skips
@@ -76,7 +78,7 @@ constexpr uint32_t kSegLdsMax = 8192;  // = the kernel's NT * IPT (bin_depth_sor
 constexpr uint32_t kSegSampleValid = 0x80000000u;
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
-                                 hipStream_t st);
+                                 hipStream_t st, hipEvent_t done = nullptr);
 
 // ---- radix_sort.hip --------------------------------------------------------
 constexpr int kSortBins = 256;   // 8-bit digits

@@ -12,6 +12,8 @@
 // order with the depth key carried above the bin id (key = dkey << bin_bits
 // | bin); after the bin sort each list is put in depth order by a stable
 // per-bin sort (bin_depth_sort.hip).
+#include <hip/hip_ext.h>
+
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st) {
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
@@ -310,7 +312,8 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
     } else {
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
-    scan_partials_kernel<<<1, kPartThreads, 0, st>>>(partials, nb, total, seg_sample, npairs, cap);
+    hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
+                          total, seg_sample, npairs, cap);
     return hipGetLastError();
 }
 
