@@ -66,10 +66,12 @@ __device__ __forceinline__ uint32_t block512_exclusive_scan(uint32_t v, uint32_t
     return base + inc - v;
 }
 
-// Lanes of one wave holding the same digit: mask of peers (digit_bits ballots).
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int digit_bits) {
+// Lanes of one wave holding the same digit: mask of peers (BITS ballots).
+template <int BITS>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     uint64_t peers = __ballot(valid);
-    for (int b = 0; b < digit_bits; ++b) {
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
         const bool bit = (d >> b) & 1u;
         const uint64_t bal = __ballot(bit);
         peers &= bit ? bal : ~bal;
@@ -152,9 +154,9 @@ __global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __re
 // the caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
 // Bits above rmask ride along unsorted (the bin-first binning carries each
 // pair's depth key there, bin_depth_sort.hip).
-template <int NV>
+template <int NV, int BITS>
 __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
-                                                       int digit_bits, const uint32_t* __restrict__ C,
+                                                       const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
                                                        uint2* __restrict__ ranges, uint32_t rmask,
                                                        const uint32_t* __restrict__ n_dev) {
@@ -163,16 +165,17 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     if (n_dev) n = *n_dev;
     if (blockIdx.x * TILE >= n) return;  // (whole workgroup: before any barrier)
     constexpr uint32_t WAVE_ITEMS = 64u * IPT;
-    __shared__ uint32_t wh[kRsWaves][kSortBins];  // wave-private running counts -> wave offsets
-    __shared__ uint32_t blk_start[kSortBins];     // tile-local start of each digit
-    __shared__ uint32_t gbase[kSortBins];         // global start of this tile's digit run
+    constexpr uint32_t ND = 1u << BITS;
+    __shared__ uint32_t wh[kRsWaves][ND];  // wave-private running counts -> wave offsets
+    __shared__ uint32_t blk_start[ND];     // tile-local start of each digit
+    __shared__ uint32_t gbase[ND];         // global start of this tile's digit run
     __shared__ uint32_t stage[TILE];
     __shared__ uint32_t tmp[kRsWaves];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t tile = blockIdx.x;
-    for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&wh[0][0])[i] = 0;
+    for (uint32_t i = tid; i < kRsWaves * ND; i += kRsThreads) (&wh[0][0])[i] = 0;
     // Keys and all value arrays are loaded up front so their latency hides
     // behind the ranking.  Barriers here order LDS only: they never wait for
     // this tile's outstanding global stores.
@@ -195,12 +198,16 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     uint32_t all;
     const uint32_t dstart = block512_exclusive_scan(tid <= mask ? totals[tid] : 0u, tmp, &all);
     if (tid <= mask) gbase[tid] = dstart + C[(size_t)tid * ntiles + tile];
+    // Stable ranks: slot k of every lane in order, a wave's lanes matched by
+    // digit (ballots), the wave's running count per digit in LDS.  (A second,
+    // independent counting chain over half the slots was measured: the per-bin
+    // sort unchanged, this pass slower.)
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t idx = base + k * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (key[k] >> shift) & mask;
-        const uint64_t peers = match_digit(d, valid, digit_bits);
+        const uint64_t peers = match_digit<BITS>(d, valid);
         const uint32_t below = mbcnt(peers);
         const uint32_t old = wh[wave][d];
         pos[k] = old + below;
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     }
     block_lds_sync();
     uint32_t c = 0;
-    if (tid < kSortBins) {
+    if (tid < ND) {
 #pragma unroll
         for (int w = 0; w < kRsWaves; ++w) {
             const uint32_t x = wh[w][tid];
@@ -217,9 +224,17 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
         }
     }
     uint32_t tot;
-    const uint32_t ex = block512_exclusive_scan(tid < kSortBins ? c : 0u, tmp, &tot);
-    if (tid < kSortBins) blk_start[tid] = ex;
+    const uint32_t ex = block512_exclusive_scan(tid < ND ? c : 0u, tmp, &tot);
+    if (tid < ND) blk_start[tid] = ex;
     block_lds_sync();
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const uint32_t idx = base + k * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (key[k] >> shift) & mask;
+            pos[k] += blk_start[d] + wh[wave][d];
+        }
+    }
     const uint32_t t0 = tile * TILE;
     const uint32_t cnt = n - t0 < TILE ? n - t0 : TILE;
     // keys: stage in tile-local sorted order, write out; each slot's global
@@ -228,11 +243,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t idx = base + k * 64 + lane;
-        if (idx < n) {
-            const uint32_t d = (key[k] >> shift) & mask;
-            pos[k] += blk_start[d] + wh[wave][d];
-            stage[pos[k]] = key[k];
-        }
+        if (idx < n) stage[pos[k]] = key[k];
     }
     block_lds_sync();
     uint32_t gdst[IPT];
@@ -296,6 +307,23 @@ size_t radix_sort_scratch_words(uint32_t n) {
     return (size_t)(tiles ? tiles : 1) * kSortBins + kSortBins;
 }
 
+// rts_pass_kernel for a digit width (the ballot match unrolled per width)
+template <int NV, typename... A>
+static hipError_t launch_pass(int width, uint32_t tiles, hipStream_t st, A... args) {
+    switch (width) {
+    case 1: rts_pass_kernel<NV, 1><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 2: rts_pass_kernel<NV, 2><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 3: rts_pass_kernel<NV, 3><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 4: rts_pass_kernel<NV, 4><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 5: rts_pass_kernel<NV, 5><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 6: rts_pass_kernel<NV, 6><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 7: rts_pass_kernel<NV, 7><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 8: rts_pass_kernel<NV, 8><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int NV>
 static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
@@ -324,9 +352,10 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
             rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
         rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
-        rts_pass_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io, n, plan.shift[p], plan.mask[p], plan.width[p], C,
-                                                          totals, tiles, p + 1 == plan.passes ? ranges : nullptr,
-                                                          bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev);
+        const hipError_t e = launch_pass<NV>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+                                             tiles, p + 1 == plan.passes ? ranges : nullptr,
+                                             bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev);
+        if (e != hipSuccess) return e;
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;
