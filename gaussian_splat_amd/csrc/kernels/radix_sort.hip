@@ -90,10 +90,16 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
     for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint32_t t0 = blockIdx.x * TILE;
-#pragma unroll 4
-    for (uint32_t k = 0; k < TILE / kRsThreads; ++k) {
-        const uint32_t idx = t0 + k * kRsThreads + tid;
-        if (idx < n) atomicAdd(&h[wave][(keys[idx] >> shift) & mask], 1u);
+    constexpr int K = TILE / kRsThreads;
+    if (t0 >= n) {  // (n read on the device: tiles past it count zeros)
+    } else {
+        // all keys loaded first (clamped): one memory round trip
+        uint32_t kk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) kk[k] = keys[min(t0 + k * kRsThreads + tid, n - 1u)];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (t0 + k * kRsThreads + tid < n) atomicAdd(&h[wave][(kk[k] >> shift) & mask], 1u);
     }
     __syncthreads();
     if (tid <= mask) {

@@ -28,33 +28,37 @@ struct CountSrc {
     bool masked;  // rect words carry the bin-exclusion mask
 };
 
-__device__ __forceinline__ uint32_t count_at(const CountSrc& c, uint32_t i) {
-    return rect_tile_count(c.lo[i], c.hi[i], c.own, c.masked);
-}
-
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials,
                                                           uint2* __restrict__ fill, uint32_t nfill,
                                                           uint32_t* __restrict__ zero, uint32_t nzero) {
     __shared__ uint2 tmp[4];
-    // the frame's bin ranges start empty and the first sort pass's digit
-    // counts at zero (saves two fill dispatches)
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nfill; i += gridDim.x * 256u)
-        fill[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
     const uint32_t base = blockIdx.x * kScanItems;
+    // every rect loaded before the first use (clamped, branch-free): one
+    // memory round trip instead of one per item (a conditional load is waited
+    // for inside its branch)
+    uint32_t lo[kScanIpt], hi[kScanIpt];
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t i = min(base + k * 256 + threadIdx.x, n - 1u);
+        lo[k] = src.lo[i];
+        hi[k] = src.hi[i];
+    }
     // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
     uint32_t s = 0, vis = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
-        uint32_t i = base + k * 256 + threadIdx.x;
-        if (i < n) {
-            const uint32_t c = count_at(src, i);
-            s += c;
-            vis += c > 0;
-        }
+        const uint32_t c = base + k * 256 + threadIdx.x < n ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
+        s += c;
+        vis += c > 0;
     }
+    // the frame's bin ranges start empty and the first sort pass's digit
+    // counts at zero (saves two fill dispatches; stored after the loads, which
+    // a store would otherwise delay: vmcnt counts both)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nfill; i += gridDim.x * 256u)
+        fill[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nzero; i += gridDim.x * 256u) zero[i] = 0u;
     // block sums: wave reductions (DPP), then one barrier
     s = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(s), 63);
     vis = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(vis), 63);
@@ -179,15 +183,32 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    // every global load of the block up front (clamped, branch-free), before
+    // the first pair store: vmcnt counts loads and stores together, so a load
+    // issued between stores would wait for them
+    // (absent arrays read a stand-in, so no load sits in a branch, where its
+    // value would be waited for at once)
+    const uint64_t part = partials[blockIdx.x];
+    const uint32_t* dsrc = dkey ? dkey : src.lo;
+    const uint32_t* osrc = order ? order : src.lo;
+    uint32_t rlo[kDupIpt], rhi[kDupIpt], dk[kDupIpt], ord[kDupIpt];
+#pragma unroll
+    for (int k = 0; k < kDupIpt; ++k) {
+        const uint32_t j = min(blk + k * kDupThreads + tid, n - 1u);
+        rlo[k] = src.lo[j];
+        rhi[k] = src.hi[j];
+        dk[k] = dsrc[j];
+        ord[k] = osrc[j];
+    }
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
-    uint32_t rlo[kDupIpt], rhi[kDupIpt];
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid;
-        const bool ok = blk + i < n;
-        rlo[k] = ok ? src.lo[blk + i] : kEmptyRectLo;
-        rhi[k] = ok ? src.hi[blk + i] : 0u;
+        if (blk + i >= n) {
+            rlo[k] = kEmptyRectLo;
+            rhi[k] = 0u;
+        }
         st[pad32(i)] = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
     }
     block_lds_sync();
@@ -200,7 +221,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     }
     uint32_t t;
     const uint32_t ex = block_dup_exclusive_scan(s, tmp, &t);  // (ends with a barrier)
-    uint32_t run = (uint32_t)partials[blockIdx.x] + ex;
+    uint32_t run = (uint32_t)part + ex;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         st[pad32(tid * kDupIpt + k)] = run;
@@ -210,17 +231,18 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // the first sort pass's digit counts per tile of pc.tile pairs (rts_count
     // without its key re-read): the block's pairs are contiguous from its
     // partial, so its first kDupCountTiles tiles count in LDS
-    const uint32_t t_lo = pc.C ? (uint32_t)(partials[blockIdx.x] / pc.tile) : 0u;
+    const uint32_t t_lo = pc.C ? (uint32_t)(part / pc.tile) : 0u;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid, j = blk + i;
         const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);
         if (j >= n || r.empty) continue;
-        const uint32_t key_hi = dkey ? dkey[j] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t off = st[pad32(i)];
+        const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
+        const uint32_t val = order ? ord[k] : j;
         if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, off, keys, vals,
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals,
                            [&](uint32_t g, uint32_t bin) {
                                if (g == next) {
                                    ++t;
@@ -231,7 +253,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
                            });
         } else {
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, order ? order[j] : j, off, keys, vals);
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals);
         }
     }
     if (pc.C) {
@@ -254,10 +276,17 @@ __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n
     __shared__ uint32_t tmp[4];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    uint32_t lo[kScanIpt], hi[kScanIpt];  // (all loads first, as in scan_reduce)
+#pragma unroll
+    for (int k = 0; k < kScanIpt; ++k) {
+        const uint32_t j = min(blk + k * 256 + tid, n - 1u);
+        lo[k] = src.lo[j];
+        hi[k] = src.hi[j];
+    }
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const uint32_t i = k * 256 + tid;
-        st[pad32(i)] = blk + i < n ? count_at(src, blk + i) : 0u;
+        st[pad32(i)] = blk + i < n ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
     }
     __syncthreads();
     uint32_t v[kScanIpt];
