@@ -263,12 +263,16 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
     const int kmax = (int)((m + NT - 1) / NT);  // slots per lane (<= IPT)
     const uint32_t base = wave * (uint32_t)kmax * 64u;
     uint32_t it[IPT], pos[IPT];
+    // every key loaded before the first use (positions clamped into the list,
+    // branch-free): one memory round trip, not one per slot
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) it[k] = keys[s + min(base + (uint32_t)k * 64u + lane, m - 1u)];
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t p = base + (uint32_t)k * 64u + lane;
         const bool ok = k < kmax && p < m;
-        const uint32_t dk = ok ? keys[s + p] >> bin_bits : 0u;
+        const uint32_t dk = it[k] >> bin_bits;
         it[k] = ok ? (dk << kSegPosBits) | p : 0xFFFFFFFFu;
         lo = ok ? min(lo, dk) : lo;
         hi = ok ? max(hi, dk) : hi;
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
 #ifdef GS_SEG_ABL_NOGATHER  // ablation (timing only): coalesced read of the own slot (ids stay valid)
         v[k] = (k < kmax && p < m) ? vals[s + p] : 0u;
 #else
-        v[k] = (k < kmax && p < m) ? vals[s + (it[k] & ((1u << kSegPosBits) - 1u))] : 0u;
+        v[k] = vals[s + ((k < kmax && p < m) ? (it[k] & ((1u << kSegPosBits) - 1u)) : 0u)];
 #endif
     }
 #pragma unroll
