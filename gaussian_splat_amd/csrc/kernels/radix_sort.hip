@@ -187,17 +187,30 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     // this tile's outstanding global stores.
     const uint32_t base = tile * TILE + wave * WAVE_ITEMS;
     uint32_t key[IPT], pos[IPT], val[NV][IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const uint32_t idx = base + k * 64 + lane;
-        key[k] = idx < n ? io.kin[idx] : 0u;
-    }
-#pragma unroll
-    for (int a = 0; a < NV; ++a) {
+    if constexpr (NV == 1) {
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t idx = base + k * 64 + lane;
-            val[a][k] = idx < n ? (io.vin[a] ? io.vin[a][idx] : idx) : 0u;
+            key[k] = idx < n ? io.kin[idx] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t idx = base + k * 64 + lane;
+            val[0][k] = idx < n ? (io.vin[0] ? io.vin[0][idx] : idx) : 0u;
+        }
+    } else {
+        // several value arrays, the first possibly absent (value = index):
+        // unconditional loads, positions clamped into the input (a select on
+        // the absent array waits for each load where it is made), the index
+        // substituted when staged.  (For one array the conditional loads keep
+        // fewer registers live: measured faster there.)
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) key[k] = io.kin[min(base + k * 64 + lane, n - 1u)];
+#pragma unroll
+        for (int a = 0; a < NV; ++a) {
+            const uint32_t* vs = io.vin[a] ? io.vin[a] : io.kin;
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) val[a][k] = vs[min(base + k * 64 + lane, n - 1u)];
         }
     }
     // global start of every digit of this tile (independent of the ranking)
@@ -278,7 +291,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t idx = base + k * 64 + lane;
-            if (idx < n) stage[pos[k]] = val[a][k];
+            if (idx < n) stage[pos[k]] = (NV == 1 || io.vin[a]) ? val[a][k] : idx;
         }
         block_lds_sync();
 #pragma unroll
