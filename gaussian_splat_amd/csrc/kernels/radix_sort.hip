@@ -200,17 +200,22 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
         }
     } else {
         // several value arrays, the first possibly absent (value = index):
-        // unconditional loads, positions clamped into the input (a select on
-        // the absent array waits for each load where it is made), the index
-        // substituted when staged.  (For one array the conditional loads keep
-        // fewer registers live: measured faster there.)
+        // unconditional loads, positions clamped into the input (a per-item
+        // select waits for each load where it is made), an absent array not
+        // read at all (a uniform branch) and its index substituted when
+        // staged.  (For one array the conditional loads keep fewer registers
+        // live: measured faster there.)
 #pragma unroll
         for (int k = 0; k < IPT; ++k) key[k] = io.kin[min(base + k * 64 + lane, n - 1u)];
 #pragma unroll
         for (int a = 0; a < NV; ++a) {
-            const uint32_t* vs = io.vin[a] ? io.vin[a] : io.kin;
+            if (io.vin[a]) {
 #pragma unroll
-            for (int k = 0; k < IPT; ++k) val[a][k] = vs[min(base + k * 64 + lane, n - 1u)];
+                for (int k = 0; k < IPT; ++k) val[a][k] = io.vin[a][min(base + k * 64 + lane, n - 1u)];
+            } else {
+#pragma unroll
+                for (int k = 0; k < IPT; ++k) val[a][k] = 0u;
+            }
         }
     }
     // global start of every digit of this tile (independent of the ranking)
