@@ -15,13 +15,17 @@ does not exist offline):
 Multi-GPU is STRONG scaling over one global scene: `--gpus N` (without
 torchrun) starts N rank processes itself (torch.distributed.run, one rank per
 GPU, 127.0.0.1) before anything touches a GPU; under torchrun WORLD_SIZE must
-equal --gpus.  Rank r renders the splat-index shard [r*N/g, (r+1)*N/g) of the
-global scene (generated chunk-wise, so a rank builds only its shard), value =
-global splats / frame time (max over ranks).  Both multi-GPU schemes run
-(--scheme both): "rows" (bin-row ownership + all_to_all + band gather; the
-frame is bit-identical to one GPU's) gives `value`; "slabs" (the north star's
-depth slabs + transmittance all_gather + RGBA reduce; approximate, DESIGN.md
-§6b) is reported beside it.
+equal --gpus.  value = global splats / frame time (max over ranks).  Three
+multi-GPU schemes run (--scheme all), each timed on its own:
+  rows   rank r renders the splat-index shard [r*N/g, (r+1)*N/g) of the global
+         scene (generated chunk-wise, so a rank builds only its shard):
+         bin-row ownership + all_to_all of projected records + band gather
+  bands  SURVEY §8(e)'s fallback: every rank holds the whole scene and
+         renders its own bin rows (gs_band_render), then the band gather
+  slabs  the north star's depth slabs + transmittance all_gather + RGBA
+         reduce (approximate)
+rows and bands are bit-identical to one GPU's frame; `value` is the faster of
+the two (named in config.parallelism), and every scheme is in `schemes`.
 
 At N=1 the line also carries
   roofline      the dominant kernel's algorithmic bytes / its standalone
@@ -91,7 +95,7 @@ def parse():
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="N=1: 2 = a frame's projection/sort overlaps the previous frame's composite")
-    ap.add_argument("--scheme", default="both", choices=["rows", "slabs", "both"],
+    ap.add_argument("--scheme", default="all", choices=["rows", "slabs", "bands", "both", "all"],
                     help="N>1: bin-row ownership (exact; value), depth slabs + RGBA reduce, or both")
     a = ap.parse_args()
     c = CONFIGS[a.config]
@@ -277,11 +281,17 @@ def main():
         rh = r
         ms = timed(step, args.steps, args.warmup)
     else:
-        from gaussian_splat_amd.distributed import HipShardBackend, HipSlabBackend, ShardedRenderer, SlabRenderer
+        from gaussian_splat_amd.distributed import (BandRenderer, HipBandBackend, HipShardBackend, HipSlabBackend,
+                                                    ShardedRenderer, SlabRenderer)
 
-        order = ["rows", "slabs"] if args.scheme == "both" else [args.scheme]
+        order = {"both": ["rows", "slabs"], "all": ["rows", "bands", "slabs"]}.get(args.scheme, [args.scheme])
         for sch in order:
-            if sch == "slabs":
+            if sch == "bands":  # the whole scene on every rank
+                full = S.activate(S.synthetic_raw(N, seed=args.seed, aspect=W / H, rest=args.sh > 0,
+                                                  profile=args.profile), args.sh)
+                be = HipBandBackend(full, rank, world, opts, local)
+                sr = BandRenderer(be, rank, world)
+            elif sch == "slabs":
                 be = HipSlabBackend(scene, rank, world, b, opts, local)
                 sr = SlabRenderer(be, rank, world)
             else:
@@ -289,7 +299,8 @@ def main():
                 sr = ShardedRenderer(be, rank, world)
             stp = (lambda s_=sr: s_.render(view, proj, W, H, gather=True))
             schemes[sch] = {"ms": timed(stp, args.steps, args.warmup), "handle": be.r, "step": stp}
-        head = "rows" if "rows" in schemes else order[0]
+        exact = [k for k in ("rows", "bands") if k in schemes]
+        head = min(exact, key=lambda k: schemes[k]["ms"]) if exact else order[0]
         ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
     value = N / (ms * 1e-3) / 1e6
 
@@ -337,8 +348,11 @@ def main():
             "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)",
             "hbm_gbs": round(frame_bytes / (ms * 1e6), 1) if frame_bytes else None,
             "config": {"workload": args.label, "global_splats": N, "width": W, "height": H, "sh_degree": args.sh,
-                       "parallelism": (f"{world} ranks, splat-index shards of one global scene; rows: 32-px bin-row "
-                                       f"ownership, all_to_all + band gather ({backend}, world {world})")
+                       "parallelism": ((f"{world} ranks, splat-index shards of one global scene; rows: 32-px bin-row "
+                                        f"ownership, all_to_all + band gather ({backend}, world {world})")
+                                       if head == "rows" else
+                                       (f"{world} ranks, the scene replicated on every rank; bands: each renders its "
+                                        f"32-px bin rows, band gather ({backend}, world {world})"))
                        if world > 1 else
                        ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the composite of frame k)"
                         if args.frames_in_flight == 2 else "single GPU"),

@@ -242,6 +242,8 @@ gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
     u.tiles_x = (W + gs::kBin - 1) / gs::kBin;  // binning granularity (32x32 bins)
     u.tiles_y = (H + gs::kBin - 1) / gs::kBin;
     u.cell_mask = (W <= gs::kCellMaskDim && H <= gs::kCellMaskDim) ? 1 : 0;
+    u.band_y0 = 0;
+    u.band_y1 = H - 1;
     return u;
 }
 
@@ -1249,6 +1251,49 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
     gs::DestRule rule{};
     rule.owner = own.dev.owner;
     return pack_exchange(h, rule, U.cell_mask != 0, send, send_cap_bytes, send_counts, st);
+}
+
+// Replicated-scene bands (SURVEY §8(e) fallback): the handle
+// holds the whole scene; the rank renders its owned bin rows into a compact
+// band (the gs_shard_render layout) with no exchange.  With contiguous
+// ownership the rects are clipped to the band's pixel rows, so splats off
+// the band are culled before their colour is read.
+gs_status gs_band_render(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, float* out_band,
+                         void* stream) {
+    gs_status s = check_ready(h);
+    if (s != GS_OK) return s;
+    if (!view || !proj || !out_band || W <= 0 || H <= 0 || W > 65535 || H > 65535)
+        return fail(GS_ERR_INVALID_ARG, "gs_band_render: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    if (bits_for((uint32_t)(U.tiles_x * U.tiles_y)) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
+    h->slab_frame = false;
+    h->shard_frame = false;
+    h->slab_lists = false;
+    Ownership own;
+    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+    std::memset(&h->stats, 0, sizeof h->stats);
+    if (own.nrows == 0) return GS_OK;  // no owned rows: an empty band
+    const std::vector<uint16_t>& rows = h->rows_host;
+    const bool contiguous = own.dev.owner == nullptr || (int)rows.back() - (int)rows.front() + 1 == (int)rows.size();
+    if (own.dev.owner && contiguous) {
+        U.band_y0 = (int32_t)rows.front() * gs::kBin;
+        U.band_y1 = std::min(H, ((int32_t)rows.back() + 1) * gs::kBin) - 1;
+    }
+    GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));  // a pipelined composite may still read the set
+    begin_frame(h, st);
+    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
+                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
+                                 kernel_event(h, 1), fetch_counter(h)));
+    mark(h, 1, st);
+    if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, own.dev.owner ? 1 : 0, reinterpret_cast<float4*>(out_band),
+                                nullptr, st)) != GS_OK)
+        return s;
+    fill_stats(h, (uint64_t)h->stats.pairs, U);
+    GS_HIP(hipEventRecord(h->set_free[h->set], st));
+    return GS_OK;
 }
 
 gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,

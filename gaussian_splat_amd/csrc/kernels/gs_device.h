@@ -44,6 +44,10 @@ struct FrameUniforms {
     int32_t width, height;
     int32_t tiles_x, tiles_y;  // 32x32 bins (see kBin)
     int32_t cell_mask;         // 1: records carry the 8x8-cell exclusion mask (frames <= 4096 px)
+    // pixel rows [band_y0, band_y1] the rects are clipped to: the frame
+    // (0, height - 1), or one rank's band in the replicated-scene scheme
+    // (gs_band_render), where splats outside it are culled before their colour
+    int32_t band_y0, band_y1;
 };
 
 // Record rect words (record float4 #2 .zw).  With cell masks (frames up to

@@ -315,9 +315,9 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                 float x0f = ceilf(cx - hx - 0.5f), x1f = floorf(cx + hx - 0.5f);
                 float y0f = ceilf(cy - hy - 0.5f), y1f = floorf(cy + hy - 0.5f);
                 x0f = fmaxf(x0f, 0.0f);
-                y0f = fmaxf(y0f, 0.0f);
+                y0f = fmaxf(y0f, (float)U.band_y0);  // (0 unless a band frame)
                 x1f = fminf(x1f, W_ - 1.0f);
-                y1f = fminf(y1f, H_ - 1.0f);
+                y1f = fminf(y1f, (float)U.band_y1);  // (H - 1 unless a band frame)
                 if (x0f <= x1f && y0f <= y1f) {
                     uint32_t x0 = (uint32_t)x0f, x1 = (uint32_t)x1f, y0 = (uint32_t)y0f, y1 = (uint32_t)y1f;
                     float cr, cg, cbl;

@@ -20,6 +20,10 @@ tests/test_distributed.py).  The backend object does the per-rank compute:
 `HipShardBackend` (libgsplat.so) in production; the gloo tests plug in a
 CPU backend from tests/.
 
+`BandRenderer` is SURVEY §8(e)'s fallback: every rank holds the whole
+scene and renders only its owned bin rows (gs_band_render), then the bands
+are gathered as above; no exchange, bit-identical like the row scheme.
+
 `SlabRenderer` is the north star's literal scheme: rank d
 composites depth slab d of the whole frame, then an RCCL reduce sums the
 per-pixel RGBA + weight (alpha) contributions:
@@ -129,6 +133,60 @@ class HipShardBackend:
         check(lib().gs_shard_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
                                     C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_shard_render")
         return band
+
+
+class HipBandBackend:
+    """Per-rank compute of the replicated-scene band scheme (SURVEY §8(e)
+    fallback): the rank holds the WHOLE scene and renders its
+    owned bin rows (gs_band_render); no exchange."""
+
+    def __init__(self, scene: Scene, rank: int, world: int, options: Options, device: int, owner=None):
+        import torch
+
+        self.r = InstancedSplatRenderer(scene, options)
+        self.r.initialize(device)
+        check(lib().gs_shard_configure(self.r._h, rank, world, 0), "gs_shard_configure")
+        self.owner = None if owner is None else np.ascontiguousarray(owner, np.uint8)
+        if self.owner is not None:
+            check(lib().gs_shard_set_rows(self.r._h, self.owner.ctypes.data, len(self.owner)), "gs_shard_set_rows")
+        self.world, self.rank, self.device = world, rank, torch.device(f"cuda:{device}")
+
+    def render(self, view, proj, width, height):
+        import torch
+
+        rows = height if self.world == 1 else band_rows(height, self.world, self.owner)
+        band = torch.empty((rows, width, 4), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().gs_band_render(self.r._h, _mat16(view), _mat16(proj), width, height,
+                                   C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_band_render")
+        return band
+
+
+class BandRenderer:
+    """One rank of a replicated-scene band frame (torch.distributed initialised)."""
+
+    def __init__(self, backend, rank: int, world: int, group=None):
+        self.b, self.rank, self.world, self.group = backend, rank, world, group
+
+    def render(self, view, proj, width, height, gather: bool = True):
+        """The full frame on rank 0 (None elsewhere) when gather=True, else
+        this rank's band."""
+        import torch.distributed as dist
+
+        band = self.b.render(view, proj, width, height)
+        if not gather:
+            return band
+        if self.world == 1:
+            return band[:height]
+        if _host_staged(self.group):
+            hb = band.cpu()
+            bands = [hb.new_empty(hb.shape) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(hb, bands, dst=0, group=self.group)
+            bands = [b.to(band.device) for b in bands] if self.rank == 0 else None
+        else:
+            bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(band, bands, dst=0, group=self.group)
+        return assemble(bands, width, height, self.world, self.b.owner) if self.rank == 0 else None
 
 
 SLAB_BINS = 2048      # GS_SLAB_BINS: slab histogram bins ...

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 5
+#define GSPLAT_ABI_VERSION 6
 
 typedef enum {
     GS_OK = 0,
@@ -208,6 +208,16 @@ gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[
  * 12-bit rect coordinates with the depth key). */
 gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height,
                           float *out_rgba, void *hip_stream);
+
+/* Replicated-scene bands (SURVEY §8(e) fallback).  The handle
+ * holds the WHOLE scene (gs_create / gs_create_subset over all splats) and is
+ * configured with gs_shard_configure(h, rank, world, 0) (+ gs_shard_set_rows).
+ * Renders this rank's owned 32-px bin rows of the frame into out_band (device,
+ * fp32 RGBA, the gs_shard_render band layout: owned rows stacked in ascending
+ * order, rows x 32 x width); no exchange.  Bit-identical to those rows of
+ * gs_render.  With world 1 the band is the whole frame. */
+gs_status gs_band_render(gs_handle *h, const float view[16], const float proj[16], int32_t width, int32_t height,
+                         float *out_band, void *stream);
 int32_t gs_exchange_record_bytes(void);
 
 /* ---- multi-GPU: depth slabs + RGBA reduce --------- */

@@ -117,3 +117,28 @@ class OracleSlabBackend(OracleShardBackend):
         ta = t_all.numpy()
         return torch.from_numpy(O.composite_slab(self._srec, self._sdk, ta.shape[2], ta.shape[1], 2, rank=self.rank,
                                                  t_all=ta, mode=self.mode))
+
+
+class OracleBandBackend:
+    """CPU stand-in for HipBandBackend: the whole scene on every rank, the
+    rank's owned bin rows composited by the oracle into the product's band
+    layout (no exchange)."""
+
+    owner = None
+
+    def __init__(self, scene, rank, world, sh_degree=0, mode="tile", cap=0):
+        self.scene, self.rank, self.world = scene, rank, world
+        self.sh, self.mode, self.cap = sh_degree, mode, cap
+
+    def render(self, view, proj, width, height):
+        import torch
+
+        from gaussian_splat_amd.distributed import band_rows, row_owner
+
+        rec, dk, nt = O.project(self.scene, view, proj, width, height, sh_degree=self.sh)
+        vis = nt > 0
+        band = np.zeros((band_rows(height, self.world), width, 4), np.float32)
+        out = O.composite_records(rec[vis], dk[vis], width, height, owner=row_owner(height, self.world),
+                                  rank=self.rank, compact=True, mode=self.mode, cap=self.cap)
+        band[: out.shape[0]] = out
+        return torch.from_numpy(band)

@@ -66,6 +66,55 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
     assert same, f"sharded frame differs from single-process oracle (L-inf {linf})"
 
 
+def _band_worker(rank, world, port, n, w, h, sh, mode, q):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import torch.distributed as dist
+    from cpu_shard_backend import OracleBandBackend
+    from gaussian_splat_amd import scene as S
+    from gaussian_splat_amd.api import default_camera
+    from gaussian_splat_amd.distributed import BandRenderer
+
+    os.environ["OMP_NUM_THREADS"] = "2"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sc = S.synthetic_scene(n, seed=19, sh_degree=sh, aspect=w / h)
+        cam = default_camera(w, h)
+        cam.orbit(-0.2, 0.1)
+        V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+        frame = BandRenderer(OracleBandBackend(sc, rank, world, sh_degree=sh, mode=mode), rank, world).render(V, P, w, h)
+        if rank == 0:
+            from oracle import oracle_py as O
+            ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
+            got = frame.numpy()
+            q.put((got.shape == ref.shape and bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))),
+                   float(np.abs(got - ref).max()) if got.shape == ref.shape else -1.0))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sh,mode", [(2, 0, "tile"), (3, 3, "live50")])
+def test_gloo_band_frame_bitexact(world, sh, mode):
+    """Replicated-scene bands (SURVEY §8(e) fallback): every rank renders its
+    owned rows of the whole scene; the gathered frame is the oracle frame."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, 20000, 320, 400, sh, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    same, linf = res
+    assert same, f"band frame differs from single-process oracle (L-inf {linf})"
+
+
 def test_assemble_layout():
     import numpy as np
     import torch
