@@ -289,7 +289,10 @@ def main():
             if sch == "bands":  # the whole scene on every rank
                 full = S.activate(S.synthetic_raw(N, seed=args.seed, aspect=W / H, rest=args.sh > 0,
                                                   profile=args.profile), args.sh)
-                be = HipBandBackend(full, rank, world, opts, local)
+                # (no exchange between the frame's stages: two frames in flight as at N=1)
+                import dataclasses
+                be = HipBandBackend(full, rank, world,
+                                    dataclasses.replace(opts, frames_in_flight=args.frames_in_flight), local)
                 sr = BandRenderer(be, rank, world)
             elif sch == "slabs":
                 be = HipSlabBackend(scene, rank, world, b, opts, local)

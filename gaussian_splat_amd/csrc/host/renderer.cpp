@@ -940,16 +940,36 @@ gs_status gs_set_cap(gs_handle* h, int32_t cap) {
 // One frame into a caller-owned framebuffer: fp32 RGBA (16 B/pixel) or, with
 // bgra8, packed BGRA8Unorm (4 B/pixel, converted inside the composite).
 static gs_status render_frame(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
-                              void* out_user, int32_t out_is_device, bool bgra8, void* stream) {
+                              void* out_user, int32_t out_is_device, bool bgra8, void* stream, bool band = false) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
     if (!view || !proj || !out_user || W <= 0 || H <= 0 || W > 65535 || H > 65535)
         return fail(GS_ERR_INVALID_ARG, "gs_render: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const gs::FrameUniforms U = make_uniforms(view, proj, W, H);
+    gs::FrameUniforms U = make_uniforms(view, proj, W, H);
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     if (T == 0 || bits_for(T) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    int compact = 0;
+    if (band) {
+        // this rank's owned bin rows into a compact band; with contiguous
+        // ownership the rects are clipped to the band's pixel rows (splats
+        // off it are culled before their colour is read)
+        h->slab_frame = false;
+        h->slab_lists = false;
+        Ownership own;
+        if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+        if (own.nrows == 0) {  // no owned rows: an empty band
+            std::memset(&h->stats, 0, sizeof h->stats);
+            return GS_OK;
+        }
+        const std::vector<uint16_t>& rows = h->rows_host;
+        if (own.dev.owner && (int)rows.back() - (int)rows.front() + 1 == (int)rows.size()) {
+            U.band_y0 = (int32_t)rows.front() * gs::kBin;
+            U.band_y1 = std::min(H, ((int32_t)rows.back() + 1) * gs::kBin) - 1;
+        }
+        compact = own.dev.owner ? 1 : 0;
+    }
     const size_t bytes = (size_t)W * H * (bgra8 ? 4 : 16);
     void* out = out_user;
     if (!out_is_device) {
@@ -980,7 +1000,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
                                  kernel_event(h, 1), fetch_counter(h)));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
-                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, 0,
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, compact,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
                                 bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st)) != GS_OK)
         return s;
@@ -1260,40 +1280,9 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
 // the band are culled before their colour is read.
 gs_status gs_band_render(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H, float* out_band,
                          void* stream) {
-    gs_status s = check_ready(h);
-    if (s != GS_OK) return s;
-    if (!view || !proj || !out_band || W <= 0 || H <= 0 || W > 65535 || H > 65535)
-        return fail(GS_ERR_INVALID_ARG, "gs_band_render: bad arguments");
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
-    gs::FrameUniforms U = make_uniforms(view, proj, W, H);
-    if (bits_for((uint32_t)(U.tiles_x * U.tiles_y)) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
-    h->slab_frame = false;
-    h->shard_frame = false;
-    h->slab_lists = false;
-    Ownership own;
-    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
-    std::memset(&h->stats, 0, sizeof h->stats);
-    if (own.nrows == 0) return GS_OK;  // no owned rows: an empty band
-    const std::vector<uint16_t>& rows = h->rows_host;
-    const bool contiguous = own.dev.owner == nullptr || (int)rows.back() - (int)rows.front() + 1 == (int)rows.size();
-    if (own.dev.owner && contiguous) {
-        U.band_y0 = (int32_t)rows.front() * gs::kBin;
-        U.band_y1 = std::min(H, ((int32_t)rows.back() + 1) * gs::kBin) - 1;
-    }
-    GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));  // a pipelined composite may still read the set
-    begin_frame(h, st);
-    GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
-                                 h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h)));
-    mark(h, 1, st);
-    if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
-                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, own.dev.owner ? 1 : 0, reinterpret_cast<float4*>(out_band),
-                                nullptr, st)) != GS_OK)
-        return s;
-    fill_stats(h, (uint64_t)h->stats.pairs, U);
-    GS_HIP(hipEventRecord(h->set_free[h->set], st));
-    return GS_OK;
+    if (!out_band) return fail(GS_ERR_INVALID_ARG, "gs_band_render: null output");
+    // (two frames in flight like gs_render when the options ask for them)
+    return render_frame(h, view, proj, W, H, out_band, 1, false, stream, true);
 }
 
 gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the replicated-scene band scheme on one GPU (virtual
+ranks): for world g, each rank's gs_band_render time over the whole 6M SH3
+scene at 1080p (mean of K frames after warm-up), and the slowest rank, the
+compute part of a g-GPU frame (the band gather comes on top).
+
+  python tools/band_probe.py [--splats 6000000] [--worlds 1,2,4,8]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--splats", type=int, default=6_000_000)
+ap.add_argument("--worlds", default="1,2,4,8")
+ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--fif", type=int, default=2, help="frames in flight per rank")
+a = ap.parse_args()
+
+import torch  # noqa: E402
+
+from gaussian_splat_amd import scene as S  # noqa: E402
+from gaussian_splat_amd.api import Options, default_camera  # noqa: E402
+from gaussian_splat_amd.distributed import HipBandBackend  # noqa: E402
+
+W, H = 1920, 1080
+sc = S.synthetic_scene(a.splats, seed=2, sh_degree=3, aspect=W / H)
+cam = default_camera(W, H)
+V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+opt = Options(sh_degree=3, crop=False, frames_in_flight=a.fif)
+res = {}
+for g in [int(x) for x in a.worlds.split(",")]:
+    per = []
+    for r in range(g):
+        be = HipBandBackend(sc, r, g, opt, 0)
+        for _ in range(3):
+            be.render(V, P, W, H)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.frames):
+            be.render(V, P, W, H)
+        torch.cuda.synchronize()
+        per.append((time.perf_counter() - t) * 1e3 / a.frames)
+        st = be.r.last_stats()
+        del be
+        torch.cuda.empty_cache()
+    res[g] = {"ms_per_rank": [round(x, 4) for x in per], "max_ms": round(max(per), 4),
+              "pairs_last_rank": int(st["pairs"])}
+    print(f"[band_probe] world {g}: max {max(per):.4f} ms  ranks {[round(x, 3) for x in per]}", file=sys.stderr,
+          flush=True)
+print(json.dumps({"splats": a.splats, "frame": [W, H], "sh_degree": 3, "scheme": "bands (virtual ranks, one GPU)",
+                  "note": f"per-rank gs_band_render, {a.fif} frame(s) in flight; gather excluded",
+                  "worlds": res}))
