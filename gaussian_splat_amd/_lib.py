@@ -82,6 +82,8 @@ SIGNATURES = {
     "gs_slab_composite": (C.c_int, [_P, _P, _P, _P]),
     "gs_create_sharded": (C.c_int, [C.c_char_p, C.POINTER(GsOptions), C.c_int32, C.POINTER(_P)]),
     "gs_create_sharded_from_handle": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
+    "gs_create_replicated": (C.c_int, [C.c_char_p, C.POINTER(GsOptions), C.c_int32, C.POINTER(_P)]),
+    "gs_create_replicated_from_handle": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
     "gs_group_initialize": (C.c_int, [_P, _P, C.c_int32]),
     "gs_group_set_scheme": (C.c_int, [_P, C.c_int32]),
     "gs_group_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),

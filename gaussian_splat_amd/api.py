@@ -368,7 +368,7 @@ def radix_sort_pairs(keys, vals, bits: int, stream=None):
     return keys, vals
 
 
-SCHEMES = {"rows": 0, "slabs": 1}          # gs_scheme
+SCHEMES = {"rows": 0, "slabs": 1, "bands": 2}  # gs_scheme
 TRANSPORTS = {"auto": 0, "rccl": 1, "copy": 2}  # gs_transport
 
 
@@ -378,16 +378,19 @@ class ShardedGroup:
     the bin-row scheme (bit-identical to one GPU) or the depth-slab scheme;
     RCCL when every rank has its own device, peer copies otherwise."""
 
-    def __init__(self, source, num_gpus: int, options: Optional[Options] = None):
+    def __init__(self, source, num_gpus: int, options: Optional[Options] = None, replicated: bool = False):
+        """replicated: every rank holds the whole scene (gs_create_replicated),
+        rendering its own bin rows ("bands")."""
         self.options = options or Options()
         self._g = C.c_void_p()
+        kind = "replicated" if replicated else "sharded"
         if isinstance(source, InstancedSplatRenderer):
-            check(lib().gs_create_sharded_from_handle(source._h, int(num_gpus), C.byref(self._g)),
-                  "gs_create_sharded_from_handle")
+            check(getattr(lib(), f"gs_create_{kind}_from_handle")(source._h, int(num_gpus), C.byref(self._g)),
+                  f"gs_create_{kind}_from_handle")
         else:
             opt = self.options.to_c()
-            check(lib().gs_create_sharded(str(source).encode(), C.byref(opt), int(num_gpus), C.byref(self._g)),
-                  "gs_create_sharded")
+            check(getattr(lib(), f"gs_create_{kind}")(str(source).encode(), C.byref(opt), int(num_gpus),
+                                                       C.byref(self._g)), f"gs_create_{kind}")
         self.device = None
 
     def initialize(self, devices=None, transport: str = "auto") -> bool:

@@ -202,6 +202,7 @@ struct gs_group {
     int world = 1;
     int64_t n = 0;
     int scheme = GS_SCHEME_ROWS;
+    bool replicated = false;  // every rank holds the whole scene (bands only)
     int transport = GS_TRANSPORT_COPY;
     bool initialized = false;
     std::vector<Rank> r;
@@ -307,6 +308,8 @@ gs_status exchange(gs_group* g, std::vector<int64_t>* nrec) {
     return GS_OK;
 }
 
+gs_status gather_bands(gs_group* g, int Wd, int Ht, float* out);
+
 gs_status render_rows(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out) {
     const int W = g->world;
     const int64_t xb = gs_exchange_record_bytes();
@@ -332,7 +335,13 @@ gs_status render_rows(gs_group* g, const float* V, const float* P, int Wd, int H
              return GS_OK;
          })) != GS_OK)
         return s;
-    // bands (owned rows stacked, contiguous under the default table) into the frame
+    return gather_bands(g, Wd, Ht, out);
+}
+
+// Bands (owned rows stacked, contiguous under the default table) into the
+// frame on devices[0]: RCCL send/recv straight into `out`, or peer copies.
+gs_status gather_bands(gs_group* g, int Wd, int Ht, float* out) {
+    const int W = g->world;
     Rank& r0 = g->r[0];
     auto span = [&](int d, size_t* off, size_t* bytes) {
         int row0, nrows;
@@ -372,6 +381,22 @@ gs_status render_rows(gs_group* g, const float* V, const float* P, int Wd, int H
         GG_HIP(hipMemcpyPeerAsync(out + off, r0.dev, g->r[(size_t)d].band.ptr, g->r[(size_t)d].dev, bytes, r0.st));
     }
     return GS_OK;
+}
+
+// Replicated-scene bands: each rank renders its owned rows
+// of the whole scene (gs_band_render), then the band gather.
+gs_status render_bands(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out) {
+    gs_status s = run_ranks(g, [&](Rank& k, int d) -> gs_status {
+        int row0, nrows;
+        owned_rows(Ht, g->world, d, &row0, &nrows);
+        GG_HIP(k.band.reserve(k.dev, (size_t)std::max(nrows, 1) * gs::kBin * Wd * 16));
+        gs_status st = gs_band_render(k.h, V, P, Wd, Ht, k.band.as<float>(), k.st);
+        if (st != GS_OK) return st;
+        GG_HIP(hipEventRecord(k.ev_done, k.st));
+        return GS_OK;
+    });
+    if (s != GS_OK) return s;
+    return gather_bands(g, Wd, Ht, out);
 }
 
 gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out) {
@@ -484,17 +509,19 @@ gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int 
     return GS_OK;
 }
 
-gs_status make_group(gs_handle* scene, int32_t num_gpus, gs_group** out) {
+gs_status make_group(gs_handle* scene, int32_t num_gpus, gs_group** out, bool replicated = false) {
     if (num_gpus < 1 || num_gpus > gs::kMaxWorld) return gfail(GS_ERR_INVALID_ARG, "num_gpus must be 1..32");
     gs_group* g = new gs_group();
     g->world = num_gpus;
     g->n = gs_point_count(scene);
+    g->replicated = replicated;
+    g->scheme = replicated ? GS_SCHEME_BANDS : GS_SCHEME_ROWS;
     g->r.resize((size_t)num_gpus);
     for (int i = 0; i < num_gpus; ++i) {
         Rank& k = g->r[(size_t)i];
         k.dev = -1;
-        k.base = g->n * i / num_gpus;
-        const int64_t e = g->n * (i + 1) / num_gpus;
+        k.base = replicated ? 0 : g->n * i / num_gpus;
+        const int64_t e = replicated ? g->n : g->n * (i + 1) / num_gpus;
         gs_status s = gs_create_subset(scene, k.base, e, &k.h);
         if (s == GS_OK) s = gs_shard_configure(k.h, i, num_gpus, k.base);
         if (s != GS_OK) {
@@ -514,6 +541,23 @@ gs_status gs_create_sharded_from_handle(const gs_handle* scene, int32_t num_gpus
     if (!out || !scene) return gfail(GS_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
     return make_group(const_cast<gs_handle*>(scene), num_gpus, out);
+}
+
+gs_status gs_create_replicated_from_handle(const gs_handle* scene, int32_t num_gpus, gs_group** out) {
+    if (!out || !scene) return gfail(GS_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return make_group(const_cast<gs_handle*>(scene), num_gpus, out, true);
+}
+
+gs_status gs_create_replicated(const char* ply_path, const gs_options* opt, int32_t num_gpus, gs_group** out) {
+    if (!out || !ply_path) return gfail(GS_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    gs_handle* scene = nullptr;
+    gs_status s = gs_create(ply_path, opt, &scene);
+    if (s != GS_OK) return s;
+    s = make_group(scene, num_gpus, out, true);
+    gs_destroy(scene);
+    return s;
 }
 
 gs_status gs_create_sharded(const char* ply_path, const gs_options* opt, int32_t num_gpus, gs_group** out) {
@@ -585,8 +629,11 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
 }
 
 gs_status gs_group_set_scheme(gs_group* g, int32_t scheme) {
-    if (!g || (scheme != GS_SCHEME_ROWS && scheme != GS_SCHEME_SLABS))
-        return gfail(GS_ERR_INVALID_ARG, "scheme must be GS_SCHEME_ROWS or GS_SCHEME_SLABS");
+    if (!g || (scheme != GS_SCHEME_ROWS && scheme != GS_SCHEME_SLABS && scheme != GS_SCHEME_BANDS))
+        return gfail(GS_ERR_INVALID_ARG, "scheme must be GS_SCHEME_ROWS, GS_SCHEME_SLABS or GS_SCHEME_BANDS");
+    if ((scheme == GS_SCHEME_BANDS) != g->replicated)
+        return gfail(GS_ERR_INVALID_ARG, g->replicated ? "a replicated group renders GS_SCHEME_BANDS only"
+                                                       : "GS_SCHEME_BANDS needs a replicated group (gs_create_replicated)");
     g->scheme = scheme;
     return GS_OK;
 }
@@ -613,6 +660,7 @@ gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int
     GG_HIP(hipEventSynchronize(g->frame_done));
     gs_status s = g->world == 1 ? gs_render(r0.h, view, proj, width, height, out, 1, r0.st)
                  : g->scheme == GS_SCHEME_SLABS ? render_slabs(g, view, proj, width, height, out)
+                 : g->scheme == GS_SCHEME_BANDS ? render_bands(g, view, proj, width, height, out)
                                                 : render_rows(g, view, proj, width, height, out);
     if (s != GS_OK) return s;
     GG_HIP(hipSetDevice(r0.dev));

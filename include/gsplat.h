@@ -266,10 +266,16 @@ gs_status gs_slab_composite(gs_handle *h, const float *t_all, float *out_rgba, v
  * required when ranks share a device).  Drop-in use: replace
  * gs_create/gs_initialize/gs_render by their gs_group counterparts. */
 typedef struct gs_group gs_group;
-typedef enum { GS_SCHEME_ROWS = 0, GS_SCHEME_SLABS = 1 } gs_scheme;
+typedef enum { GS_SCHEME_ROWS = 0, GS_SCHEME_SLABS = 1, GS_SCHEME_BANDS = 2 } gs_scheme;
 typedef enum { GS_TRANSPORT_AUTO = 0, GS_TRANSPORT_RCCL = 1, GS_TRANSPORT_COPY = 2 } gs_transport;
 gs_status gs_create_sharded(const char *ply_path, const gs_options *opt, int32_t num_gpus, gs_group **out);
 gs_status gs_create_sharded_from_handle(const gs_handle *scene, int32_t num_gpus, gs_group **out);
+/* Replicated-scene group: every rank holds the WHOLE
+ * (cropped) scene and renders its owned bin rows (GS_SCHEME_BANDS, the only
+ * scheme of such a group); the bands are gathered into the frame on
+ * devices[0].  Bit-identical to one GPU's frame. */
+gs_status gs_create_replicated(const char *ply_path, const gs_options *opt, int32_t num_gpus, gs_group **out);
+gs_status gs_create_replicated_from_handle(const gs_handle *scene, int32_t num_gpus, gs_group **out);
 /* devices: num_gpus ordinals (NULL = 0 .. num_gpus-1; repeats allowed with
  * GS_TRANSPORT_COPY); transport: gs_transport. */
 gs_status gs_group_initialize(gs_group *g, const int32_t *devices, int32_t transport);

@@ -113,3 +113,22 @@ def test_group_rejects_rccl_on_shared_device(built):
     g = ShardedGroup(r, 2)
     with pytest.raises(GsError):
         g.initialize([0, 0], "rccl")
+
+
+@pytest.mark.parametrize("world,mode,sh", [(2, "tile", 3), (4, "live50", 0)])
+def test_group_replicated_bands_bitexact(built, world, mode, sh):
+    """gs_create_replicated: the whole scene on every rank, owned rows per
+    rank (GS_SCHEME_BANDS), gathered into the frame: the 1-GPU frame."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options, ShardedGroup
+    W, H = 960, 540
+    sc = _scene(80000, 101 + world, sh, W / H)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    g = ShardedGroup(r, world, replicated=True)
+    g.initialize([0] * world, "copy")
+    for V, P in orbit_views(W, H, 2):
+        ref = r.render_host(V, P, W, H)
+        np.testing.assert_array_equal(g.render_host(V, P, W, H).view(np.uint32), ref.view(np.uint32))
+    from gaussian_splat_amd import GsError
+    with pytest.raises(GsError):
+        g.set_scheme("rows")  # a replicated group renders bands only
