@@ -19,6 +19,7 @@ ap.add_argument("--splats", type=int, default=6_000_000)
 ap.add_argument("--worlds", default="1,2,4,8")
 ap.add_argument("--frames", type=int, default=20)
 ap.add_argument("--fif", type=int, default=2, help="frames in flight per rank")
+ap.add_argument("--stages", type=int, default=0, help="world size whose per-rank stage times to print (0: off)")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -52,6 +53,17 @@ for g in [int(x) for x in a.worlds.split(",")]:
               "pairs_last_rank": int(st["pairs"])}
     print(f"[band_probe] world {g}: max {max(per):.4f} ms  ranks {[round(x, 3) for x in per]}", file=sys.stderr,
           flush=True)
+if a.stages:
+    from dataclasses import replace
+    for r in range(a.stages):
+        be = HipBandBackend(sc, r, a.stages, replace(opt, stage_timing=1, frames_in_flight=1), 0)
+        for _ in range(5):
+            be.render(V, P, W, H)
+        torch.cuda.synchronize()
+        st = be.r.last_stats()
+        print(f"[band_probe] world {a.stages} rank {r}: " + " ".join(
+            f"{k[3:]}={st[k]:.4f}" for k in st if k.startswith("ms_")), file=sys.stderr, flush=True)
+        del be
 print(json.dumps({"splats": a.splats, "frame": [W, H], "sh_degree": 3, "scheme": "bands (virtual ranks, one GPU)",
                   "note": f"per-rank gs_band_render, {a.fif} frame(s) in flight; gather excluded",
                   "worlds": res}))
