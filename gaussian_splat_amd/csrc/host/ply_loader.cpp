@@ -84,6 +84,19 @@ bool PLYLoader::load(const std::string& filepath, std::vector<PointData>& points
     for (size_t j = 0; j < np; ++j)
         if (slot[j] >= S_R && slot[j] <= S_B) dc_col[slot[j] - S_R] = (int)j;
 
+    // A vertex count far beyond the file: the reference would allocate it all
+    // (vertexCount x 248 B) and fail; reject it instead.  Moderately truncated
+    // payloads keep the reference's stale-chunk results below.
+    {
+        const std::streamoff hdr_end = file.tellg();
+        file.seekg(0, std::ios::end);
+        const std::streamoff fsize = file.tellg();
+        file.seekg(hdr_end);
+        if (hdr_end < 0 || fsize < 0 || !file) return false;
+        const double have = (double)(fsize - hdr_end);
+        const double claimed = binary ? (double)vcount * (double)np * 4.0 : (double)vcount;  // ASCII: >= 1 B per line
+        if (claimed > 2.0 * have + 64.0 && (double)vcount * sizeof(PointData) > 256.0 * 1024 * 1024) return false;
+    }
     points.clear();
     points.resize(vcount);
     if (raw_dc) raw_dc->assign((size_t)vcount * 3, 0.0f);
