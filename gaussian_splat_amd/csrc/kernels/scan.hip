@@ -323,6 +323,101 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
     emit_bin_pairs(r, tiles_x, src.own, 0u, order ? order[j] : j, offsets[j], keys, vals);
 }
 
+// a / b for the small quotients of the emission (a < 2^32, b < 2^16): float
+// reciprocal, then one correction step (the estimate is off by at most one)
+__device__ __forceinline__ uint32_t udiv_est(uint32_t a, uint32_t b) {
+    uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
+    const int64_t r = (int64_t)a - (int64_t)q * b;
+    if (r < 0) --q;
+    else if (r >= (int64_t)b) ++q;
+    return q;
+}
+
+// Position (0..15) of the i-th set bit of a 16-bit mask (i < popcount).
+__device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
+    uint32_t b = 0;
+    uint32_t c = (uint32_t)__builtin_popcount(m & 0xFFu);
+    if (i >= c) { i -= c; m >>= 8; b += 8; }
+    c = (uint32_t)__builtin_popcount(m & 0xFu);
+    if (i >= c) { i -= c; m >>= 4; b += 4; }
+    c = (uint32_t)__builtin_popcount(m & 0x3u);
+    if (i >= c) { i -= c; m >>= 2; b += 2; }
+    return b + (i >= (m & 1u) ? 1u : 0u);
+}
+
+// Depth-ordered duplicate, wave-cooperative (every bin row owned): in depth
+// order the splats' sizes follow their depth, so one splat per lane leaves
+// most lanes idle behind a few large near splats.  A wave's 64 splats own the
+// contiguous pair range [off0, off0 + T); lane q of a 64-pair chunk writes
+// pair off0 + q0 + q (coalesced).  Its splat: the last lane whose range
+// starts at or before it (start marks in LDS, an inclusive max-scan); its
+// bin: the (q - start)-th bin of that splat's rect in row-major order, minus
+// the excluded bins -- exactly what duplicate_kernel's loop writes there.
+__global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint32_t n,
+                                                             const uint32_t* __restrict__ order,
+                                                             const uint32_t* __restrict__ offsets, uint32_t tiles_x,
+                                                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                             const uint32_t* __restrict__ npairs) {
+    __shared__ uint32_t mk[4][64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t w0 = blockIdx.x * 256u + wave * 64u;
+    if (w0 >= n || *npairs == 0u) return;  // (whole wave; no workgroup barrier below)
+    const uint32_t j = w0 + lane, jc = j < n ? j : n - 1u;
+    uint32_t lo = src.lo[jc], hi = src.hi[jc];
+    const uint32_t off = offsets[jc];
+    const uint32_t val = order ? order[jc] : jc;
+    if (j >= n) {
+        lo = kEmptyRectLo;
+        hi = 0u;
+    }
+    const BinRect r = bin_rect(lo, hi, src.masked);
+    const uint32_t c = rect_tile_count(lo, hi, src.own, src.masked);
+    const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
+    const uint32_t start = off - off0;
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c > 0u ? start + c : 0u), 63);
+    const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u;
+    uint32_t inc = 0;  // with excluded bins (rect <= 4x4 bins): the included ones, bit dy*4 + dx
+    if (r.excl) {
+        const uint32_t rm = (1u << cols) - 1u;
+#pragma unroll
+        for (uint32_t dy = 0; dy < 4u; ++dy)
+            if (dy < rows) inc |= rm << (4u * dy);
+        inc &= ~r.excl;
+    }
+    const uint32_t pa = r.bx0 | (r.by0 << 16), pb = (cols & 0xFFFFu) | (inc << 16);
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
+        wave_lds_sync();  // the last chunk's mark reads are done
+        mk[wave][lane] = 0u;
+        wave_lds_sync();
+        if (c > 0u && start >= q0 && start - q0 < 64u) mk[wave][start - q0] = lane + 1u;
+        wave_lds_sync();
+        uint32_t own1 = wave_scan_dpp<true>(mk[wave][lane]);
+        own1 = own1 > carry ? own1 : carry;
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)own1, 63);
+        const int ol = (int)(own1 > 0u ? own1 - 1u : 0u);
+        const uint32_t o_start = (uint32_t)__shfl((int)start, ol, 64);
+        const uint32_t o_pa = (uint32_t)__shfl((int)pa, ol, 64);
+        const uint32_t o_pb = (uint32_t)__shfl((int)pb, ol, 64);
+        const uint32_t o_val = (uint32_t)__shfl((int)val, ol, 64);
+        const uint32_t q = q0 + lane;
+        if (q < T) {
+            const uint32_t li = q - o_start, oinc = o_pb >> 16, ocols = o_pb & 0xFFFFu;
+            uint32_t dy, dx;
+            if (oinc) {
+                const uint32_t b = nth_bit16(oinc, li);
+                dy = b >> 2;
+                dx = b & 3u;
+            } else {
+                dy = udiv_est(li, ocols);
+                dx = li - dy * ocols;
+            }
+            keys[off0 + q] = ((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx;
+            vals[off0 + q] = o_val;
+        }
+    }
+}
+
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
@@ -357,7 +452,12 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
-        duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
+#ifndef GS_AB_DUP_LANE
+        if (!own.owner)
+            duplicate_coop_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
+        else
+#endif
+            duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
         return hipGetLastError();
     }
     scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
