@@ -89,7 +89,7 @@ struct SortPlan {
     int width[kMaxSortPasses];
     uint32_t mask[kMaxSortPasses];
 };
-SortPlan make_sort_plan(int bits);
+SortPlan make_sort_plan(int bits, bool narrow_first = false);  // narrow_first: the depth sort (radix_sort.hip)
 // Scratch words (uint32) needed by launch_radix_sort for n items.
 size_t radix_sort_scratch_words(uint32_t n);
 // Items per tile of launch_radix_sort (its C matrix has ceil(n / tile) columns

@@ -307,14 +307,18 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     }
 }
 
-SortPlan make_sort_plan(int bits) {
+SortPlan make_sort_plan(int bits, bool narrow_first) {
     SortPlan p{};
     if (bits <= 0) return p;
     p.passes = (bits + 7) / 8;
-    // balanced digit widths (e.g. 13 -> 7+6, 15 -> 8+7)
+    // balanced digit widths, the wider first (13 -> 7+6, 15 -> 8+7) or, with
+    // narrow_first, the narrower (15 -> 7+8).  Measured: the one-array bin
+    // sort is faster wide-first (1080p 128 vs 135 us), the three-array depth
+    // sort narrow-first (6M splats 145 vs 132 us): its low 8-bit digits split
+    // a 4096-item tile into 256 runs of ~16 items, partial lines per array.
     int left = bits;
     for (int i = 0; i < p.passes; ++i) {
-        const int w = (left + (p.passes - i) - 1) / (p.passes - i);
+        const int w = narrow_first ? left / (p.passes - i) : (left + (p.passes - i) - 1) / (p.passes - i);
         p.shift[i] = bits - left;
         p.width[i] = w;
         p.mask[i] = (1u << w) - 1u;
@@ -354,7 +358,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
                                   const uint32_t* n_dev, bool first_counted) {
     *result_in_tmp = false;
-    const SortPlan plan = make_sort_plan(bits);
+    const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
     const uint32_t tiles = (n + tile_items(NV) - 1) / tile_items(NV);
     uint32_t* C = scratch;                                   // [digit][tile]
