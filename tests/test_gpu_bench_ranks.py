@@ -1,0 +1,31 @@
+"""The driver's multi-GPU bench path, rehearsed on one GPU: `bench.py --gpus 2`
+starts two rank processes itself (torch.distributed.run, 127.0.0.1), both on
+device 0 with gloo collectives (GS_BENCH_SAME_DEVICE / GS_BENCH_BACKEND are
+rehearsal knobs the driver never sets).  Checks that every scheme runs and
+rank 0 prints one well-formed JSON line with value = the faster exact scheme."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_bench_two_rank_rehearsal(built):
+    env = dict(os.environ, GS_BENCH_BACKEND="gloo", GS_BENCH_SAME_DEVICE="1")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--splats", "300000", "--cpu-baseline", "0", "--pmc", "0"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["global_splats"] == 300000
+    assert set(d["schemes"]) == {"rows", "bands", "slabs"}
+    best = min(d["schemes"][k]["ms_per_step"] for k in ("rows", "bands"))
+    assert abs(d["ms_per_step"] - best) < 1e-3
+    assert d["value"] > 0 and d["scaling"] == "strong"
