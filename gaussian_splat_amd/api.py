@@ -51,7 +51,9 @@ class Options:
     stage_timing: int = 0  # 0 off, 1 every stage (adds event gaps), 2 preprocess + composite only
     cap: int = 0  # per-pixel fragment cap by arrival order (0 = none; 32 tile shader, 50 live shader)
     frames_in_flight: int = 1  # 2: projection/sort of a frame overlaps the previous frame's composite
-    binning: str = "default"  # bin-list build order: "default" (= bin-first), "depth_first", "bin_first"
+    # bin-list build order: "default" (per frame from the previous frame's pair count at this
+    # resolution; depth-first on the first frame), "depth_first", "bin_first"
+    binning: str = "default"
 
     def to_c(self) -> GsOptions:
         o = GsOptions()

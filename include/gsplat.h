@@ -72,9 +72,11 @@ typedef struct gs_options {
                               on the caller's stream in call order.  Device outputs only;
                               stage_timing 1 renders with 1. */
     int32_t binning;       /* order in which the bin lists are built (same lists, same image):
-                              0 = default (bin-first), 1 = depth-first (global depth sort of the
-                              splats, then binning), 2 = bin-first (bin lists in arrival order,
-                              then a stable per-bin depth sort).  DESIGN.md §1 */
+                              0 = default: chosen per frame by a cost model fed with the pair
+                              count of the previous frame at the same resolution (the first frame
+                              at a resolution goes depth-first), 1 = depth-first (global depth
+                              sort of the splats, then binning), 2 = bin-first (bin lists in
+                              arrival order, then a stable per-bin depth sort).  DESIGN.md §1 */
     int32_t reserved[4];
 } gs_options;
 

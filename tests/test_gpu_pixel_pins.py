@@ -1,0 +1,54 @@
+"""K6 + F1 per pixel on the device: the HIP path (preprocess + binning +
+composite, through the C-ABI) against the float64 raster restatement of
+tile.metal:142-156,185-197,239-266 (tests/pixel_pins.py), not against the
+oracle.  Bars as in tests/pixel_pins.py: alpha within 1e-6 given the
+device's own record, within 2e-5 from the splat's parameters, frames within
+1e-4 per channel off the straddle mask; straddling pixels are counted."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import pixel_pins as PX
+
+pytestmark = pytest.mark.gpu
+
+KP = json.loads((Path(__file__).resolve().parent / "golden" / "known_answers.json").read_text())["k_pins"]
+
+
+def _renderer(scene, **kw):
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    r = InstancedSplatRenderer(scene, Options(**kw))
+    r.initialize(0)
+    return r
+
+
+@pytest.mark.parametrize("name", sorted(PX.alpha_pins()))
+def test_device_alpha_pins(built, name):
+    pin = PX.alpha_pins()[name]
+    sp = next(s for s in KP["splats"] if s["name"] == name)
+    cam = KP["cameras"][sp["camera"]]
+    V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+    W, H = KP["width"], KP["height"]
+    sc = PX.pin_scene(sp)
+    r = _renderer(sc)
+    img = r.render_host(V, P, W, H)
+    worst, nst, nflip = PX.check_alpha(img, pin)
+    # K6 + F1 alone, at the device's own record
+    rec, dk, nt = r.project_host(V, P, W, H)
+    zf = float(np.float32(sp["expect"]["zf"]))
+    x0, y0, al, st = PX.record_alpha(rec[0], zf, W, H)
+    w2, nst2, nflip2 = PX.check_alpha(img, {"x0": x0, "y0": y0, "alpha": al, "straddle": st}, tol=PX.ALPHA_TOL)
+    print(f"{name}: e2e {worst:.3g} ({nst} straddling, {nflip} differ); given record {w2:.3g} "
+          f"({nst2} straddling, {nflip2} differ)")
+
+
+@pytest.mark.parametrize("binning", ["depth_first", "bin_first"])
+@pytest.mark.parametrize("name", PX.frame_names())
+def test_device_pixel_frames(built, name, binning):
+    fx = PX.load_frame(name)
+    r = _renderer(PX.frame_scene(fx), binning=binning)
+    img = r.render_host(fx["view"], fx["proj"], int(fx["width"]), int(fx["height"]))
+    worst, nst, nflip = PX.check_frame(img, fx)
+    print(f"{name} ({binning}): max error {worst:.3g}, {nst} straddling pixels ({nflip} beyond 1e-4)")

@@ -206,3 +206,53 @@ def test_sh_basis_pins():
         rec, dbg = O.project_debug(sc, V, P, kp["width"], kp["height"], sh_degree=c["deg"])
         assert dbg["visible"][0]
         np.testing.assert_allclose([rec[0]["r"], rec[0]["g"], rec[0]["b"]], c["rgb"], rtol=2e-5, atol=2e-6)
+
+
+# ---- K6 + F1 per pixel (tests/pixel_pins.py; tools/make_golden.py --pixels) ----
+import pixel_pins as PX  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(PX.alpha_pins()))
+def test_pixel_alpha_pins(name):
+    """K6 (quad coverage) + F1 (gaussian, 0.01 cutoff, alpha) of one splat at
+    every pixel of its quad's box, the oracle against the float64 raster
+    restatement (edge functions + barycentric uv, tile.metal:142-156,185-197):
+    within 1e-6 off the straddling centres, which are counted."""
+    pin = PX.alpha_pins()[name]
+    kp = KA["k_pins"]
+    sp = next(s for s in kp["splats"] if s["name"] == name)
+    cam = kp["cameras"][sp["camera"]]
+    V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+    img, _ = O.render(PX.pin_scene(sp), V, P, kp["width"], kp["height"])
+    worst, nst, nflip = PX.check_alpha(img, pin)
+    print(f"{name}: max |alpha - pin| {worst:.3g}, {nst} straddling centres ({nflip} differ)")
+
+
+@pytest.mark.parametrize("name", PX.frame_names())
+def test_pixel_frames(name):
+    """Small frames of overlapping rotated splats (needles, dense stacks that
+    saturate, half-depth ties) against the float64 tile-rule image: within
+    1e-4 per channel off the straddle mask."""
+    fx = PX.load_frame(name)
+    img, _ = O.render(PX.frame_scene(fx), fx["view"], fx["proj"], int(fx["width"]), int(fx["height"]))
+    worst, nst, nflip = PX.check_frame(img, fx)
+    assert img[..., 3].max() > 0.9
+    print(f"{name}: max error {worst:.3g}, {nst} straddling pixels ({nflip} beyond 1e-4)")
+
+
+@pytest.mark.parametrize("name", sorted(PX.alpha_pins()))
+def test_pixel_alpha_given_record(name):
+    """K6 + F1 alone: the float64 raster restatement evaluated at the oracle's
+    own fp32 record (centre, conic, opacity taken exactly) against the
+    oracle's frame, within 1e-6 off the straddling centres."""
+    kp = KA["k_pins"]
+    sp = next(s for s in kp["splats"] if s["name"] == name)
+    cam = kp["cameras"][sp["camera"]]
+    V, P = np.array(cam["view"], np.float32), np.array(cam["proj"], np.float32)
+    sc = PX.pin_scene(sp)
+    W, H = kp["width"], kp["height"]
+    rec, dbg = O.project_debug(sc, V, P, W, H)
+    x0, y0, al, st = PX.record_alpha(rec[0], float(dbg["zf"][0]), W, H)
+    img, _ = O.render(sc, V, P, W, H)
+    worst, nst, nflip = PX.check_alpha(img, {"x0": x0, "y0": y0, "alpha": al, "straddle": st}, tol=PX.ALPHA_TOL)
+    print(f"{name}: max |alpha - pin(record)| {worst:.3g}, {nst} straddling centres ({nflip} differ)")

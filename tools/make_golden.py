@@ -345,7 +345,172 @@ def k_pins() -> dict:
     return out
 
 
+# ---- K6 + F1 (+ S1/A1) per pixel ----
+# The float64 raster restatement itself lives in tests/pixel_pins.py (the
+# GPU tests evaluate it at the device's own records too); these functions
+# build the committed fixtures from it.
+sys.path.insert(0, str(ROOT / "tests"))
+from pixel_pins import STRADDLE, ref64_quad_alpha  # noqa: E402
+
+
+def _vertex_alpha(v: dict, opacity: float, W: int, H: int):
+    if not v.get("visible"):
+        return 0, 0, np.zeros((0, 0)), np.zeros((0, 0), bool)
+    return ref64_quad_alpha(v["cx"], v["cy"], v["e1"], v["r1"], v["r2"], v["zf"], opacity, W, H)
+
+
+def _half(x) -> float:
+    return float(np.float16(np.float32(x)))
+
+
+def ref64_frame(splats: list, W: int, H: int):
+    """Tile-rule frame in float64 (tile.metal:239-266): per pixel the covering
+    fragments sorted by descending half depth, ties in arrival (index) order,
+    then sa = a (1 - A), C += rgb sa, A += sa, break at A >= 0.99.  splats:
+    (vertex dict, opacity, rgb).  Returns (rgba[H, W, 4] float64, straddle
+    mask[H, W]): a pixel is flagged if any fragment straddles K6/F1 or if A
+    lands within STRADDLE of the 0.99 break at some step."""
+    frags = [[[] for _ in range(W)] for _ in range(H)]
+    strad = np.zeros((H, W), bool)
+    for i, (v, op, rgb) in enumerate(splats):
+        x0, y0, al, st = _vertex_alpha(v, op, W, H)
+        if al.size == 0:
+            continue
+        strad[y0:y0 + al.shape[0], x0:x0 + al.shape[1]] |= st
+        for yy, xx in zip(*np.nonzero(al)):
+            frags[y0 + yy][x0 + xx].append((-_half(v["zf"]), i, al[yy, xx], rgb))
+    out = np.zeros((H, W, 4))
+    for y in range(H):
+        for x in range(W):
+            A, C = 0.0, np.zeros(3)
+            for _, _, a, rgb in sorted(frags[y][x], key=lambda f: (f[0], f[1])):
+                sa = a * (1.0 - A)
+                C = C + np.asarray(rgb) * sa
+                A += sa
+                if abs(A - 0.99) < STRADDLE:
+                    strad[y, x] = True
+                if A >= 0.99:
+                    break
+            out[y, x, :3], out[y, x, 3] = C, A
+    return out, strad
+
+
+def _look_at64(eye, tgt, up):
+    e, t = np.asarray(eye, np.float64), np.asarray(tgt, np.float64)
+    f = (t - e) / np.linalg.norm(t - e)
+    s = np.cross(f, up)
+    s /= np.linalg.norm(s)
+    u = np.cross(s, f)
+    V = np.eye(4)
+    V[0, :3], V[1, :3], V[2, :3] = s, u, -f
+    V[:3, 3] = [-s @ e, -u @ e, f @ e]
+    return V
+
+
+def _persp64(fov, aspect, n, fr):
+    ys = 1 / math.tan(math.radians(fov) / 2)
+    P = np.zeros((4, 4))
+    P[0, 0], P[1, 1] = ys / aspect, ys
+    P[2, 2], P[2, 3], P[3, 2] = -(fr + n) / (fr - n), -2 * fr * n / (fr - n), -1
+    return P
+
+
+def _half_safe(zf: float) -> bool:
+    """zF far enough from a half rounding boundary that fp32 rounding of the
+    projection cannot move its S1 key."""
+    return _half(zf * (1 - 4e-6)) == _half(zf * (1 + 4e-6))
+
+
+def pixel_frames() -> dict:
+    """Small frames of overlapping rotated splats (SH 0) and their float64
+    tile-rule images: name -> dict of arrays for np.savez."""
+    specs = [
+        # name, W, H, eye, n, scale range (log10), opacity range, seed
+        ("rotated_96x64", 96, 64, (0.0, 2.0, 5.0), 40, (-1.6, -0.7), (0.2, 0.98), 11),
+        ("needles_128x72", 128, 72, (1.5, 1.0, 4.5), 36, (-2.6, -0.6), (0.3, 0.99), 12),
+        ("dense_64x64", 64, 64, (0.0, 0.5, 3.5), 160, (-1.7, -1.0), (0.5, 0.995), 13),
+        ("ties_80x80", 80, 80, (0.0, 0.0, 4.0), 24, (-1.4, -0.9), (0.3, 0.9), 14),
+    ]
+    out = {}
+    for name, W, H, eye, n, (lo, hi), (olo, ohi), seed in specs:
+        rng = np.random.default_rng(seed)
+        V = _f32(_look_at64(eye, [0, 0, 0], [0, -1, 0]))
+        P = _f32(_persp64(45, W / H, 0.1, 1000))
+        s, u, f = V[0, :3], V[1, :3], -V[2, :3]
+        e = np.asarray(eye, np.float64)
+        t = math.tan(math.radians(22.5))
+        pos, rot, scale, opac, col = [], [], [], [], []
+        while len(pos) < n:
+            z = rng.uniform(2.5, 6.5)
+            p = e + z * f + rng.uniform(-0.8, 0.8) * z * t * (W / H) * s + rng.uniform(-0.8, 0.8) * z * t * u
+            if name.startswith("ties") and len(pos) % 6 == 1:
+                # same half depth as the previous splat, different fp32 zF:
+                # S1's tie goes to the earlier arrival (index)
+                p = pos[-1] + rng.uniform(-1e-3, 1e-3) * f + 0.03 * s
+            sc = 10 ** rng.uniform(lo, hi, 3)
+            if name.startswith("needles"):
+                sc[rng.integers(3)] *= 12.0  # long thin splats: the quad's box edge and the cutoff matter
+            cand = (_f32(p), _f32(rng.normal(0, 1, 4)), _f32(sc))
+            v = ref64_vertex(*cand, V, P, W, H)
+            if not v["visible"] or not _half_safe(v["zf"]):
+                continue
+            if name.startswith("ties") and len(pos) % 6 == 1:
+                if _half(v["zf"]) != _half(ref64_vertex(pos[-1], rot[-1], scale[-1], V, P, W, H)["zf"]):
+                    continue
+            pos.append(cand[0]); rot.append(cand[1]); scale.append(cand[2])
+            opac.append(float(np.float32(rng.uniform(olo, ohi))))
+            col.append(_f32(rng.uniform(0, 1, 3)))
+        splats = [(ref64_vertex(pos[i], rot[i], scale[i], V, P, W, H), opac[i], col[i]) for i in range(n)]
+        if name.startswith("ties"):
+            assert all(_half(splats[i][0]["zf"]) == _half(splats[i - 1][0]["zf"])
+                       and splats[i][0]["zf"] != splats[i - 1][0]["zf"] for i in range(1, n, 6))
+        img, strad = ref64_frame(splats, W, H)
+        out[name] = {"view": V.astype(np.float32), "proj": P.astype(np.float32), "width": np.int32(W),
+                     "height": np.int32(H), "pos": np.array(pos, np.float32), "rot": np.array(rot, np.float32),
+                     "scale": np.array(scale, np.float32), "opacity": np.array(opac, np.float32),
+                     "color": np.array(col, np.float32), "rgba": img.astype(np.float32),
+                     "straddle": strad.astype(np.uint8)}
+        print(f"{name}: {W}x{H}, {n} splats, covered {int((img[..., 3] > 0).sum())} px, "
+              f"straddling {int(strad.sum())} px")
+    return out
+
+
+def pixel_alpha_pins() -> dict:
+    """Per-pixel alpha of every visible k_pin splat over its quad's pixel box
+    (1920x1080, opacity 0.7): name -> dict(x0, y0, alpha float32, straddle)."""
+    kp = k_pins()
+    W, H = kp["width"], kp["height"]
+    out = {}
+    for sp in kp["splats"]:
+        e = sp["expect"]
+        if not e["visible"]:
+            continue
+        x0, y0, al, st = _vertex_alpha(e, float(np.float32(0.7)), W, H)
+        out[sp["name"]] = {"x0": np.int32(x0), "y0": np.int32(y0), "alpha": al.astype(np.float32),
+                           "straddle": st.astype(np.uint8)}
+        print(f"{sp['name']}: box {al.shape[1]}x{al.shape[0]} at ({x0},{y0}), "
+              f"{int((al > 0).sum())} covered, {int(st.sum())} straddling")
+    return out
+
+
+def write_pixel_fixtures() -> None:
+    d = GOLD / "pixels"
+    d.mkdir(parents=True, exist_ok=True)
+    for name, arrs in pixel_frames().items():
+        np.savez_compressed(d / f"frame_{name}.npz", **arrs)
+    pins = pixel_alpha_pins()
+    flat = {}
+    for name, a in pins.items():
+        for k, v in a.items():
+            flat[f"{name}__{k}"] = v
+    np.savez_compressed(d / "alpha_pins.npz", **flat)
+    print("wrote", d)
+
+
 if __name__ == "__main__":
+    if "--pixels" in sys.argv:  # K6 + F1 per-pixel pins (float64), no reference build needed
+        write_pixel_fixtures()
+        sys.exit(0)
     if "--known-only" in sys.argv:  # the float64 pins need no reference build
         ka = json.loads((GOLD / "known_answers.json").read_text()) if (GOLD / "known_answers.json").exists() else {}
         ka.update(known_answers())
