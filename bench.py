@@ -97,6 +97,8 @@ def parse():
                     help="N=1: 2 = a frame's projection/sort overlaps the previous frame's composite")
     ap.add_argument("--scheme", default="all", choices=["rows", "slabs", "bands", "both", "all"],
                     help="N>1: bin-row ownership (exact; value), depth slabs + RGBA reduce, or both")
+    ap.add_argument("--comm-timeout", type=float, default=120.0,
+                    help="N>1: seconds before a rendezvous or collective that a peer never joins fails")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     a.splats = a.splats or c["splats"]
@@ -229,11 +231,12 @@ def main():
     if os.environ.get("GS_BENCH_SAME_DEVICE") == "1":
         local = 0
     if world > 1:
+        from gaussian_splat_amd.distributed import init_ranks
+
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
+        # bounded: a rank that never joins or stops answering makes the others
+        # exit non-zero after --comm-timeout seconds instead of hanging
+        init_ranks(backend, args.comm_timeout, device=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
 
     from gaussian_splat_amd import scene as S

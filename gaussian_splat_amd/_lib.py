@@ -86,6 +86,7 @@ SIGNATURES = {
     "gs_create_replicated_from_handle": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
     "gs_group_initialize": (C.c_int, [_P, _P, C.c_int32]),
     "gs_group_set_scheme": (C.c_int, [_P, C.c_int32]),
+    "gs_group_set_timeout": (C.c_int, [_P, C.c_int32]),
     "gs_group_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
     "gs_group_point_count": (C.c_int64, [_P]),
     "gs_group_size": (C.c_int32, [_P]),

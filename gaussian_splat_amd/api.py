@@ -421,6 +421,11 @@ class ShardedGroup:
     def set_scheme(self, scheme: str):
         check(lib().gs_group_set_scheme(self._g, SCHEMES[scheme]), "gs_group_set_scheme")
 
+    def set_timeout(self, timeout_ms: int):
+        """Bound of every host wait (gs_group_set_timeout): an expired wait or
+        an RCCL peer error aborts the communicators and raises (GS_ERR_COMM)."""
+        check(lib().gs_group_set_timeout(self._g, int(timeout_ms)), "gs_group_set_timeout")
+
     def render(self, view, proj, width: int, height: int, out=None, stream=None):
         import torch
 

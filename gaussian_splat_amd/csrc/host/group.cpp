@@ -21,11 +21,19 @@
 // bytes with peer copies (hipMemcpyPeerAsync) and sums slab contributions
 // on devices[0] in rank order — the only choice when ranks share a device
 // (virtual ranks on one GPU, the tests' configuration).
+//
+// Failure handling (the reference's only recovery is
+// instanced_splat_renderer.mm:319-336): every host wait of a group is
+// bounded (gs_group_set_timeout, default GS_COMM_TIMEOUT_MS or 60 s) and,
+// under RCCL, polls ncclCommGetAsyncError; a peer error or an expired wait
+// aborts every communicator (ncclCommAbort) and fails the frame with
+// GS_ERR_COMM.  The group is then unusable (later calls return GS_ERR_COMM).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -67,6 +75,8 @@ struct Rccl {
     decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclReduce) reduce = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
     bool load(std::string* why) {
         if (so) return true;
         for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
@@ -92,6 +102,8 @@ struct Rccl {
         sym(all_gather, "ncclAllGather");
         sym(reduce, "ncclReduce");
         sym(error_string, "ncclGetErrorString");
+        sym(async_error, "ncclCommGetAsyncError");
+        sym(comm_abort, "ncclCommAbort");
         if (!ok) *why = "RCCL: missing symbols";
         return ok;
     }
@@ -210,7 +222,8 @@ struct gs_group {
     Pool* pool = nullptr;
     hipEvent_t frame_done = nullptr;  // on devices[0]: everything of the last frame
     DevMem fb;                        // host-output frames
-    gs_stats stats{};
+    int64_t timeout_ms = 60000;       // bound of every host wait (gs_group_set_timeout)
+    bool failed = false;              // communicators aborted: the group is unusable
     ~gs_group() {
         delete pool;
         for (auto& k : r) {
@@ -222,7 +235,7 @@ struct gs_group {
             gs_destroy(k.h);
         }
         for (ncclComm_t c : comms)
-            if (c) (void)g_rccl.comm_destroy(c);
+            if (c) (void)(failed ? g_rccl.comm_abort(c) : g_rccl.comm_destroy(c));
         if (frame_done) (void)hipEventDestroy(frame_done);
         fb.release();
     }
@@ -240,13 +253,58 @@ gs_status run_ranks(gs_group* g, const std::function<gs_status(Rank&, int)>& f) 
             k.error = "hipSetDevice";
             return;
         }
-        k.status = f(k, i);
-        k.error = k.status == GS_OK ? std::string() : std::string(gs_last_error());
+        // nothing may escape a worker thread (std::terminate): allocation
+        // failures map to GS_ERR_OOM, anything else to GS_ERR_DEVICE
+        try {
+            k.status = f(k, i);
+            k.error = k.status == GS_OK ? std::string() : std::string(gs_last_error());
+        } catch (const std::bad_alloc&) {
+            k.status = GS_ERR_OOM;
+            k.error = "out of host memory";
+        } catch (const std::exception& e) {
+            k.status = GS_ERR_DEVICE;
+            k.error = e.what();
+        } catch (...) {
+            k.status = GS_ERR_DEVICE;
+            k.error = "unknown exception";
+        }
     };
     g->pool->run(job);
     for (auto& k : g->r)
         if (k.status != GS_OK) return gfail(k.status, "rank: " + k.error);
     return GS_OK;
+}
+
+// Abort every communicator after a peer error or an expired wait.
+gs_status comm_failure(gs_group* g, const std::string& why) {
+    if (g->transport == GS_TRANSPORT_RCCL && !g->failed)
+        for (ncclComm_t c : g->comms)
+            if (c) (void)g_rccl.comm_abort(c);
+    g->failed = true;
+    return gfail(GS_ERR_COMM, why);
+}
+
+// Host wait for `ev` (recorded on a stream of device `dev`), bounded by the
+// group's timeout; under RCCL each poll also checks every communicator's
+// asynchronous error state.
+gs_status wait_bounded(gs_group* g, int dev, hipEvent_t ev, const char* what) {
+    GG_HIP(hipSetDevice(dev));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return GS_OK;
+        if (e != hipErrorNotReady) GG_HIP(e);
+        if (g->transport == GS_TRANSPORT_RCCL)
+            for (ncclComm_t c : g->comms) {
+                ncclResult_t ae = ncclSuccess;
+                if (c && g_rccl.async_error(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+                    return comm_failure(g, std::string(what) + ": RCCL peer error: " + g_rccl.error_string(ae));
+            }
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > g->timeout_ms)
+            return comm_failure(g, std::string(what) + ": no completion within " + std::to_string(g->timeout_ms) + " ms");
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
 }
 
 // Row ownership of the default table (gs_shard_set_rows not used by groups):
@@ -259,51 +317,59 @@ void owned_rows(int H, int world, int d, int* row0, int* nrows) {
 
 // All-to-all of the exchange records: rank d receives, in source-rank order,
 // the records every rank packed for it.  Returns the received counts.
+// One transfer of the all-to-all: n records from src's send buffer at
+// record offset soff into dst's receive buffer at roff.  Both transports run
+// this same plan, so the peer-copy path the one-GPU tests exercise checks
+// the offsets the RCCL path sends and receives at.
+struct Xfer {
+    int src, dst;
+    int64_t soff, roff, n;
+};
+
+// counts[s][d]: records rank s packed for rank d (grouped by destination in
+// s's send buffer); d receives them in source-rank order.
+std::vector<Xfer> exchange_plan(const std::vector<std::vector<int64_t>>& counts) {
+    const int W = (int)counts.size();
+    std::vector<Xfer> plan;
+    for (int s = 0; s < W; ++s)
+        for (int d = 0; d < W; ++d) {
+            int64_t so = 0, ro = 0;
+            for (int j = 0; j < d; ++j) so += counts[(size_t)s][(size_t)j];
+            for (int j = 0; j < s; ++j) ro += counts[(size_t)j][(size_t)d];
+            if (counts[(size_t)s][(size_t)d] > 0) plan.push_back({s, d, so, ro, counts[(size_t)s][(size_t)d]});
+        }
+    return plan;
+}
+
 gs_status exchange(gs_group* g, std::vector<int64_t>* nrec) {
     const int W = g->world;
     const int64_t xb = gs_exchange_record_bytes();
+    std::vector<std::vector<int64_t>> counts((size_t)W);
     nrec->assign((size_t)W, 0);
-    for (int d = 0; d < W; ++d)
-        for (int s = 0; s < W; ++s) (*nrec)[(size_t)d] += g->r[(size_t)s].counts[(size_t)d];
+    for (int s = 0; s < W; ++s) {
+        counts[(size_t)s] = g->r[(size_t)s].counts;
+        for (int d = 0; d < W; ++d) (*nrec)[(size_t)d] += counts[(size_t)s][(size_t)d];
+    }
     for (int d = 0; d < W; ++d) GG_HIP(g->r[(size_t)d].recv.reserve(g->r[(size_t)d].dev, (size_t)std::max<int64_t>((*nrec)[(size_t)d], 1) * xb));
-    auto soff = [&](int s, int d) {  // offset (records) of s's group for d in its send buffer
-        int64_t o = 0;
-        for (int j = 0; j < d; ++j) o += g->r[(size_t)s].counts[(size_t)j];
-        return o;
-    };
-    auto roff = [&](int d, int s) {  // offset of s's records in d's receive buffer
-        int64_t o = 0;
-        for (int j = 0; j < s; ++j) o += g->r[(size_t)j].counts[(size_t)d];
-        return o;
-    };
+    const std::vector<Xfer> plan = exchange_plan(counts);
     if (g->transport == GS_TRANSPORT_RCCL) {
         GG_NCCL(g_rccl.group_start());
-        for (int s = 0; s < W; ++s) {
-            Rank& k = g->r[(size_t)s];
-            for (int d = 0; d < W; ++d) {
-                const int64_t cs = k.counts[(size_t)d], cr = g->r[(size_t)d].counts[(size_t)s];
-                if (cs > 0)
-                    GG_NCCL(g_rccl.send(k.send.as<char>() + soff(s, d) * xb, (size_t)(cs * xb), ncclUint8, d,
-                                        g->comms[(size_t)s], k.st));
-                if (cr > 0)
-                    GG_NCCL(g_rccl.recv(k.recv.as<char>() + roff(s, d) * xb, (size_t)(cr * xb), ncclUint8, d,
-                                        g->comms[(size_t)s], k.st));
-            }
+        for (const Xfer& x : plan) {  // each transfer: a send on src's communicator, the matching recv on dst's
+            Rank &ks = g->r[(size_t)x.src], &kd = g->r[(size_t)x.dst];
+            GG_NCCL(g_rccl.send(ks.send.as<char>() + x.soff * xb, (size_t)(x.n * xb), ncclUint8, x.dst,
+                                g->comms[(size_t)x.src], ks.st));
+            GG_NCCL(g_rccl.recv(kd.recv.as<char>() + x.roff * xb, (size_t)(x.n * xb), ncclUint8, x.src,
+                                g->comms[(size_t)x.dst], kd.st));
         }
         GG_NCCL(g_rccl.group_end());
         return GS_OK;
     }
-    for (int d = 0; d < W; ++d) {
-        Rank& k = g->r[(size_t)d];
-        GG_HIP(hipSetDevice(k.dev));
-        for (int s = 0; s < W; ++s) {
-            const int64_t c = g->r[(size_t)s].counts[(size_t)d];
-            if (c <= 0) continue;
-            GG_HIP(hipStreamWaitEvent(k.st, g->r[(size_t)s].ev_ready, 0));
-            GG_HIP(hipMemcpyPeerAsync(k.recv.as<char>() + roff(d, s) * xb, k.dev,
-                                      g->r[(size_t)s].send.as<char>() + soff(s, d) * xb, g->r[(size_t)s].dev,
-                                      (size_t)(c * xb), k.st));
-        }
+    for (const Xfer& x : plan) {
+        Rank &ks = g->r[(size_t)x.src], &kd = g->r[(size_t)x.dst];
+        GG_HIP(hipSetDevice(kd.dev));
+        GG_HIP(hipStreamWaitEvent(kd.st, ks.ev_ready, 0));
+        GG_HIP(hipMemcpyPeerAsync(kd.recv.as<char>() + x.roff * xb, kd.dev, ks.send.as<char>() + x.soff * xb, ks.dev,
+                                  (size_t)(x.n * xb), kd.st));
     }
     return GS_OK;
 }
@@ -421,7 +487,8 @@ gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int 
         GG_NCCL(g_rccl.group_end());
         GG_HIP(hipSetDevice(g->r[0].dev));
         GG_HIP(hipMemcpyAsync(hsum.data(), g->r[0].hist.ptr, GS_SLAB_BINS * 8, hipMemcpyDeviceToHost, g->r[0].st));
-        GG_HIP(hipStreamSynchronize(g->r[0].st));
+        GG_HIP(hipEventRecord(g->r[0].ev_ready, g->r[0].st));
+        if ((s = wait_bounded(g, g->r[0].dev, g->r[0].ev_ready, "slab histogram all-reduce")) != GS_OK) return s;
     } else {
         for (int i = 0; i < W; ++i) {
             GG_HIP(hipSetDevice(g->r[(size_t)i].dev));
@@ -585,23 +652,54 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
     std::vector<int> sorted = dev;
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (transport == GS_TRANSPORT_AUTO) transport = (distinct && g->world > 1) ? GS_TRANSPORT_RCCL : GS_TRANSPORT_COPY;
-    if (transport != GS_TRANSPORT_RCCL && transport != GS_TRANSPORT_COPY)
+    if (transport != GS_TRANSPORT_AUTO && transport != GS_TRANSPORT_RCCL && transport != GS_TRANSPORT_COPY)
         return gfail(GS_ERR_INVALID_ARG, "bad transport");
     if (transport == GS_TRANSPORT_RCCL && !distinct)
         return gfail(GS_ERR_INVALID_ARG, "RCCL needs one device per rank (GS_TRANSPORT_COPY for shared devices)");
+    // RCCL is loaded before any rank state exists: AUTO falls back to peer
+    // copies when it cannot be loaded, an explicit RCCL request fails cleanly
+    if (transport == GS_TRANSPORT_AUTO) {
+        std::string why;
+        transport = (distinct && g->world > 1 && g_rccl.load(&why)) ? GS_TRANSPORT_RCCL : GS_TRANSPORT_COPY;
+    } else if (transport == GS_TRANSPORT_RCCL) {
+        std::string why;
+        if (!g_rccl.load(&why)) return gfail(GS_ERR_COMM, why);
+    }
+    // Per-rank state; on failure the streams and events made here are
+    // released again, so a retry starts clean (gs_initialize is idempotent
+    // per handle and device).
+    auto rollback = [&](gs_status st) {
+        const std::string msg = gs_last_error();
+        for (auto& k : g->r) {
+            if (k.dev >= 0) (void)hipSetDevice(k.dev);
+            if (k.own_stream && k.st) (void)hipStreamDestroy(k.st);
+            if (k.ev_ready) (void)hipEventDestroy(k.ev_ready);
+            if (k.ev_done) (void)hipEventDestroy(k.ev_done);
+            k.st = nullptr;
+            k.own_stream = false;
+            k.ev_ready = k.ev_done = nullptr;
+        }
+        for (ncclComm_t c : g->comms)
+            if (c) (void)g_rccl.comm_destroy(c);
+        g->comms.clear();
+        return gfail(st, msg);
+    };
     for (int i = 0; i < g->world; ++i) {
         Rank& k = g->r[(size_t)i];
         k.dev = dev[(size_t)i];
         gs_status s = gs_initialize(k.h, k.dev);
-        if (s != GS_OK) return s;
-        GG_HIP(hipSetDevice(k.dev));
-        if (i > 0) {
-            GG_HIP(hipStreamCreateWithFlags(&k.st, hipStreamNonBlocking));
-            k.own_stream = true;
+        hipError_t e = s == GS_OK ? hipSetDevice(k.dev) : hipSuccess;
+        if (s == GS_OK && e == hipSuccess && i > 0) {
+            e = hipStreamCreateWithFlags(&k.st, hipStreamNonBlocking);
+            k.own_stream = e == hipSuccess;
         }
-        GG_HIP(hipEventCreateWithFlags(&k.ev_ready, hipEventDisableTiming));
-        GG_HIP(hipEventCreateWithFlags(&k.ev_done, hipEventDisableTiming));
+        if (s == GS_OK && e == hipSuccess) e = hipEventCreateWithFlags(&k.ev_ready, hipEventDisableTiming);
+        if (s == GS_OK && e == hipSuccess) e = hipEventCreateWithFlags(&k.ev_done, hipEventDisableTiming);
+        if (s == GS_OK && e != hipSuccess) {
+            gs_set_last_error(std::string("gs_group_initialize: ") + hipGetErrorString(e));
+            s = e == hipErrorOutOfMemory ? GS_ERR_OOM : GS_ERR_DEVICE;
+        }
+        if (s != GS_OK) return rollback(s);
     }
     if (transport == GS_TRANSPORT_COPY && distinct) {  // direct peer access over xGMI where the devices allow it
         for (int a = 0; a < g->world; ++a)
@@ -615,16 +713,27 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
             }
     }
     if (transport == GS_TRANSPORT_RCCL) {
-        std::string why;
-        if (!g_rccl.load(&why)) return gfail(GS_ERR_COMM, why);
         g->comms.assign((size_t)g->world, nullptr);
-        GG_NCCL(g_rccl.comm_init_all(g->comms.data(), g->world, dev.data()));
+        const ncclResult_t r = g_rccl.comm_init_all(g->comms.data(), g->world, dev.data());
+        if (r != ncclSuccess) {
+            gs_set_last_error(std::string("ncclCommInitAll: ") + g_rccl.error_string(r));
+            return rollback(GS_ERR_COMM);
+        }
     }
-    GG_HIP(hipSetDevice(dev[0]));
-    GG_HIP(hipEventCreateWithFlags(&g->frame_done, hipEventDisableTiming));
+    if (hipSetDevice(dev[0]) != hipSuccess || hipEventCreateWithFlags(&g->frame_done, hipEventDisableTiming) != hipSuccess) {
+        gs_set_last_error("gs_group_initialize: frame event");
+        return rollback(GS_ERR_DEVICE);
+    }
+    if (const char* t = std::getenv("GS_COMM_TIMEOUT_MS")) g->timeout_ms = std::max<int64_t>(1, std::atoll(t));
     g->transport = transport;
     g->pool = new Pool(g->world);
     g->initialized = true;
+    return GS_OK;
+}
+
+gs_status gs_group_set_timeout(gs_group* g, int32_t timeout_ms) {
+    if (!g || timeout_ms <= 0) return gfail(GS_ERR_INVALID_ARG, "gs_group_set_timeout: bad arguments");
+    g->timeout_ms = timeout_ms;
     return GS_OK;
 }
 
@@ -645,6 +754,7 @@ int32_t gs_group_transport(const gs_group* g) { return g && g->initialized ? g->
 gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int32_t width, int32_t height,
                           float* out_rgba, int32_t out_is_device, void* hip_stream) {
     if (!g || !g->initialized) return gfail(GS_ERR_STATE, "gs_group_initialize not called");
+    if (g->failed) return gfail(GS_ERR_COMM, "group unusable after a collective failure");
     if (!view || !proj || !out_rgba || width <= 0 || height <= 0)
         return gfail(GS_ERR_INVALID_ARG, "gs_group_render: bad arguments");
     Rank& r0 = g->r[0];
@@ -657,8 +767,10 @@ gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int
         out = g->fb.as<float>();
     }
     // the last frame is done everywhere (its gather waited for every rank)
-    GG_HIP(hipEventSynchronize(g->frame_done));
-    gs_status s = g->world == 1 ? gs_render(r0.h, view, proj, width, height, out, 1, r0.st)
+    gs_status s = wait_bounded(g, r0.dev, g->frame_done, "previous frame");
+    if (s != GS_OK) return s;
+    GG_HIP(hipSetDevice(r0.dev));
+    s = g->world == 1 ? gs_render(r0.h, view, proj, width, height, out, 1, r0.st)
                  : g->scheme == GS_SCHEME_SLABS ? render_slabs(g, view, proj, width, height, out)
                  : g->scheme == GS_SCHEME_BANDS ? render_bands(g, view, proj, width, height, out)
                                                 : render_rows(g, view, proj, width, height, out);
@@ -667,9 +779,12 @@ gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int
     GG_HIP(hipEventRecord(g->frame_done, r0.st));
     if (!out_is_device) {
         GG_HIP(hipMemcpyAsync(out_rgba, out, bytes, hipMemcpyDeviceToHost, r0.st));
-        GG_HIP(hipStreamSynchronize(r0.st));
+        GG_HIP(hipEventRecord(g->frame_done, r0.st));
+        return wait_bounded(g, r0.dev, g->frame_done, "frame");
     }
-    return gs_last_stats(r0.h, &g->stats);
+    // device output: asynchronous on the caller's stream (stats are read
+    // lazily by gs_group_last_stats)
+    return GS_OK;
 }
 
 gs_status gs_group_last_stats(gs_group* g, int32_t rank, gs_stats* out) {

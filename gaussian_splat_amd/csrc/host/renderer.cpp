@@ -862,6 +862,8 @@ gs_status gs_get_scene(const gs_handle* h, float* pos, float* rot, float* scale,
 
 gs_status gs_initialize(gs_handle* h, int32_t device) {
     if (!h) return fail(GS_ERR_INVALID_ARG, "null handle");
+    if (h->initialized)  // idempotent: a retried group initialize reuses the upload, streams and events
+        return h->device == device ? GS_OK : fail(GS_ERR_STATE, "handle already initialized on another device");
     int count = 0;
     GS_HIP(hipGetDeviceCount(&count));
     if (device < 0 || device >= count) return fail(GS_ERR_DEVICE, "no such HIP device");

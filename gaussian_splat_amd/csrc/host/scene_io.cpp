@@ -252,6 +252,10 @@ gs_status planes_from_ply(const char* path, float crop_radius, bool crop, int sh
 
 void planes_subset(const HostPlanes& src, int64_t b, int64_t e, HostPlanes* out) {
     const int64_t m = std::max<int64_t>(e - b, 0);
+    if (b == 0 && m == src.n) {  // read-only planes: share them
+        *out = src;
+        return;
+    }
     out->alloc(m, src.sh_degree);
     if (!m) return;
     std::memcpy(out->p0.data(), src.p0.data() + 4 * b, (size_t)m * 16);

@@ -20,8 +20,11 @@
 
 namespace gsio {
 
+// Planes are written once by their builder and read-only afterwards, so
+// handles may share them: a full-range gs_create_subset (every rank of a
+// replicated group) keeps one host copy of the scene, not one per rank.
 struct FloatBuf {
-    std::unique_ptr<float[]> p;
+    std::shared_ptr<float[]> p;
     size_t n = 0;
     void alloc(size_t count) {
         p.reset(count ? new float[count] : nullptr);  // uninitialised
@@ -56,7 +59,7 @@ gs_status planes_from_points(const PointData* pts, int64_t n, const float* raw_d
 // headers.
 gs_status planes_from_ply(const char* path, float crop_radius, bool crop, int sh_degree, HostPlanes* out,
                           bool* handled);
-// Splats [b, e) of src.
+// Splats [b, e) of src (the whole range shares src's buffers).
 void planes_subset(const HostPlanes& src, int64_t b, int64_t e, HostPlanes* out);
 
 }  // namespace gsio

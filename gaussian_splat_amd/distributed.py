@@ -50,6 +50,30 @@ from ._lib import check, lib
 
 ROW = 32  # ownership unit: one 32-pixel bin row
 
+# Bound of every rendezvous and collective of a rank (SURVEY §5 failure
+# detection): a peer that never joins or stops answering makes the others
+# raise within this time instead of hanging (the reference, one Metal
+# device, has no such path: instanced_splat_renderer.mm:319-336).
+DEFAULT_TIMEOUT_S = 120.0
+
+
+def init_ranks(backend: str = "nccl", timeout_s: float = DEFAULT_TIMEOUT_S, device=None, **kw):
+    """torch.distributed.init_process_group with a bounded timeout: the
+    rendezvous and every later collective of the group (gloo: each
+    send/recv; nccl = RCCL: the watchdog with async error handling, which
+    aborts the communicator) fail after timeout_s.  `kw`: init_method, rank,
+    world_size (default: the torchrun environment)."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    td = datetime.timedelta(seconds=float(timeout_s))
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, timeout=td, **kw)
+
 
 def row_owner(height: int, world: int) -> np.ndarray:
     """Default owner table (the C-ABI's, gs_shard_set_rows): rank r owns the

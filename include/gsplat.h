@@ -282,6 +282,13 @@ gs_status gs_create_replicated_from_handle(const gs_handle *scene, int32_t num_g
  * GS_TRANSPORT_COPY); transport: gs_transport. */
 gs_status gs_group_initialize(gs_group *g, const int32_t *devices, int32_t transport);
 gs_status gs_group_set_scheme(gs_group *g, int32_t scheme);
+/* Bound of every host wait of the group (default 60 s, or GS_COMM_TIMEOUT_MS).
+ * A wait that expires, or an RCCL communicator reporting an asynchronous
+ * error (ncclCommGetAsyncError, polled during the waits), aborts every
+ * communicator and fails the call with GS_ERR_COMM; the group is then
+ * unusable.  (No reference counterpart: instanced_splat_renderer.mm:319-336
+ * is the reference's only failure path.) */
+gs_status gs_group_set_timeout(gs_group *g, int32_t timeout_ms);
 /* The frame (fp32 RGBA, W*H*16 B) on devices[0]: out_is_device = 1 async on
  * hip_stream (a stream of devices[0]); 0 = host memory, the call syncs. */
 gs_status gs_group_render(gs_group *g, const float view[16], const float proj[16], int32_t width, int32_t height,

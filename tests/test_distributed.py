@@ -140,3 +140,78 @@ def test_assemble_layout():
             b[k * 32: k * 32 + rows.shape[0]] = rows
         bands.append(b)
     torch.testing.assert_close(assemble(bands, w, h, world, custom), frame, rtol=0, atol=0)
+
+
+# ---- failure detection: bounded rendezvous and collectives ----
+
+def _lonely_rank(port, q):
+    """Rank 0 of a world of 2 whose peer never starts."""
+    import sys
+    import time
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from gaussian_splat_amd.distributed import init_ranks
+    t0 = time.time()
+    try:
+        init_ranks("gloo", 3.0, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=2)
+        q.put(("joined", time.time() - t0))
+    except Exception as e:  # the rendezvous must give up
+        q.put((type(e).__name__, time.time() - t0))
+
+
+def test_gloo_peer_never_joins_fails_within_timeout():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_lonely_rank, args=(_free_port(), q))
+    p.start()
+    try:
+        what, dt = q.get(timeout=90)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert what != "joined" and dt < 30, (what, dt)
+
+
+def _stuck_exchange_rank(rank, port, q):
+    """Both ranks join; rank 1 then stops answering, rank 0 enters the
+    row scheme's record exchange, which must fail within the timeout."""
+    import sys
+    import time
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import torch
+    import torch.distributed as dist
+    from gaussian_splat_amd.distributed import exchange, init_ranks
+    init_ranks("gloo", 3.0, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    if rank == 1:
+        time.sleep(8)  # a stuck peer: never enters the all_to_all
+        q.put(("peer", 0.0))
+        return
+    t0 = time.time()
+    try:
+        exchange(torch.zeros(96, dtype=torch.uint8), [1, 1], 48, 2)
+        q.put(("completed", time.time() - t0))
+    except Exception as e:
+        q.put((type(e).__name__, time.time() - t0))
+    dist.destroy_process_group()
+
+
+def test_gloo_stuck_peer_exchange_fails_within_timeout():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stuck_exchange_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=120) for _ in range(2)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    r0 = next(r for r in res if r[0] != "peer")
+    assert r0[0] != "completed" and r0[1] < 15, r0

@@ -93,17 +93,53 @@ def test_group_rccl_two_gpus(built):
     sc = _scene(60000, 81, 0, W / H)
     r = InstancedSplatRenderer(sc, Options(crop=False))
     r.initialize(0)
-    for scheme in ("rows", "slabs"):
-        g = _group(r, 2, devices=[0, 1], transport="auto", scheme=scheme)
+    from gaussian_splat_amd import ShardedGroup
+    for scheme in ("rows", "slabs", "bands"):
+        if scheme == "bands":
+            g = ShardedGroup(r, 2, replicated=True)
+            g.initialize([0, 1], "auto")
+        else:
+            g = _group(r, 2, devices=[0, 1], transport="auto", scheme=scheme)
         assert g.transport == "rccl"
         V, P = orbit_views(W, H, 1)[0]
         ref = r.render_host(V, P, W, H)
         got = g.render_host(V, P, W, H)
-        if scheme == "rows":
+        if scheme in ("rows", "bands"):
             np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
         else:
             check_slab_frame(got, ref)
         g.close()
+
+
+def test_group_bounded_wait(built):
+    """Every host wait of a group is bounded (gs_group_set_timeout): a wait
+    that cannot finish in time fails the frame with GS_ERR_COMM and leaves
+    the group unusable, instead of hanging.  Here a 4K host-output frame of
+    a 6M-splat scene (tens of ms) under a 1 ms bound."""
+    from gaussian_splat_amd import GsError, InstancedSplatRenderer, Options, ShardedGroup
+    W, H = 3840, 2160
+    sc = _scene(2_000_000, 91, 0, W / H)
+    r = InstancedSplatRenderer(sc, Options(crop=False))
+    r.initialize(0)
+    g = _group(r, 2)
+    V, P = orbit_views(W, H, 1)[0]
+    ref = r.render_host(V, P, W, H)
+    np.testing.assert_array_equal(g.render_host(V, P, W, H).view(np.uint32), ref.view(np.uint32))
+    with pytest.raises(GsError):
+        g.set_timeout(0)
+    g.set_timeout(1)
+    # host output into pinned memory: the 133-MB device-to-host copy alone
+    # (asynchronous into pinned memory) outlasts a 1 ms bound
+    import ctypes as C
+    import torch
+    from gaussian_splat_amd._lib import lib
+    from gaussian_splat_amd.api import _mat16
+    pinned = torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True)
+    rc = lib().gs_group_render(g._g, _mat16(V), _mat16(P), W, H, C.c_void_p(pinned.data_ptr()), 0, None)
+    assert rc == 6, rc  # GS_ERR_COMM: the wait expired
+    with pytest.raises(GsError, match="unusable"):
+        g.render_host(V, P, W, H)
+    torch.cuda.synchronize()  # the abandoned frame's work drains before the buffers go
 
 
 def test_group_rejects_rccl_on_shared_device(built):

@@ -19,7 +19,7 @@ KP = json.loads((Path(__file__).resolve().parent / "golden" / "known_answers.jso
 
 def _renderer(scene, **kw):
     from gaussian_splat_amd import InstancedSplatRenderer, Options
-    r = InstancedSplatRenderer(scene, Options(**kw))
+    r = InstancedSplatRenderer(scene, Options(crop=False, **kw))  # the fixtures are raw scenes (no crop), as the oracle renders them
     r.initialize(0)
     return r
 
