@@ -362,7 +362,9 @@ def main():
                        if world > 1 else
                        ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the composite of frame k)"
                         if args.frames_in_flight == 2 else "single GPU"),
-                       "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning},
+                       "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning,
+                       "two_slab": bool(s0.get("two_slab", 0)), "pairs_sorted": int(s0.get("pairs_sorted", s0["pairs"])),
+                       "open_tiles": int(s0.get("open_tiles", 0))},
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
             "timed_kernel_ms": {k: round(v, 4) for k, v in timed_k.items()},
             "standalone_kernel_ms": {k: round(v, 4) for k, v in standalone.items()},

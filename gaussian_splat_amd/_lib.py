@@ -18,8 +18,8 @@ class GsOptions(C.Structure):
     _fields_ = [("mode", C.c_int32), ("sh_degree", C.c_int32), ("crop", C.c_int32),
                 ("crop_radius", C.c_float), ("stage_timing", C.c_int32), ("cap", C.c_int32),
                 ("frames_in_flight", C.c_int32),
-                ("binning", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("binning", C.c_int32), ("depth_split", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 class GsSceneSoa(C.Structure):
@@ -36,7 +36,9 @@ class GsStats(C.Structure):
                 ("bytes_preprocess", C.c_int64), ("bytes_scan", C.c_int64), ("bytes_duplicate", C.c_int64),
                 ("bytes_sort", C.c_int64), ("bytes_ranges", C.c_int64), ("bytes_composite", C.c_int64),
                 ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
-                ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64)]
+                ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64),
+                ("pairs_sorted", C.c_int64), ("open_tiles", C.c_int64), ("two_slab", C.c_int32),
+                ("depth_cut", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -60,6 +62,7 @@ SIGNATURES = {
     "gs_destroy": (None, [_P]),
     "gs_set_mode": (C.c_int, [_P, C.c_int32]),
     "gs_set_cap": (C.c_int, [_P, C.c_int32]),
+    "gs_set_depth_split": (C.c_int, [_P, C.c_int32]),
     "gs_set_stage_timing": (C.c_int, [_P, C.c_int32]),
     "gs_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
     "gs_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),

@@ -54,6 +54,9 @@ class Options:
     # bin-list build order: "default" (per frame from the previous frame's pair count at this
     # resolution; depth-first on the first frame), "depth_first", "bin_first"
     binning: str = "default"
+    # bin-first frames in two depth slabs, the second only where the first left pixels open
+    # (True) or in one (False, the default: measured faster); the same image
+    depth_split: bool = False
 
     def to_c(self) -> GsOptions:
         o = GsOptions()
@@ -74,6 +77,7 @@ class Options:
         if self.binning not in BINNING:
             raise ValueError(f"binning must be one of {list(BINNING)}")
         o.binning = BINNING[self.binning]
+        o.depth_split = 1 if self.depth_split else 0
         return o
 
 
@@ -251,6 +255,11 @@ class InstancedSplatRenderer:
         """Per-pixel fragment cap by arrival order (0 = none)."""
         check(lib().gs_set_cap(self._h, int(cap)), "gs_set_cap")
         self.options.cap = int(cap)
+
+    def set_depth_split(self, on: bool):
+        """Two depth slabs for bin-first frames (gs_set_depth_split): same image, less sorting."""
+        check(lib().gs_set_depth_split(self._h, 1 if on else 0), "gs_set_depth_split")
+        self.options.depth_split = bool(on)
 
     def render(self, view, proj, width: int, height: int, out=None, stream=None):
         """Render into `out` (torch float32 CUDA tensor (H, W, 4)); returns it."""

@@ -92,11 +92,14 @@ struct gs_handle {
     uint32_t* host_xtotal = nullptr;                                    // pinned, kMaxWorld
     uint64_t* host_total = nullptr;  // pinned, mapped: the scan writes P here directly
     uint64_t* dev_total = nullptr;   // its device-side address
-    hipEvent_t ev[9] = {};   // stage boundaries 0..7; 8 = exchange done (shard frames)
+    hipEvent_t ev[14] = {};  // stage boundaries 0..7; 8 = exchange done (shard frames); 9..13 second slab
     // stage_timing 2: packet events (preprocess start/stop, composite start/stop)
     // in a ring of per-frame slots, read without stalling the frames
     static constexpr int kKevRing = 64;
-    hipEvent_t kev[kKevRing][4] = {};
+    // [0, 1] preprocess start/stop, [2, 3] composite start/stop; two-slab
+    // frames: [4] first composite stop, [5] second composite start
+    hipEvent_t kev[kKevRing][6] = {};
+    bool kev_two[kKevRing] = {};
     int64_t kev_frames = 0;    // frames recorded since stage timing was (re)set
     int kev_slot = 0;          // slot of the frame being enqueued
     bool kev_pending = false;  // last frame's kernel times not yet copied into stats
@@ -137,9 +140,23 @@ struct gs_handle {
     int set = 0;
     bool last_pipe = false;  // the last frame ran pipelined (a switch into pipelining waits for the caller's stream)
     DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr;
+    // Two-slab frames (gs_options.depth_split): the depth
+    // histogram of the cut (filled by the preprocess, cleared by the first
+    // slab's scan), the cut per buffer set, the composite's open-tile flags,
+    // and the second slab's own scan / sort scratch: its lists are built on
+    // the composite stream while the side stream builds the next frame's.
+    // The rects are double-buffered with the sets for the same reason.
+    DevBuf ghist, kcut, open4, partials2, npairs2, scratch2, tot2, alt_rlo, alt_rhi;
+    bool two_slab_frame = false;
+    uint64_t p1_pairs = 0;   // first-slab pairs of the frame in `stats`
+    uint32_t pair_cap = 0;   // pair capacity of the set of the last build_bin_lists
     void swap_sets() {
         std::swap(rec, alt_rec);
         std::swap(dkey, alt_dkey);
+        if (alt_rlo.ptr) {
+            std::swap(rlo, alt_rlo);
+            std::swap(rhi, alt_rhi);
+        }
         std::swap(keys, alt_keys);
         std::swap(vals, alt_vals);
         std::swap(tkeys, alt_tkeys);
@@ -154,7 +171,8 @@ struct gs_handle {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
-                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch})
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch,
+                          &ghist, &kcut, &open4, &partials2, &npairs2, &scratch2, &tot2, &alt_rlo, &alt_rhi})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -193,6 +211,7 @@ gs_status check_options(const gs_options& opt) {
     if (opt.frames_in_flight < 0 || opt.frames_in_flight > 2)
         return fail(GS_ERR_INVALID_ARG, "frames_in_flight must be 1 or 2");
     if (opt.binning < 0 || opt.binning > 2) return fail(GS_ERR_INVALID_ARG, "binning must be 0, 1 or 2");
+    if (opt.depth_split < 0 || opt.depth_split > 1) return fail(GS_ERR_INVALID_ARG, "depth_split must be 0 or 1");
     return GS_OK;
 }
 
@@ -246,6 +265,12 @@ gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
     u.band_y1 = H - 1;
     return u;
 }
+
+// Two-slab frames: the first slab's share of the frame's
+// pairs.  The composite reads ~1/4 of each bin list before its tiles
+// saturate (6M @ 1080p); 30 % leaves ~20 % of the bins open, whose second
+// slab is then ~13 % of the pairs (measured on the oracle's lists).
+constexpr float kDepthSplitFrac = 0.3f;
 
 int bits_for(uint32_t v) {  // bits needed to represent values < v
     int b = 0;
@@ -302,9 +327,23 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->dkey.reserve(n * 4));
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
-    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
+    // (3 words per scan block: the two-slab first pass also sums both slabs' pairs)
+    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 24));
+    static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
+    if (ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1) {  // two-slab frames
+        if (!h->ghist.ptr) {
+            GS_HIP(h->ghist.reserve((size_t)gs::kCutCopies * gs::kCutBuckets * 4));
+            GS_HIP(hipMemset(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4));
+        }
+        GS_HIP(h->kcut.reserve(8));
+        GS_HIP(h->tot2.reserve(2 * 64));
+        GS_HIP(h->npairs2.reserve(4));
+        GS_HIP(h->partials2.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
+        GS_HIP(h->alt_rlo.reserve(n * 4));
+        GS_HIP(h->alt_rhi.reserve(n * 4));
+    }
     if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
-        GS_HIP(hipHostMalloc((void**)&h->host_total, 32, hipHostMallocMapped | hipHostMallocCoherent));
+        GS_HIP(hipHostMalloc((void**)&h->host_total, 64, hipHostMallocMapped | hipHostMallocCoherent));
         GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
     }
     if (!h->seg_sample.ptr) {
@@ -312,7 +351,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 16));
     }
     GS_HIP(h->npairs.reserve(4));
-    GS_HIP(h->fetch.reserve(16));
+    GS_HIP(h->fetch.reserve(32));  // per buffer set: [set] records fetched, [2 + set] open tiles (two-slab)
     if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
@@ -361,7 +400,14 @@ void begin_frame(gs_handle* h, hipStream_t st) {
 gs_status slot_times(gs_handle* h, int k, float* pre, float* comp, float* total) {
     GS_HIP(hipEventSynchronize(h->kev[k][3]));
     GS_HIP(hipEventElapsedTime(pre, h->kev[k][0], h->kev[k][1]));
-    GS_HIP(hipEventElapsedTime(comp, h->kev[k][2], h->kev[k][3]));
+    if (h->kev_two[k]) {  // two-slab frame: both composite launches, not the second slab's lists between them
+        float a = 0.0f, b = 0.0f;
+        GS_HIP(hipEventElapsedTime(&a, h->kev[k][2], h->kev[k][4]));
+        GS_HIP(hipEventElapsedTime(&b, h->kev[k][5], h->kev[k][3]));
+        *comp = a + b;
+    } else {
+        GS_HIP(hipEventElapsedTime(comp, h->kev[k][2], h->kev[k][3]));
+    }
     if (total) GS_HIP(hipEventElapsedTime(total, h->kev[k][0], h->kev[k][3]));
     return GS_OK;
 }
@@ -419,10 +465,14 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
 // read the pair count on the device and are sized by the pair buffers'
 // capacity (grown to the last frame's P); a frame whose P exceeds it runs
 // them as no-ops, and they are queued again once the buffers have grown.
+// sel (two-slab frames): the first slab's filter; *pairs is then that slab's
+// pair count, h->stats.pairs both slabs', and the buffers hold both.
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
-                          const uint32_t* carry_dkey = nullptr) {
+                          const uint32_t* carry_dkey = nullptr, const gs::SlabSel* sel = nullptr) {
+    const gs::SlabSel no_sel;
+    const gs::SlabSel& fs = sel ? *sel : no_sel;
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     // at least one key bit: the bin ranges are written by the last sort pass,
     // so a single-bin frame (W, H <= 32) still needs one pass
@@ -465,7 +515,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                         h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
                                         h->npairs.as<uint32_t>(), cap, pc.C, pc.C ? (pc.mask + 1) * pc.ntiles : 0u,
-                                        st, h->totals_ev));
+                                        st, h->totals_ev, fs));
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
     // bin id), then a stable sort by bin id only; the last pass also writes
@@ -475,7 +525,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc);
+                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc, fs);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
@@ -486,16 +536,19 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(enqueue_lists());
     GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
     const uint64_t P = h->host_total[0];
+    // two-slab: the pairs of both slabs (the buffers must hold the second's too)
+    const uint64_t P_all = sel ? h->host_total[4] : P;
     h->stats.visible = (int64_t)h->host_total[1];
+    h->stats.pairs = (int64_t)P_all;
     // the last per-bin depth sort's share of pairs in lists too long for LDS
     if ((h->host_total[3] & gs::kSegSampleValid) && h->order.sample_pairs)
         h->order.long_share = (double)h->host_total[2] / (double)h->order.sample_pairs;
-    h->order.frame_pairs = P;
-    if (P >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
-    if (P > cap) {
+    h->order.frame_pairs = P_all;
+    if (P_all >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
+    if (P_all > cap) {
         // the queued lists were no-ops (ranges still empty): grow, queue again
         GS_HIP(hipStreamSynchronize(st));
-        if (!(cap = reserve_pairs(P))) return fail(GS_ERR_OOM, "pair buffers");
+        if (!(cap = reserve_pairs(P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
         pc = pass_counts(P);
@@ -513,8 +566,55 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     if (timed && !carry_dkey) mark(h, 6, st);  // (ranges come out of the last sort pass)
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
+    h->pair_cap = cap;
     *vals_out = sv;
     *pairs = P;
+    return GS_OK;
+}
+
+// Two-slab frames, after the first slab's composite on sc:
+// the second slab's pairs (depth keys >= the cut) only into the bins that
+// composite left open, sorted, and composited from the saved state.  Sized
+// by the set's pair capacity (>= both slabs' pairs) and the device-side
+// count, so nothing here waits for the host.
+gs_status second_slab(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo, const uint32_t* rect_hi,
+                      const gs::FrameUniforms& U, const Ownership& own, gs::CompositeArgs ca, hipStream_t sc) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    const uint32_t cap = h->pair_cap;
+    const int bits = h->last_key_bits;
+    GS_HIP(h->partials2.reserve(((size_t)std::max<uint32_t>(m, 1) + gs::kScanItems - 1) / gs::kScanItems * 16 + 16));
+    GS_HIP(h->scratch2.reserve(gs::radix_sort_scratch_words(cap) * 4));
+    gs::SlabSel sel;
+    sel.mode = 2;
+    sel.dkey = dkey;
+    sel.kcut = h->kcut.as<uint32_t>() + h->set;
+    sel.open = h->open4.as<const uint32_t>();
+    sel.tiles_x = (uint32_t)U.tiles_x;
+    const bool masked = U.cell_mask != 0;
+    GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, masked, h->partials2.as<uint64_t>(),
+                                        h->tot2.as<uint64_t>() + 8 * h->set, nullptr, h->ranges.as<uint2>(), T,
+                                        h->npairs2.as<uint32_t>(), cap, nullptr, 0, sc, nullptr, sel));
+    mark(h, 10, sc);
+    GS_HIP(gs::launch_scan_duplicate(nullptr, rect_lo, rect_hi, h->partials2.as<uint64_t>(), m, (uint32_t)U.tiles_x,
+                                     own.dev, masked, dkey, bits, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
+                                     h->npairs2.as<uint32_t>(), sc, nullptr, gs::PassCounts{}, sel));
+    mark(h, 11, sc);
+    bool in_tmp = false;
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
+                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap, bits,
+                                 h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(),
+                                 h->npairs2.as<uint32_t>(), false));
+    mark(h, 12, sc);
+    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+    uint32_t* tk = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
+    uint32_t* tv = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+    GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), T, sk, sv, tk, tv, bits, nullptr, sc));
+    mark(h, 13, sc);
+    ca.vals = sv;
+    ca.ranges = h->ranges.as<uint2>();
+    ca.pass = 2;
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 5), kernel_event(h, 3)));
     return GS_OK;
 }
 
@@ -525,7 +625,9 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
                              int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr,
-                             const hipStream_t* composite_stream = nullptr) {
+                             const hipStream_t* composite_stream = nullptr, bool cut_hist = false) {
+    // cut_hist: the preprocess of these items filled the two-slab depth
+    // histogram (local frames with depth_split 0)
     // the composite runs on *composite_stream when given (frames_in_flight 2:
     // the caller's stream, while st is the handle's side stream) once the
     // lists are ready on st.  A pointer, since the caller's stream may be the
@@ -563,10 +665,13 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* vals = nullptr;
     uint64_t P = 0;
     const bool mlab = h->opt.mode == GS_MODE_MLAB;
+    h->two_slab_frame = false;
     if (mlab && (ca.cap > 0 || slab_t))
         return fail(GS_ERR_UNSUPPORTED, "MLAB mode has no fragment cap and no depth slabs");
     if (mlab) {
         // MLAB k-buffer: arrival (index) order per pixel, no depth sort
+        h->kev_two[h->kev_slot] = false;
+        if (cut_hist) GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
         mark(h, 2, st);
         gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P);
         if (s != GS_OK) return s;
@@ -585,10 +690,35 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         // sorted by depth key -> (depth, index) order, the same lists as the
         // depth-first order below.
         h->bin_first_frame = true;
+        // Two depth slabs: first the pairs of the splats below
+        // a depth-key cut, composited with each tile's state kept where a
+        // pixel stays open; then the rest, only for the bins left open.  The
+        // per-pixel operation sequence is the one-slab sequence (same image).
+        static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
+        const bool split_on = ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1;
+        const bool two = split_on && cut_hist && ca.cap == 0 && !slab_t && !out_bgra8 && out &&
+                         (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) && h->ghist.ptr;
+        gs::SlabSel sel1;
+        if (two) {
+            GS_HIP(h->open4.reserve((size_t)U.tiles_x * U.tiles_y * 4));
+            sel1.mode = 1;
+            sel1.dkey = dkey;
+            sel1.kcut = h->kcut.as<uint32_t>() + h->set;
+            sel1.hist = h->ghist.as<uint32_t>();
+            static const char* fr_env = std::getenv("GS_DEPTH_SPLIT_FRAC");
+            sel1.frac = fr_env ? (float)std::atof(fr_env) : kDepthSplitFrac;
+            sel1.zero64 = h->fetch.as<unsigned long long>() + 2 + h->set;
+        }
+        h->two_slab_frame = two;
+        h->kev_two[h->kev_slot] = two;
+        if (cut_hist && !two)  // filled but unused: cleared for the next frame's cut
+            GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
         mark(h, 2, st);
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey,
+                                      two ? &sel1 : nullptr);
         if (s != GS_OK) return s;
         h->order.sample_pairs = P;
+        h->p1_pairs = P;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
         // (the per-bin sort stays on the side stream: on the composite stream,
@@ -612,16 +742,28 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         }
         GS_HIP(handoff(true));
         ca.fetched = fetch_counter(h);
-        GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
+        if (two) {
+            ca.pass = 1;
+            ca.open4 = h->open4.as<uint8_t>();
+            ca.open_tiles = h->fetch.as<unsigned long long>() + 2 + h->set;
+        }
+        GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, two ? 4 : 3)));
         if (slab_t) {
             h->slab_ca = ca;
             h->slab_lists = true;
         }
+        if (two) {
+            mark(h, 9, sc);
+            if ((s = second_slab(h, m, dkey, rect_lo, rect_hi, U, own, ca, sc)) != GS_OK) return s;
+        }
         mark(h, 7, sc);
-        h->stats.pairs = (int64_t)P;
+        if (!two) h->stats.pairs = (int64_t)P;  // (two slabs: both slabs' pairs, build_bin_lists)
         return GS_OK;
     }
     h->bin_first_frame = false;
+    h->kev_two[h->kev_slot] = false;
+    if (cut_hist)  // (depth-first frames take no cut: the histogram is cleared for the next frame's)
+        GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
@@ -702,6 +844,20 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     h->stats_set = h->set;
     s.bytes_composite = h->stats_fixed_bytes + 4 * Pi * (4 + 48);
     s.records_fetched = -1;
+    s.pairs_sorted = Pi;
+    s.two_slab = h->two_slab_frame ? 1 : 0;
+    if (h->two_slab_frame) {
+        // first slab: its pairs through duplicate, sort and per-bin sort; the
+        // scan also reads the depth keys.  The second slab's share (read
+        // lazily with the fetch counter, gs_last_stats) is added there.
+        const int64_t P1 = (int64_t)h->p1_pairs;
+        s.pairs_sorted = P1;
+        s.bytes_scan = N * 12 + T * 8;
+        s.bytes_duplicate = N * 12 + P1 * 8;
+        s.bytes_sort = P1 * 20 * (int64_t)s.sort_passes;
+        s.bytes_depth_sort = P1 * 12;
+        h->stats_fixed_bytes += 4 * T * 8;  // the second composite reads its ranges too
+    }
     // stage_timing 2: read lazily (gs_last_stats / gs_kernel_times), so a
     // frame never waits for itself
     if (h->opt.stage_timing == 2 && h->events) {
@@ -723,6 +879,13 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         }
         s.ms_composite = elapsed(h, 6, 7);
         s.ms_total = elapsed(h, 0, 7);
+        if (h->two_slab_frame) {  // the second slab's lists ran between the two composites
+            s.ms_composite = elapsed(h, 6, 9) + elapsed(h, 13, 7);
+            s.ms_scan += elapsed(h, 9, 10);
+            s.ms_duplicate += elapsed(h, 10, 11);
+            s.ms_sort += elapsed(h, 11, 12);
+            s.ms_depth_sort += elapsed(h, 12, 13);
+        }
     }
 }
 
@@ -933,6 +1096,13 @@ gs_status gs_set_frames_in_flight(gs_handle* h, int32_t n) {
     return GS_OK;
 }
 
+gs_status gs_set_depth_split(gs_handle* h, int32_t depth_split) {
+    if (!h || depth_split < 0 || depth_split > 1) return fail(GS_ERR_INVALID_ARG, "depth_split must be 0 or 1");
+    // (the next frame's ensure_frame_scratch allocates the two-slab buffers)
+    h->opt.depth_split = depth_split;
+    return GS_OK;
+}
+
 gs_status gs_set_cap(gs_handle* h, int32_t cap) {
     if (!h || cap < 0) return fail(GS_ERR_INVALID_ARG, "bad cap");
     h->opt.cap = cap;
@@ -997,14 +1167,19 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     }
     h->last_pipe = pipe;
     begin_frame(h, sp);
+    // (two-slab frames: the depth histogram of the cut rides on the preprocess)
+    static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
+    const bool split_on = ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1;
+    uint32_t* hist = split_on && !bgra8 && h->ghist.ptr ? h->ghist.as<uint32_t>() : nullptr;
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h)));
+                                 kernel_event(h, 1), fetch_counter(h), hist));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, compact,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
-                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st)) != GS_OK)
+                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st,
+                                hist != nullptr)) != GS_OK)
         return s;
     GS_HIP(hipEventRecord(h->set_free[h->set], st));  // this set's last reader
     const uint64_t P = (uint64_t)h->stats.pairs;
@@ -1045,6 +1220,26 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
         GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + h->stats_set, 8, hipMemcpyDeviceToHost));
         h->stats.records_fetched = (int64_t)v;
         h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
+        if (h->stats.two_slab) {
+            // the second slab: its pairs (the scan's total), the open tiles
+            // (each resumed from and written back as 16-B pixel states), the cut
+            unsigned long long open = 0;
+            uint64_t p2 = 0;
+            uint32_t K = 0;
+            GS_HIP(hipMemcpy(&open, h->fetch.as<unsigned long long>() + 2 + h->stats_set, 8, hipMemcpyDeviceToHost));
+            GS_HIP(hipMemcpy(&p2, h->tot2.as<uint64_t>() + 8 * h->stats_set, 8, hipMemcpyDeviceToHost));
+            GS_HIP(hipMemcpy(&K, h->kcut.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
+            gs_stats& s = h->stats;
+            const int64_t P2 = (int64_t)p2, N = s.splats, T = s.tiles;
+            s.open_tiles = (int64_t)open;
+            s.depth_cut = K;
+            s.pairs_sorted += P2;
+            s.bytes_scan += N * 12 + T * 8;
+            s.bytes_duplicate += N * 12 + P2 * 8;
+            s.bytes_sort += P2 * 20 * (int64_t)s.sort_passes;
+            s.bytes_depth_sort += P2 * 12;
+            s.bytes_composite += (int64_t)open * gs::kTileThreads * 32;
+        }
     }
     *out = h->stats;
     return GS_OK;
@@ -1106,6 +1301,8 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
 
 gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int64_t cap, int64_t* count) {
     if (!h || !count) return fail(GS_ERR_INVALID_ARG, "null argument");
+    if (h->two_slab_frame)
+        return fail(GS_ERR_UNSUPPORTED, "the last frame's lists were built in two depth slabs (depth_split = 1 keeps one)");
     int64_t P = h->stats.pairs;
     *count = P;
     if (!h->last_keys || P == 0) return GS_OK;

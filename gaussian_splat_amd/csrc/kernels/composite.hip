@@ -170,13 +170,18 @@ __device__ __forceinline__ const StagedRec& staged_at(const StagedRec* base, uin
     return *reinterpret_cast<const StagedRec*>(reinterpret_cast<const char*>(base) + off);
 }
 
-template <int MODE, bool CAP, int SLAB = 0>
+// PASS (two-slab frames; modes 0/1, no cap, fp32 output):
+// 1 = the first slab, leaving the state (C, T) of every tile with an open
+// pixel; 2 = the second slab, resuming those tiles only.
+template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
+    static_assert(PASS == 0 || ((MODE == 0 || MODE == 1) && !CAP && SLAB == 0), "two-slab passes: tile/live50 rules");
     __shared__ StagedRec srec[kTileThreads];
     __shared__ uint16_t wlist[4][kTileThreads];  // per wave: slot byte offsets
     __shared__ uint8_t sqm[kTileThreads];  // per staged record: the quadrants it may reach
     __shared__ uint32_t sopen[4];          // per wave: pixels still open after its last walk
+    __shared__ uint32_t sopen_end[4];      // (PASS 1) the same at the end of the list
 
     // XCD-aware bijective remap (blocks b and b+8 share an XCD,
     // cdna_hip_programming.md §5, T1).
@@ -205,6 +210,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     const int by = a.rows ? (int)a.rows[owned_row] : owned_row;
     const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
     const int width = a.width, height = a.height;
+    const uint32_t tile_flag = (uint32_t)(by * a.tiles_x + bx) * 4u + (k4 & 3u);  // (two-slab open4 slot)
+    if constexpr (PASS == 2) {
+        if (a.open4[tile_flag] == 0) return;  // (whole workgroup) every pixel finished in the first slab
+    }
     const int tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
@@ -227,6 +236,17 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     // separate per-lane flag is carried through the loop.
     float T = inside ? 1.0f : 0.0f;  // transmittance (tile rule: T = 1 - A)
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+    // compact = owned bin rows stacked (multi-GPU band buffer)
+    const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
+    if constexpr (PASS == 2) {
+        if (inside) {  // the state the first slab left: the same registers, resumed
+            const float4 st = a.out[(size_t)orow * width + px];
+            C0 = st.x;
+            C1 = st.y;
+            C2 = st.z;
+            T = st.w;
+        }
+    }
     bool done = !inside;  // MODE 2 / 3
     uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
     int cnt = 0;                 // MODE 2: covering fragments seen
@@ -465,7 +485,26 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     GS_CT_FLUSH();
     GS_TR_FLUSH();
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
+    bool keep_state = false;
+    if constexpr (PASS == 1) {
+        // does any pixel of the tile remain open for the second slab?
+        const bool open_w = __ballot(!finished()) != 0;
+        if (lane == 0) sopen_end[wave] = open_w ? 1u : 0u;
+        __syncthreads();
+        const uint4 o = *reinterpret_cast<const uint4*>(sopen_end);
+        keep_state = (o.x | o.y | o.z | o.w) != 0u;
+        if (tid == 0) {
+            a.open4[tile_flag] = keep_state ? 1 : 0;
+            if (keep_state && a.open_tiles) (void)atomicAdd(a.open_tiles, 1ull);
+        }
+    }
     if (!inside) return;
+    if constexpr (PASS == 1) {
+        if (keep_state) {  // (C, T) for the second slab; final pixels otherwise
+            a.out[(size_t)orow * width + px] = make_float4(C0, C1, C2, T);
+            return;
+        }
+    }
     if constexpr (SLAB == 1) {
         a.t_out[(size_t)py * width + px] = T;
     } else if constexpr (SLAB == 2) {
@@ -475,8 +514,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         a.thr_out[(size_t)py * width + px] = thr;
     } else {
         const float4 o = MODE == 3 ? kb.resolve() : make_float4(C0, C1, C2, 1.0f - T);
-        // compact = owned bin rows stacked (multi-GPU band buffer)
-        const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
         if (a.out_bgra8)
             a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
         else
@@ -484,7 +521,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     }
 }
 
-template <int MODE, bool CAP, int SLAB = 0>
+template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
@@ -495,7 +532,7 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
         return hipSuccess;
     }
     // t0/t1 (optional) are recorded by the dispatch packet itself
-    hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
+    hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
                           nwg);
     return hipGetLastError();
 }
@@ -503,6 +540,13 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
+    if (a.pass) {  // two-slab frames: tile / live50 rules, fp32 output, no cap, no depth slabs
+        if (cap || a.slab || a.out_bgra8 || !a.out || !a.open4 || (mode != 0 && mode != 1) || a.pass > 2)
+            return hipErrorInvalidValue;
+        if (a.pass == 1)
+            return mode == 0 ? launch_mode<0, false, 0, 1>(a, st, t0, t1) : launch_mode<1, false, 0, 1>(a, st, t0, t1);
+        return mode == 0 ? launch_mode<0, false, 0, 2>(a, st, t0, t1) : launch_mode<1, false, 0, 2>(a, st, t0, t1);
+    }
     if (a.slab) {  // full frame, no cap
         if (cap || a.rows || a.compact || a.out_bgra8 || (a.slab == 1 ? !a.t_out : (!a.out || (a.slab_rank && !a.t_all))))
             return hipErrorInvalidValue;

@@ -16,10 +16,17 @@ namespace gs {
 // without extra packets).
 // zero8 (optional): a 64-bit word the kernel clears (the frame's composite
 // fetch counter, CompositeArgs::fetched), so no memset dispatch is needed.
+// hist (optional): += the depth histogram of the two-slab cut (SlabSel),
+// kCutCopies x kCutBuckets words, bucket dkey >> kCutShift weighted by the
+// bins of the splat's rect, one copy per XCD (workgroup & 7); zeroed by
+// launch_tile_count_totals once the cut is taken.
+constexpr int kCutShift = 7;
+constexpr int kCutBuckets = (1 << kDepthBits) >> kCutShift;  // 256
+constexpr int kCutCopies = 8;
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
                              hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr,
-                             unsigned long long* zero8 = nullptr);
+                             unsigned long long* zero8 = nullptr, uint32_t* hist = nullptr);
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
@@ -35,10 +42,30 @@ constexpr int kScanItems = 4096;  // per block
 // host re-queues them with larger buffers).  Then launch_scan_duplicate.
 // zero[0..nzero) is cleared on the way (the first sort pass's digit counts,
 // PassCounts).
+// Two-slab frames: the frame's pairs in two passes split at a
+// depth-key cut K (S1 order composites ascending dkey, so every pair of the
+// first slab precedes every pair of the second in every bin list).
+//   mode 1: items with dkey < K only; the reduce takes K from the preprocess
+//           histogram (the bucket boundary where the pair share first reaches
+//           `frac`), stores it in *kcut and zeroes the histogram; total[4] =
+//           the pairs of both slabs (partials: 3 * nblocks words)
+//   mode 2: items with dkey >= K, and only into bins with open[bin] != 0
+//           (the first slab's composite left a pixel of the bin unsaturated)
+struct SlabSel {
+    int mode = 0;
+    const uint32_t* dkey = nullptr;  // per item (index order)
+    uint32_t* kcut = nullptr;
+    uint32_t* hist = nullptr;        // mode 1
+    const uint32_t* open = nullptr;  // mode 2: per bin
+    uint32_t tiles_x = 0;            // mode 2: bins per row
+    float frac = 0.3f;               // mode 1
+    unsigned long long* zero64 = nullptr;  // mode 1 (optional): cleared once the cut is taken (open-tile counter)
+};
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr);
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr,
+                                    const SlabSel& sel = SlabSel{});
 // (done: recorded by the totals kernel's own dispatch packet, not a separate
 // marker packet, which would leave a ~6 us bubble in the stream.)
 // The first LSD pass's digit counts of the pairs, C[digit][tile] with
@@ -58,11 +85,13 @@ constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts i
 // Index order runs one fused kernel; depth order (order set) a down-sweep
 // into offsets (n words of scratch) and a one-splat-per-lane duplicate.
 // Nothing is written when *npairs == 0 (see launch_tile_count_totals).
+// sel (index order only): the two-slab filter (mode 1 / 2, as the reduce).
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
-                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{});
+                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
+                                 const SlabSel& sel = SlabSel{});
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -146,6 +175,14 @@ struct CompositeArgs {
     // prefetched one; each of a bin's four tiles fetches its list itself),
     // the early-out-aware basis of the composite's algorithmic bytes
     unsigned long long* fetched;
+    // Two-slab frames (modes 0/1, no cap, fp32 output).  pass 1: the first
+    // slab's lists; a tile whose pixels all finished writes its final pixels,
+    // any other tile writes its state (C, T) and open4[bin * 4 + tile] = 1
+    // (else 0); open_tiles += open tiles.  pass 2: only open tiles, resuming
+    // from the state with the second slab's lists.
+    int pass;
+    uint8_t* open4;
+    unsigned long long* open_tiles;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals

@@ -183,14 +183,15 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
                                                          uint32_t* __restrict__ rect_hi,
-                                                         unsigned long long* __restrict__ zero8) {
+                                                         unsigned long long* __restrict__ zero8,
+                                                         uint32_t* __restrict__ hist) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i == 0 && zero8) *zero8 = 0ull;
-    if (i >= s.n) return;
+    uint32_t rlo = kEmptyRectLo, rhi = 0u;
+    uint32_t key = 0;
+    if (i < s.n) {
     const float* V = U.V;
     const float* VP = U.VP;
-    uint32_t key = 0;
-    uint32_t rlo = kEmptyRectLo, rhi = 0u;
 
     float4 a0 = scene_load(&s.p0[i]);
     float px = a0.x, py = a0.y, pz = a0.z;
@@ -358,11 +359,28 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
     dkey[i] = key;
     rect_lo[i] = rlo;
     rect_hi[i] = rhi;
+    }
+    if (hist) {
+        // two-slab cut (SlabSel): the workgroup's depth histogram, weighted by
+        // the bins of each rect, added into this XCD's copy (after every load
+        // and store of the kernel, so the barriers cost it nothing)
+        __shared__ uint32_t wh[kCutBuckets];
+        static_assert(kCutBuckets == 256, "one bucket per lane");
+        wh[threadIdx.x] = 0u;
+        __syncthreads();
+        if (rlo != kEmptyRectLo) {
+            const BinRect r = bin_rect(rlo, rhi, U.cell_mask != 0);
+            atomicAdd(&wh[key >> kCutShift], (r.bx1 - r.bx0 + 1u) * (r.by1 - r.by0 + 1u));
+        }
+        __syncthreads();
+        const uint32_t v = wh[threadIdx.x];
+        if (v) atomicAdd(&hist[(blockIdx.x & (kCutCopies - 1u)) * kCutBuckets + threadIdx.x], v);
+    }
 }
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
-                             hipEvent_t t1, unsigned long long* zero8) {
+                             hipEvent_t t1, unsigned long long* zero8, uint32_t* hist) {
     if (s.n == 0) {
         // no dispatch: the timing events still mark the (empty) stage
         if (zero8 && hipMemsetAsync(zero8, 0, 8, st) != hipSuccess) return hipGetLastError();
@@ -374,10 +392,10 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
     switch (sh_degree) {
-    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
-    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
-    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
-    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8); break;
+    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
+    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
+    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
+    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

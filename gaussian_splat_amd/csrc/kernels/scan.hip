@@ -26,32 +26,73 @@ struct CountSrc {
     const uint32_t* hi;
     RowOwnership own;
     bool masked;  // rect words carry the bin-exclusion mask
+    SlabSel sel;  // two-slab filter (mode 0: every item)
 };
 
-// Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
+// Two-slab cut from the preprocess histogram (one 256-lane workgroup; every
+// workgroup computes the same K): the first bucket boundary at which the
+// share of pairs reaches sel.frac; 0x8000 (every key) for an empty frame.
+__device__ __forceinline__ uint32_t slab_cut(const SlabSel& sel, uint32_t* tmp4, uint32_t* kres) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int c = 0; c < kCutCopies; ++c) v += sel.hist[c * kCutBuckets + threadIdx.x];
+    uint32_t tot;
+    const uint32_t ex = block256_exclusive_scan<uint32_t>(v, tmp4, &tot);
+    const uint32_t thr = (uint32_t)((float)tot * sel.frac) + 1u;  // (ties and empty frames: see below)
+    if (threadIdx.x == 0) *kres = 0x8000u;
+    __syncthreads();
+    if (tot > 0u && ex < thr && ex + v >= thr) *kres = (threadIdx.x + 1u) << kCutShift;
+    __syncthreads();
+    return *kres;
+}
+
+// The item's slab filter: does it take part, and are its bins limited to the open ones?
+__device__ __forceinline__ bool slab_item(const SlabSel& sel, uint32_t dk, uint32_t K) {
+    return sel.mode == 0 || (sel.mode == 1 ? dk < K : dk >= K);
+}
+__device__ __forceinline__ uint32_t item_count(const CountSrc& src, uint32_t lo, uint32_t hi, uint32_t dk, uint32_t K) {
+    if (!slab_item(src.sel, dk, K)) return 0u;
+    return src.sel.mode == 2 ? rect_open_count(lo, hi, src.own, src.masked, src.sel.open, src.sel.tiles_x)
+                             : rect_tile_count(lo, hi, src.own, src.masked);
+}
+
+// Per block: pair count -> partials[b], contributing splats -> partials[nb + b];
+// two-slab mode 1 also the pairs of both slabs -> partials[2 nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials,
                                                           uint2* __restrict__ fill, uint32_t nfill,
                                                           uint32_t* __restrict__ zero, uint32_t nzero) {
     __shared__ uint2 tmp[4];
+    __shared__ uint32_t ctmp[4], kres;
     const uint32_t base = blockIdx.x * kScanItems;
     // every rect loaded before the first use (clamped, branch-free): one
     // memory round trip instead of one per item (a conditional load is waited
     // for inside its branch)
-    uint32_t lo[kScanIpt], hi[kScanIpt];
+    uint32_t lo[kScanIpt], hi[kScanIpt], dk[kScanIpt];
+    const uint32_t* dsrc = src.sel.mode ? src.sel.dkey : src.lo;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const uint32_t i = min(base + k * 256 + threadIdx.x, n - 1u);
         lo[k] = src.lo[i];
         hi[k] = src.hi[i];
+        dk[k] = dsrc[i];
+    }
+    uint32_t K = 0;
+    if (src.sel.mode == 1) {
+        K = slab_cut(src.sel, ctmp, &kres);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *src.sel.kcut = K;
+    } else if (src.sel.mode == 2) {
+        K = *src.sel.kcut;
     }
     // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
-    uint32_t s = 0, vis = 0;
+    uint32_t s = 0, vis = 0, all = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
-        const uint32_t c = base + k * 256 + threadIdx.x < n ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
+        const bool in = base + k * 256 + threadIdx.x < n;
+        const uint32_t c = in ? item_count(src, lo[k], hi[k], dk[k], K) : 0u;
         s += c;
         vis += c > 0;
+        if (src.sel.mode == 1) all += in ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
     }
     // the frame's bin ranges start empty and the first sort pass's digit
     // counts at zero (saves two fill dispatches; stored after the loads, which
@@ -64,10 +105,16 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
     vis = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(vis), 63);
     const uint32_t wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 0) tmp[wave] = make_uint2(s, vis);
+    if (src.sel.mode == 1) {
+        all = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(all), 63);
+        if ((threadIdx.x & 63u) == 0) ctmp[wave] = all;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         partials[blockIdx.x] = (uint64_t)tmp[0].x + tmp[1].x + tmp[2].x + tmp[3].x;
         partials[gridDim.x + blockIdx.x] = (uint64_t)tmp[0].y + tmp[1].y + tmp[2].y + tmp[3].y;
+        if (src.sel.mode == 1)
+            partials[2 * gridDim.x + blockIdx.x] = (uint64_t)ctmp[0] + ctmp[1] + ctmp[2] + ctmp[3];
     }
 }
 
@@ -103,16 +150,23 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
-                                                                     uint32_t* __restrict__ npairs, uint64_t cap) {
+                                                                     uint32_t* __restrict__ npairs, uint64_t cap,
+                                                                     uint32_t* __restrict__ hist,
+                                                                     unsigned long long* __restrict__ zero64) {
+    if (zero64 && threadIdx.x == 0) *zero64 = 0ull;
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
         seg_sample[0] = 0u;
         seg_sample[1] = 0u;
     }
+    // two-slab mode 1: every reduce block has taken the cut, so the histogram
+    // is cleared here for the next frame's preprocess
+    if (hist)
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(kCutCopies * kCutBuckets); i += kPartThreads) hist[i] = 0u;
     __shared__ uint64_t tmp[kPartThreads / 64];
     constexpr uint32_t CH = kPartThreads * kPartIpt;
-    uint64_t carry = 0, vis = 0;
+    uint64_t carry = 0, vis = 0, all = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
         const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
         uint64_t v[kPartIpt], s = 0;
@@ -121,6 +175,7 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
             v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
             s += v[k];
             vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
+            if (hist) all += i0 + k < nb ? partials[2 * nb + i0 + k] : 0u;
         }
         uint64_t t;
         uint64_t run = carry + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
@@ -131,11 +186,13 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         }
         carry += t;
     }
-    uint64_t vt;
+    uint64_t vt, at = 0;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
+    if (hist) block1024_exclusive_scan<uint64_t>(all, tmp, &at);
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
+        if (hist) total[4] = at;  // the pairs of both slabs
         if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
     }
 }
@@ -189,6 +246,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // (absent arrays read a stand-in, so no load sits in a branch, where its
     // value would be waited for at once)
     const uint64_t part = partials[blockIdx.x];
+    const uint32_t K = src.sel.mode ? *src.sel.kcut : 0u;
     const uint32_t* dsrc = dkey ? dkey : src.lo;
     const uint32_t* osrc = order ? order : src.lo;
     uint32_t rlo[kDupIpt], rhi[kDupIpt], dk[kDupIpt], ord[kDupIpt];
@@ -209,7 +267,13 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        st[pad32(i)] = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        if (!slab_item(src.sel, dk[k], K)) {  // (two-slab frames: the other slab's items emit nothing)
+            rlo[k] = kEmptyRectLo;
+            rhi[k] = 0u;
+        }
+        st[pad32(i)] = src.sel.mode == 2
+                           ? rect_open_count(rlo[k], rhi[k], src.own, src.masked, src.sel.open, src.sel.tiles_x)
+                           : rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
     }
     block_lds_sync();
     uint32_t v[kDupIpt];
@@ -240,20 +304,23 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         const uint32_t off = st[pad32(i)];
         const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t val = order ? ord[k] : j;
+        const uint32_t* open = src.sel.mode == 2 ? src.sel.open : nullptr;
         if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals,
-                           [&](uint32_t g, uint32_t bin) {
-                               if (g == next) {
-                                   ++t;
-                                   next += pc.tile;
-                               }
-                               const uint32_t d = bin & pc.mask;
-                               if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
-                               else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
-                           });
+            emit_bin_pairs(
+                r, tiles_x, src.own, key_hi, val, off, keys, vals,
+                [&](uint32_t g, uint32_t bin) {
+                    if (g == next) {
+                        ++t;
+                        next += pc.tile;
+                    }
+                    const uint32_t d = bin & pc.mask;
+                    if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
+                    else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
+                },
+                open);
         } else {
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals);
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals, open);
         }
     }
     if (pc.C) {
@@ -421,8 +488,11 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done) {
-    const CountSrc src{rect_lo, rect_hi, own, masked};
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done,
+                                    const SlabSel& sel) {
+    if (sel.mode && (!sel.dkey || !sel.kcut || (sel.mode == 1 && !sel.hist) || (sel.mode == 2 && !sel.open)))
+        return hipErrorInvalidValue;
+    const CountSrc src{rect_lo, rect_hi, own, masked, sel};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
         if (nranges) {
@@ -436,19 +506,25 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
     } else {
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
+    // (an empty mode-1 frame runs no reduce: the cut stays from the last one,
+    // and the duplicate emits nothing either way)
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap);
+                          total, seg_sample, npairs, cap, sel.mode == 1 ? sel.hist : nullptr,
+                          sel.mode == 1 ? sel.zero64 : nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
-                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc) {
+                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
+                                 const SlabSel& sel) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
-    const CountSrc src{rect_lo, rect_hi, own, masked};
+    if (sel.mode && (order || !dkey || sel.dkey != dkey || !sel.kcut || (sel.mode == 2 && !sel.open)))
+        return hipErrorInvalidValue;
+    const CountSrc src{rect_lo, rect_hi, own, masked, sel};
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);

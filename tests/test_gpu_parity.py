@@ -364,7 +364,7 @@ def test_bin_first_equals_depth_first(built, n, w, h, mode, cap, wall, zr):
         sc.pos[:k] = (eye + 5.0 * fwd + a[:, None] * right + b[:, None] * up).astype(np.float32)
     out = {}
     for b in ("depth_first", "bin_first"):
-        r = InstancedSplatRenderer(sc, Options(mode=mode, cap=cap, binning=b))
+        r = InstancedSplatRenderer(sc, Options(mode=mode, cap=cap, binning=b, depth_split=False))  # (one-slab lists)
         r.initialize(0)
         img = r.render_host(V, P, w, h)
         keys, vals = r.sorted_pairs()
