@@ -27,7 +27,7 @@ namespace gs {
 
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
-__device__ unsigned long long g_cc[8];
+__device__ unsigned long long g_cc[16];
 #define GS_CC(i, v) (void)atomicAdd(&g_cc[i], (unsigned long long)(v))
 #else
 #define GS_CC(i, v) (void)0
@@ -248,6 +248,15 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         }
     }
     bool done = !inside;  // MODE 2 / 3
+#ifdef GS_COMPOSITE_COUNTERS
+    uint32_t cc_n4 = 0, cc_n2 = 0, cc_nl = 0;
+    uint32_t cc_b4 = 0, cc_bl = 0, cc_br = 0, cc_be = 0;  // per batch
+    __shared__ uint16_t cc_bmr[kTileThreads], cc_bme[kTileThreads];
+    // this lane's 4x4 block of the tile (bit row * 4 + column) and its lane group
+    const uint32_t cc_blk = ((wave >> 1) * 2u + (lane >> 5)) * 4u + (wave & 1u) * 2u + ((lane >> 2) & 1u);
+    const uint64_t cc_g4 = ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) &
+                           ((lane & 4u) ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full);
+#endif
     uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
     int cnt = 0;                 // MODE 2: covering fragments seen
     if constexpr (CAP) {
@@ -271,6 +280,28 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         else if constexpr (MODE == 1) return T < kTMin;
         else return done;
     };
+#ifdef GS_COMPOSITE_COUNTERS
+    auto cc_rec = [&](uint32_t off) {
+        const uint32_t k = off / (uint32_t)sizeof(StagedRec);
+        const bool gopen = (__ballot(!finished()) & cc_g4) != 0;
+        cc_br += (gopen && ((cc_bmr[k] >> cc_blk) & 1u)) ? 1u : 0u;
+        cc_be += (gopen && ((cc_bme[k] >> cc_blk) & 1u)) ? 1u : 0u;
+    };
+    auto cc_batch = [&]() {
+        if constexpr (MODE == 0) {
+            uint32_t x[4] = {cc_b4, cc_bl, cc_br, cc_be};
+            for (int o = 32; o > 0; o >>= 1)
+                for (int q = 0; q < 4; ++q) x[q] = max(x[q], (uint32_t)__shfl_xor((int)x[q], o, 64));
+            if (lane == 0) {
+                GS_CC(1, x[0]);
+                GS_CC(2, x[1]);
+                GS_CC(14, x[2]);
+                GS_CC(15, x[3]);
+            }
+        }
+        cc_b4 = cc_bl = cc_br = cc_be = 0;
+    };
+#endif
 
     // One record at this lane's pixel: coverage (K6 closed form: the quad box
     // |uv| <= 3 and the 0.01 cutoff, tile.metal:142-156,191-195), then the
@@ -300,6 +331,20 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 const uint64_t m = __ballot(in);
                 if (lane == 0 && m) GS_CC(4, 1);
                 if (lane == 0) GS_CC(7, __popcll(m));
+                // footprint estimates: open / covered lanes per body, and per
+                // 4x4 / 8x4 lane group the bodies it would walk (covered lane
+                // and an open lane in the group), per lane its own walk
+                const uint64_t mo = __ballot(!finished()), mc = __ballot(covered);
+                if (lane == 0) GS_CC(8, __popcll(mo));
+                if (lane == 0) GS_CC(9, __popcll(mc));
+                const uint64_t g4 = ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) &
+                                    ((lane & 4u) ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full);
+                const uint64_t g2 = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+                cc_n4 += ((mo & g4) && (mc & g4)) ? 1u : 0u;
+                cc_n2 += ((mo & g2) && (mc & g2)) ? 1u : 0u;
+                cc_nl += in ? 1u : 0u;
+                cc_b4 += ((mo & g4) && (mc & g4)) ? 1u : 0u;
+                cc_bl += in ? 1u : 0u;
             }
 #endif
             if (in) {
@@ -428,6 +473,29 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                     }
                 }
                 sqm[tid] = (uint8_t)qm;
+#ifdef GS_COMPOSITE_COUNTERS
+                {
+                    const uint32_t cm = a.cell_mask ? rect_cell_mask(wlo, whi) : 0u;
+                    const float eu = 1.5f * (fabsf(st.a.z) + fabsf(st.a.w)), ev = 1.5f * (fabsf(st.b.x) + fabsf(st.b.y));
+                    uint32_t bmr = 0, bme = 0;
+                    for (uint32_t j = 0; j < 4; ++j)
+                        for (uint32_t i = 0; i < 4; ++i) {
+                            const uint32_t bx0 = tx0 + 4u * i, by0 = ty0 + 4u * j;
+                            bool hit = !(x1 < bx0 || x0 > bx0 + 3u) && !(y1 < by0 || y0 > by0 + 3u);
+                            const uint32_t dcx = (bx0 >> 3) - (x0 >> 3), dcy = (by0 >> 3) - (y0 >> 3);
+                            if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) hit = false;
+                            const float cxl = 4.0f * (float)i + 2.0f, cyl = 4.0f * (float)j + 2.0f;
+                            const float uc = st.a.x + st.a.z * cxl + st.a.w * cyl;
+                            const float vc = st.a.y + st.b.x * cxl + st.b.y * cyl;
+                            const float tu = fmaxf(fabsf(uc) - eu, 0.0f), tv = fmaxf(fabsf(vc) - ev, 0.0f);
+                            const bool he = fmaxf(tu, tv) <= kBoxS * 1.001f && tu * tu + tv * tv <= kQMaxS * 1.001f;
+                            bmr |= hit ? 1u << (4u * j + i) : 0u;
+                            bme |= (hit && he) ? 1u << (4u * j + i) : 0u;
+                        }
+                    cc_bmr[tid] = (uint16_t)bmr;
+                    cc_bme[tid] = (uint16_t)bme;
+                }
+#endif
             }
         }
         GS_CT(1);
@@ -474,16 +542,47 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 const float2 c1 = make_float2(p1.c.x, p1.c.y);
                 const uint32_t i0 = kIds ? __float_as_uint(p0.c.z) : 0u, i1 = kIds ? __float_as_uint(p1.c.z) : 0u;
                 if (i + 3 < nl) w2 = wl2[(i >> 1) + 1];
+#ifdef GS_COMPOSITE_COUNTERS
+                cc_rec(wlist[wave][i]);
+#endif
                 body_v(a0, b0, c0, i0, (_Float16)0.0f);
+#ifdef GS_COMPOSITE_COUNTERS
+                cc_rec(wlist[wave][i + 1]);
+#endif
                 body_v(a1, b1, c1, i1, (_Float16)0.0f);
             }
-            if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
+            if (i < nl && __ballot(!finished()) != 0) {
+#ifdef GS_COMPOSITE_COUNTERS
+                cc_rec(wlist[wave][i]);
+#endif
+                body(wlist[wave][i++]);
+            }
         }
         if (lane == 0) GS_CC(3, i);
+#ifdef GS_COMPOSITE_COUNTERS
+        cc_batch();
+#endif
         GS_CT(4);
     }
     GS_CT_FLUSH();
     GS_TR_FLUSH();
+#ifdef GS_COMPOSITE_COUNTERS
+    if constexpr (MODE == 0) {
+        uint32_t x4 = cc_n4, x2 = cc_n2, xl = cc_nl, sl = cc_nl;
+        for (int o = 32; o > 0; o >>= 1) {
+            x4 = max(x4, (uint32_t)__shfl_xor((int)x4, o, 64));
+            x2 = max(x2, (uint32_t)__shfl_xor((int)x2, o, 64));
+            xl = max(xl, (uint32_t)__shfl_xor((int)xl, o, 64));
+            sl += (uint32_t)__shfl_xor((int)sl, o, 64);
+        }
+        if (lane == 0) {
+            GS_CC(10, x4);
+            GS_CC(11, x2);
+            GS_CC(12, xl);
+            GS_CC(13, sl);
+        }
+    }
+#endif
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
     bool keep_state = false;
     if constexpr (PASS == 1) {
@@ -581,7 +680,7 @@ extern "C" int gs_debug_composite_trace(void* out, unsigned n) {  // n uint4 ent
 #endif
 #ifdef GS_COMPOSITE_COUNTERS
 extern "C" int gs_debug_composite_counters(unsigned long long* out) {
-    unsigned long long zero[8] = {};
+    unsigned long long zero[16] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cc), sizeof zero) != hipSuccess) return 1;
     return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_cc), zero, sizeof zero) != hipSuccess;
 }

@@ -51,7 +51,7 @@ if hasattr(lib(), "gs_debug_composite_timers"):  # -DGS_COMPOSITE_TIMERS build: 
     sys.exit(0)
 f = lib().gs_debug_composite_counters
 f.argtypes = [C.POINTER(C.c_uint64)]
-buf = (C.c_uint64 * 8)()
+buf = (C.c_uint64 * 16)()
 r.render(V, P, W, H, out=out)
 torch.cuda.synchronize()
 f(buf)
@@ -61,11 +61,18 @@ f(buf)
 c = list(buf)
 st = r.last_stats()
 waves, wg = c[0], c[0] // 4
-names = ["waves", "iters if 8x4 halves", "iters if 4x4 quarters", "bodies", "bodies w/ covered lane", "wg-batches", "list entries",
-         "covered lanes"]
+names = ["waves", "batch-max exact 4x4-group walks", "batch-max per-lane walks", "bodies", "bodies w/ covered lane", "wg-batches", "list entries",
+         "covered open lanes", "open lanes", "covered lanes", "sum max 4x4-group walks", "sum max 8x4-half walks",
+         "sum max lane walks", "sum lane walks", "batch-max rect 4x4-group walks", "batch-max ellipse 4x4-group walks"]
 for n, v in zip(names, c):
     print(f"{n:>24}: {v}")
 print(f"pairs {st['pairs']}  list/bin {st['pairs'] / (st['tiles']):.0f}")
 print(f"per wave: halves {c[1] / waves:.1f}  quarters {c[2] / waves:.1f}  bodies {c[3] / waves:.1f}  "
       f"covered-bodies {c[4] / waves:.1f}  lanes/covered-body {c[7] / max(c[4], 1):.1f}")
+print(f"per body: open lanes {c[8] / max(c[3], 1):.1f}  covered lanes {c[9] / max(c[3], 1):.1f}  "
+      f"covered+open {c[7] / max(c[3], 1):.1f}")
+print(f"per wave walk steps: now {c[3] / waves:.1f}  4x4 groups {c[10] / waves:.1f}  8x4 halves {c[11] / waves:.1f}  "
+      f"per-lane max {c[12] / waves:.1f}  per-lane mean {c[13] / waves / 64:.1f}")
+print(f"per wave, summed per-batch maxima: exact 4x4 groups {c[1] / waves:.1f}  per-lane {c[2] / waves:.1f}  "
+      f"rect 4x4 groups {c[14] / waves:.1f}  ellipse 4x4 groups {c[15] / waves:.1f}")
 print(f"per wg: batches {c[5] / wg:.2f}  list {c[6] / wg:.0f}  batches if no exit {c[6] / wg / 256:.2f}")
