@@ -377,7 +377,12 @@ void mark(gs_handle* h, int k, hipStream_t st) {
 
 float elapsed(gs_handle* h, int a, int b) {
     float ms = 0.0f;
-    if (h->opt.stage_timing == 1 && h->events) (void)hipEventElapsedTime(&ms, h->ev[a], h->ev[b]);
+    // (an event this frame did not record, e.g. a shard render without its
+    // project: 0, and the error is not left for the next launch's check)
+    if (h->opt.stage_timing == 1 && h->events && hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) != hipSuccess) {
+        (void)hipGetLastError();
+        ms = 0.0f;
+    }
     return ms;
 }
 

@@ -115,6 +115,48 @@ def assemble(bands, width: int, height: int, world: int, owner=None):
     return frame[:height]
 
 
+def gather_frame(band, width: int, height: int, world: int, rank: int, owner=None, group=None, p2p=None):
+    """The rank bands -> the full frame on rank 0 (None elsewhere).  With the
+    default contiguous ownership over RCCL every rank sends its valid rows
+    straight into their place in rank 0's frame (point-to-point, no padded
+    bands, no reassembly copies); gloo (host-staged) and custom owner tables
+    gather the padded bands and scatter them (`assemble`).  p2p=True forces the
+    point-to-point path (CPU tensors over gloo: its test)."""
+    import torch
+    import torch.distributed as dist
+
+    if p2p is None:
+        p2p = owner is None and not _host_staged(group)
+    if p2p:
+        assert owner is None, "point-to-point gather: contiguous default ownership only"
+        R = (height + ROW - 1) // ROW
+        spans = [(min(height, r * R // world * ROW), min(height, (r + 1) * R // world * ROW)) for r in range(world)]
+        if rank == 0:
+            frame = torch.empty((height, width, 4), dtype=torch.float32, device=band.device)
+            ops = [dist.P2POp(dist.irecv, frame[y0:y1], r, group) for r, (y0, y1) in enumerate(spans)
+                   if r > 0 and y1 > y0]
+            reqs = dist.batch_isend_irecv(ops) if ops else []
+            y0, y1 = spans[0]
+            if y1 > y0:
+                frame[y0:y1].copy_(band[: y1 - y0])
+            for q in reqs:
+                q.wait()
+            return frame
+        y0, y1 = spans[rank]
+        if y1 > y0:
+            dist.send(band[: y1 - y0], 0, group=group)
+        return None
+    if _host_staged(group):
+        hb = band.cpu()
+        bands = [hb.new_empty(hb.shape) for _ in range(world)] if rank == 0 else None
+        dist.gather(hb, bands, dst=0, group=group)
+        bands = [b.to(band.device) for b in bands] if rank == 0 else None
+    else:
+        bands = [band.new_empty(band.shape) for _ in range(world)] if rank == 0 else None
+        dist.gather(band, bands, dst=0, group=group)
+    return assemble(bands, width, height, world, owner) if rank == 0 else None
+
+
 class HipShardBackend:
     """Per-rank compute through libgsplat.so (device buffers are torch tensors)."""
 
@@ -195,22 +237,12 @@ class BandRenderer:
     def render(self, view, proj, width, height, gather: bool = True):
         """The full frame on rank 0 (None elsewhere) when gather=True, else
         this rank's band."""
-        import torch.distributed as dist
-
         band = self.b.render(view, proj, width, height)
         if not gather:
             return band
         if self.world == 1:
             return band[:height]
-        if _host_staged(self.group):
-            hb = band.cpu()
-            bands = [hb.new_empty(hb.shape) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(hb, bands, dst=0, group=self.group)
-            bands = [b.to(band.device) for b in bands] if self.rank == 0 else None
-        else:
-            bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(band, bands, dst=0, group=self.group)
-        return assemble(bands, width, height, self.world, self.b.owner) if self.rank == 0 else None
+        return gather_frame(band, width, height, self.world, self.rank, self.b.owner, self.group)
 
 
 SLAB_BINS = 2048      # GS_SLAB_BINS: slab histogram bins ...
@@ -316,8 +348,6 @@ class ShardedRenderer:
     def render(self, view, proj, width, height, gather: bool = True):
         """Returns the full frame on rank 0 (None elsewhere) when gather=True,
         else this rank's band buffer."""
-        import torch.distributed as dist
-
         send, counts = self.b.project(view, proj, width, height)
         recv, nrec = exchange(send, counts, self.b.xbytes, self.world, self.group)
         band = self.b.render(recv, nrec, width, height)
@@ -325,15 +355,7 @@ class ShardedRenderer:
             return band
         if self.world == 1:
             return assemble([band], width, height, 1)
-        if _host_staged(self.group):
-            hb = band.cpu()
-            bands = [hb.new_empty(hb.shape) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(hb, bands, dst=0, group=self.group)
-            bands = [b.to(band.device) for b in bands] if self.rank == 0 else None
-        else:
-            bands = [band.new_empty(band.shape) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(band, bands, dst=0, group=self.group)
-        return assemble(bands, width, height, self.world, getattr(self.b, "owner", None)) if self.rank == 0 else None
+        return gather_frame(band, width, height, self.world, self.rank, getattr(self.b, "owner", None), self.group)
 
 
 def _all_reduce_sum(t, group):
