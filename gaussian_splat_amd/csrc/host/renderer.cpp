@@ -125,6 +125,18 @@ struct gs_handle {
         double long_share = 0.0;        // share of its pairs in lists longer than kSegLdsMax
     } order;
     gs_stats stats{};
+    // Bin-first single-GPU frames: the preprocess sums each scan block's
+    // pairs into ppart (PreFuse), prepared by render_frame (prepare_lists)
+    struct ListPrep {
+        bool ok = false;
+        uint32_t cap = 0;
+        gs::PassCounts pc;
+    } fused_prep;
+    DevBuf ppart;
+    size_t ppart_words = 0;
+    bool ppart_dirty = false;  // a fused preprocess ran without its scan (error path): clear first
+    bool fused_last = false;   // the frame in `stats` scanned fused block sums
+    int order_pick = -1;       // binning order decided before the preprocess (-1: not yet)
     // multi-GPU shard config
     int32_t rank = 0, world = 1;
     std::vector<uint8_t> custom_owner;  // gs_shard_set_rows (empty: default ranges)
@@ -172,7 +184,7 @@ struct gs_handle {
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch,
-                          &ghist, &kcut, &open4, &partials2, &npairs2, &scratch2, &tot2, &alt_rlo, &alt_rhi})
+                          &ghist, &kcut, &open4, &partials2, &npairs2, &scratch2, &tot2, &alt_rlo, &alt_rhi, &ppart})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -462,6 +474,63 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
     return GS_OK;
 }
 
+// Pair-key bits of a frame's bin ids: at least one, since the bin ranges are
+// written by the last sort pass (a single-bin frame still needs one pass).
+int list_key_bits(const gs::FrameUniforms& U) { return std::max(bits_for((uint32_t)(U.tiles_x * U.tiles_y)), 1); }
+
+// Pair capacity of the current buffer set: at least `want` (0 on failure).
+uint32_t reserve_pairs(gs_handle* h, uint64_t want) {
+    const size_t p = (size_t)std::max<uint64_t>(want, 1) * 4;
+    // growing frees the set's buffers: its last composite must be done
+    if (p > std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) &&
+        hipEventSynchronize(h->set_free[h->set]) != hipSuccess)
+        return 0;
+    for (DevBuf* b : {&h->keys, &h->vals, &h->tkeys, &h->tvals})
+        if (b->reserve(p) != hipSuccess) return 0;
+    const size_t c = std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) / 4;
+    const uint32_t cap = (uint32_t)std::min<size_t>(c, UINT32_MAX - 1);
+    if (h->sort_scratch.reserve(gs::radix_sort_scratch_words(cap) * 4) != hipSuccess) return 0;
+    return cap;
+}
+
+// Index order: the duplicate counts the first sort pass's digits itself when
+// a duplicate block's pairs (estimated from p_est) fit its LDS count tiles;
+// beyond them counts would go to contended global atomics (none then).
+gs::PassCounts pass_counts(gs_handle* h, uint32_t m, bool index_order, const gs::SortPlan& plan, uint32_t cap,
+                           uint64_t p_est) {
+    gs::PassCounts pc;
+    const double per_block = (double)p_est * gs::kScanItems / (double)std::max<uint32_t>(m, 1);
+    if (index_order && plan.passes > 0 && per_block <= (double)(gs::kDupCountTiles - 1) * gs::radix_sort_tile_items()) {
+        pc.C = h->sort_scratch.as<uint32_t>();
+        pc.tile = gs::radix_sort_tile_items();
+        pc.mask = plan.mask[0];
+        pc.ntiles = (cap + pc.tile - 1) / pc.tile;
+    }
+    return pc;
+}
+
+// Buffers of a frame's lists over m items: bin ranges, offsets (depth
+// order), the pair capacity (>= the last frame's P) and the first pass's
+// digit counting.
+gs_status prepare_lists(gs_handle* h, uint32_t m, bool index_order, const gs::FrameUniforms& U,
+                        gs_handle::ListPrep* lp) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
+    if (!index_order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
+    lp->cap = reserve_pairs(h, h->order.frame_pairs);
+    if (!lp->cap) return fail(GS_ERR_OOM, "pair buffers");
+    lp->pc = pass_counts(h, m, index_order, gs::make_sort_plan(list_key_bits(U)), lp->cap, h->order.frame_pairs);
+    return GS_OK;
+}
+
+// Binning order of this frame: decided once, before its preprocess when
+// that fuses the scan (render_frame), else here.
+bool pick_bin_first(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
+    const int p = h->order_pick;
+    h->order_pick = -1;
+    return p >= 0 ? p == 1 : bin_first_order(h, U, m);
+}
+
 // Bin lists from m splats visited in `order` (nullptr = index order) with
 // rects (rect_lo, rect_hi) in that order: per-block pair totals and their
 // scan (P and the visible count to host) -> down-sweep fused with the
@@ -479,48 +548,31 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     const gs::SlabSel no_sel;
     const gs::SlabSel& fs = sel ? *sel : no_sel;
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    // at least one key bit: the bin ranges are written by the last sort pass,
-    // so a single-bin frame (W, H <= 32) still needs one pass
-    const int bits = std::max(bits_for(T), 1);
-    GS_HIP(h->ranges.reserve((size_t)std::max<uint32_t>(T, 1) * sizeof(uint2)));
-    if (order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
-    // pair capacity of this buffer set: at least the last frame's P
-    auto reserve_pairs = [&](uint64_t want) -> uint32_t {
-        const size_t p = (size_t)std::max<uint64_t>(want, 1) * 4;
-        // growing frees the set's buffers: its last composite must be done
-        if (p > std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) &&
-            hipEventSynchronize(h->set_free[h->set]) != hipSuccess)
-            return 0;
-        for (DevBuf* b : {&h->keys, &h->vals, &h->tkeys, &h->tvals})
-            if (b->reserve(p) != hipSuccess) return 0;
-        const size_t c = std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) / 4;
-        const uint32_t cap = (uint32_t)std::min<size_t>(c, UINT32_MAX - 1);
-        if (h->sort_scratch.reserve(gs::radix_sort_scratch_words(cap) * 4) != hipSuccess) return 0;
-        return cap;
-    };
-    uint32_t cap = reserve_pairs(h->order.frame_pairs);
-    if (!cap) return fail(GS_ERR_OOM, "pair buffers");
-    // index order: the duplicate counts the first sort pass's digits itself,
-    // when a duplicate block's pairs (estimated from the last frame's P) fit
-    // its LDS count tiles; beyond them counts go to contended global atomics
+    const int bits = list_key_bits(U);
     const gs::SortPlan plan = gs::make_sort_plan(bits);
-    auto pass_counts = [&](uint64_t p_est) {
-        gs::PassCounts pc;
-        const double per_block = (double)p_est * gs::kScanItems / (double)std::max<uint32_t>(m, 1);
-        if (!order && plan.passes > 0 &&
-            per_block <= (double)(gs::kDupCountTiles - 1) * gs::radix_sort_tile_items()) {
-            pc.C = h->sort_scratch.as<uint32_t>();
-            pc.tile = gs::radix_sort_tile_items();
-            pc.mask = plan.mask[0];
-            pc.ntiles = (cap + pc.tile - 1) / pc.tile;
-        }
-        return pc;
-    };
-    gs::PassCounts pc = pass_counts(h->order.frame_pairs);
-    GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
-                                        h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, h->ranges.as<uint2>(), T,
-                                        h->npairs.as<uint32_t>(), cap, pc.C, pc.C ? (pc.mask + 1) * pc.ntiles : 0u,
-                                        st, h->totals_ev, fs));
+    // the preprocess already summed the scan blocks (render_frame, PreFuse)
+    const bool fused = h->fused_prep.ok && !order && !sel && own.dev.owner == nullptr;
+    gs_handle::ListPrep lp = h->fused_prep;
+    h->fused_prep.ok = false;
+    h->fused_last = fused;
+    if (!fused) {
+        gs_status ps = prepare_lists(h, m, order == nullptr, U, &lp);
+        if (ps != GS_OK) return ps;
+    }
+    uint32_t cap = lp.cap;
+    gs::PassCounts pc = lp.pc;
+    if (fused) {
+        GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
+                                              h->partials.as<uint64_t>(), h->dev_total,
+                                              h->seg_sample.as<uint32_t>() + 2 * h->set, h->npairs.as<uint32_t>(), cap,
+                                              st, h->totals_ev));
+        h->ppart_dirty = false;
+    } else {
+        GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
+                                            h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set,
+                                            h->ranges.as<uint2>(), T, h->npairs.as<uint32_t>(), cap, pc.C,
+                                            pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, h->totals_ev, fs));
+    }
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
     // bin id), then a stable sort by bin id only; the last pass also writes
@@ -553,10 +605,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     if (P_all > cap) {
         // the queued lists were no-ops (ranges still empty): grow, queue again
         GS_HIP(hipStreamSynchronize(st));
-        if (!(cap = reserve_pairs(P_all))) return fail(GS_ERR_OOM, "pair buffers");
+        if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
-        pc = pass_counts(P);
+        pc = pass_counts(h, m, order == nullptr, plan, cap, P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         GS_HIP(enqueue_lists());
     }
@@ -689,7 +741,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         h->stats.pairs = (int64_t)P;
         return GS_OK;
     }
-    if (!mlab && bin_first_order(h, U, m)) {
+    if (!mlab && pick_bin_first(h, U, m)) {
         // Bin-first: bin lists in arrival (index) order with
         // the depth key carried in the pair keys, then each list stably
         // sorted by depth key -> (depth, index) order, the same lists as the
@@ -834,6 +886,8 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     // depth-first: down-sweep (rects + offsets written, 12 B) and duplicate
     // (rects, order, offsets, 16 B).  Both write the pairs (8 B each).
     s.bytes_scan = N * 8 + T * 8;  // (+ the empty bin ranges, filled on the way)
+    if (h->fused_last)  // the block sums came from the preprocess: the scan reads them
+        s.bytes_scan = (N + gs::kScanItems - 1) / gs::kScanItems * 16 + T * 8;
     s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pi * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
@@ -1176,9 +1230,39 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
     const bool split_on = ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1;
     uint32_t* hist = split_on && !bgra8 && h->ghist.ptr ? h->ghist.as<uint32_t>() : nullptr;
+    // Bin-first frames of one GPU: the preprocess also sums every scan
+    // block's pairs, fills the empty bin ranges and zeroes the first sort
+    // pass's counts (PreFuse), so the chain starts at the scan of the block
+    // sums.  The binning order and the list buffers are settled first.
+    // GS_FUSED_SCAN=0: the separate reduce pass (A/B).
+    static const char* fs_env = std::getenv("GS_FUSED_SCAN");
+    gs::PreFuse fuse;
+    h->fused_prep.ok = false;
+    h->order_pick = -1;
+    if (!band && h->world == 1 && !hist && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
+        const bool bf = bin_first_order(h, U, (uint32_t)h->n);
+        h->order_pick = bf ? 1 : 0;
+        if (bf) {
+            if ((s = prepare_lists(h, (uint32_t)h->n, true, U, &h->fused_prep)) != GS_OK) return s;
+            const uint32_t nb = (uint32_t)((h->n + gs::kScanItems - 1) / gs::kScanItems);
+            GS_HIP(h->ppart.reserve((size_t)nb * 16));
+            if (h->ppart_words != (size_t)nb * 2 || h->ppart_dirty) {
+                GS_HIP(hipMemsetAsync(h->ppart.ptr, 0, (size_t)nb * 16, sp));  // (then kept clear by the scan)
+                h->ppart_words = (size_t)nb * 2;
+            }
+            fuse.part = h->ppart.as<unsigned long long>();
+            fuse.nb = nb;
+            fuse.fill = h->ranges.as<uint2>();
+            fuse.nfill = T;
+            fuse.zero = h->fused_prep.pc.C;
+            fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
+            h->fused_prep.ok = true;
+            h->ppart_dirty = true;  // (until its scan is queued)
+        }
+    }
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h), hist));
+                                 kernel_event(h, 1), fetch_counter(h), hist, fuse));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, compact,
@@ -1442,6 +1526,8 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     GS_HIP(h->rrlo.reserve(mm * 4));
     GS_HIP(h->rrhi.reserve(mm * 4));
     float4* rv = static_cast<float4*>(recv);
+    h->order_pick = -1;  // (decided in bin_sort_composite for received records)
+    h->fused_prep.ok = false;
     mark(h, 8, st);
     GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));

@@ -23,10 +23,26 @@ namespace gs {
 constexpr int kCutShift = 7;
 constexpr int kCutBuckets = (1 << kDepthBits) >> kCutShift;  // 256
 constexpr int kCutCopies = 8;
+// Bin-first single-GPU frames: the preprocess also does the
+// reduce half of the scan.  Every workgroup adds its splats' pair counts and
+// visible count into part[b] / part[nb + b] of its scan block b (kScanItems
+// splats; integer atomics, so the sums are exact), and the grid fills the
+// frame's empty bin ranges and zeroes the first sort pass's digit counts
+// (what scan_reduce_kernel does otherwise).  part starts at zero and is
+// consumed and cleared again by launch_scan_partials_fused.
+struct PreFuse {
+    unsigned long long* part = nullptr;  // null: off
+    uint32_t nb = 0;                     // scan blocks
+    uint2* fill = nullptr;
+    uint32_t nfill = 0;
+    uint32_t* zero = nullptr;
+    uint32_t nzero = 0;
+};
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
                              hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr,
-                             unsigned long long* zero8 = nullptr, uint32_t* hist = nullptr);
+                             unsigned long long* zero8 = nullptr, uint32_t* hist = nullptr,
+                             const PreFuse& fuse = PreFuse{});
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
@@ -68,6 +84,12 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
                                     const SlabSel& sel = SlabSel{});
 // (done: recorded by the totals kernel's own dispatch packet, not a separate
 // marker packet, which would leave a ~6 us bubble in the stream.)
+// The scan half alone, after a preprocess with PreFuse: the block sums in
+// part (2 nb words) are scanned into partials (as launch_tile_count_totals
+// leaves them) and part is cleared for the next frame.
+hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
+                                      uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
+                                      hipEvent_t done = nullptr);
 // The first LSD pass's digit counts of the pairs, C[digit][tile] with
 // `ntiles` columns, tiles of `tile` pairs, digit = bin & mask: the index-order
 // duplicate adds them up as it writes (C zeroed before), so the sort skips

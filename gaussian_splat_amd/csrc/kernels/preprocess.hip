@@ -10,6 +10,7 @@
 #include <hip/hip_ext.h>
 
 #include "gs_kernels.h"
+#include "gs_wave.h"
 
 namespace gs {
 
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                                                          uint32_t* __restrict__ rect_lo,
                                                          uint32_t* __restrict__ rect_hi,
                                                          unsigned long long* __restrict__ zero8,
-                                                         uint32_t* __restrict__ hist) {
+                                                         uint32_t* __restrict__ hist, const PreFuse fuse) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i == 0 && zero8) *zero8 = 0ull;
     uint32_t rlo = kEmptyRectLo, rhi = 0u;
@@ -376,11 +377,40 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
         const uint32_t v = wh[threadIdx.x];
         if (v) atomicAdd(&hist[(blockIdx.x & (kCutCopies - 1u)) * kCutBuckets + threadIdx.x], v);
     }
+    if (fuse.part) {
+        // the scan's reduce half: this workgroup's pairs and visible splats
+        // into its scan block's sums (the counts scan_duplicate recomputes)
+        __shared__ uint2 wsum[4];
+        const uint32_t c = rect_tile_count(rlo, rhi, RowOwnership{nullptr, 0u}, U.cell_mask != 0);
+        const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c), 63);
+        const uint32_t wv = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c > 0u ? 1u : 0u), 63);
+        if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = make_uint2(ws, wv);
+        // the frame's empty bin ranges and zeroed digit counts
+        const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+        for (uint32_t z = g; z < fuse.nfill; z += gridDim.x * 256u) fuse.fill[z] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        for (uint32_t z = g; z < fuse.nzero; z += gridDim.x * 256u) fuse.zero[z] = 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t b = blockIdx.x / (uint32_t)(kScanItems / 256);
+            const uint32_t ps = wsum[0].x + wsum[1].x + wsum[2].x + wsum[3].x;
+            const uint32_t pv = wsum[0].y + wsum[1].y + wsum[2].y + wsum[3].y;
+            if (ps) atomicAdd(&fuse.part[b], (unsigned long long)ps);
+            if (pv) atomicAdd(&fuse.part[fuse.nb + b], (unsigned long long)pv);
+        }
+    }
 }
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
-                             hipEvent_t t1, unsigned long long* zero8, uint32_t* hist) {
+                             hipEvent_t t1, unsigned long long* zero8, uint32_t* hist, const PreFuse& fuse) {
+    if (fuse.part && (hist || fuse.nb != (s.n + kScanItems - 1) / kScanItems))
+        return hipErrorInvalidValue;  // (a two-slab histogram frame keeps scan_reduce)
+    if (s.n == 0 && fuse.part) {  // no grid: the fills as copies
+        if (fuse.nfill && hipMemsetAsync(fuse.fill, 0xFF, (size_t)fuse.nfill * sizeof(uint2), st) != hipSuccess)
+            return hipGetLastError();
+        if (fuse.nzero && hipMemsetAsync(fuse.zero, 0, (size_t)fuse.nzero * 4, st) != hipSuccess)
+            return hipGetLastError();
+    }
     if (s.n == 0) {
         // no dispatch: the timing events still mark the (empty) stage
         if (zero8 && hipMemsetAsync(zero8, 0, 8, st) != hipSuccess) return hipGetLastError();
@@ -392,10 +422,10 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
     switch (sh_degree) {
-    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
-    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
-    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
-    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist); break;
+    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
+    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
+    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
+    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -147,12 +147,15 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
     return base + inc - v;
 }
 
+// src (may be null): the block sums come from there instead (the fused
+// preprocess's, PreFuse) and are cleared after reading.
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
                                                                      uint32_t* __restrict__ npairs, uint64_t cap,
                                                                      uint32_t* __restrict__ hist,
-                                                                     unsigned long long* __restrict__ zero64) {
+                                                                     unsigned long long* __restrict__ zero64,
+                                                                     unsigned long long* __restrict__ src) {
     if (zero64 && threadIdx.x == 0) *zero64 = 0ull;
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
@@ -172,9 +175,15 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         uint64_t v[kPartIpt], s = 0;
 #pragma unroll
         for (int k = 0; k < kPartIpt; ++k) {
-            v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
+            if (src) {
+                v[k] = i0 + k < nb ? (uint64_t)src[i0 + k] : 0u;
+                vis += i0 + k < nb ? (uint64_t)src[nb + i0 + k] : 0u;
+                if (i0 + k < nb) src[i0 + k] = src[nb + i0 + k] = 0ull;  // (read by this lane only)
+            } else {
+                v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
+                vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
+            }
             s += v[k];
-            vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
             if (hist) all += i0 + k < nb ? partials[2 * nb + i0 + k] : 0u;
         }
         uint64_t t;
@@ -510,7 +519,16 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
     // and the duplicate emits nothing either way)
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
                           total, seg_sample, npairs, cap, sel.mode == 1 ? sel.hist : nullptr,
-                          sel.mode == 1 ? sel.zero64 : nullptr);
+                          sel.mode == 1 ? sel.zero64 : nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
+                                      uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
+                                      hipEvent_t done) {
+    if (!part) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
+                          total, seg_sample, npairs, cap, nullptr, nullptr, part);
     return hipGetLastError();
 }
 
