@@ -155,20 +155,16 @@ struct gs_handle {
     // Two-slab frames (gs_options.depth_split): the depth
     // histogram of the cut (filled by the preprocess, cleared by the first
     // slab's scan), the cut per buffer set, the composite's open-tile flags,
-    // and the second slab's own scan / sort scratch: its lists are built on
-    // the composite stream while the side stream builds the next frame's.
-    // The rects are double-buffered with the sets for the same reason.
-    DevBuf ghist, kcut, open4, partials2, npairs2, scratch2, tot2, alt_rlo, alt_rhi;
+    // the second slab's own sort scratch (its lists are sorted on the
+    // composite stream while the side stream builds the next frame's) and,
+    // per set, the number of its pairs the filtered sort kept.
+    DevBuf ghist, kcut, open4, scratch2, tot2;
     bool two_slab_frame = false;
     uint64_t p1_pairs = 0;   // first-slab pairs of the frame in `stats`
     uint32_t pair_cap = 0;   // pair capacity of the set of the last build_bin_lists
     void swap_sets() {
         std::swap(rec, alt_rec);
         std::swap(dkey, alt_dkey);
-        if (alt_rlo.ptr) {
-            std::swap(rlo, alt_rlo);
-            std::swap(rhi, alt_rhi);
-        }
         std::swap(keys, alt_keys);
         std::swap(vals, alt_vals);
         std::swap(tkeys, alt_tkeys);
@@ -184,7 +180,7 @@ struct gs_handle {
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch,
-                          &ghist, &kcut, &open4, &partials2, &npairs2, &scratch2, &tot2, &alt_rlo, &alt_rhi, &ppart})
+                          &ghist, &kcut, &open4, &scratch2, &tot2, &ppart})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -349,10 +345,6 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         }
         GS_HIP(h->kcut.reserve(8));
         GS_HIP(h->tot2.reserve(2 * 64));
-        GS_HIP(h->npairs2.reserve(4));
-        GS_HIP(h->partials2.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
-        GS_HIP(h->alt_rlo.reserve(n * 4));
-        GS_HIP(h->alt_rhi.reserve(n * 4));
     }
     if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
         GS_HIP(hipHostMalloc((void**)&h->host_total, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -630,42 +622,46 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 }
 
 // Two-slab frames, after the first slab's composite on sc:
-// the second slab's pairs (depth keys >= the cut) only into the bins that
-// composite left open, sorted, and composited from the saved state.  Sized
-// by the set's pair capacity (>= both slabs' pairs) and the device-side
-// count, so nothing here waits for the host.
-gs_status second_slab(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo, const uint32_t* rect_hi,
-                      const gs::FrameUniforms& U, const Ownership& own, gs::CompositeArgs ca, hipStream_t sc) {
+// the duplicate wrote the second slab's pairs (depth keys >= the cut) after
+// all of the first's, [P1, P_all) of the pair arrays.  Those of the bins the
+// first composite left open are kept by the first pass of their sort (the
+// others are dropped), sorted by bin, put in depth order per bin and
+// composited from the saved state.  Nothing here waits for the host: the
+// kept count stays on the device.
+gs_status second_slab(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, hipStream_t sc) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    const uint32_t cap = h->pair_cap;
     const int bits = h->last_key_bits;
-    GS_HIP(h->partials2.reserve(((size_t)std::max<uint32_t>(m, 1) + gs::kScanItems - 1) / gs::kScanItems * 16 + 16));
-    GS_HIP(h->scratch2.reserve(gs::radix_sort_scratch_words(cap) * 4));
-    gs::SlabSel sel;
-    sel.mode = 2;
-    sel.dkey = dkey;
-    sel.kcut = h->kcut.as<uint32_t>() + h->set;
-    sel.open = h->open4.as<const uint32_t>();
-    sel.tiles_x = (uint32_t)U.tiles_x;
-    const bool masked = U.cell_mask != 0;
-    GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, masked, h->partials2.as<uint64_t>(),
-                                        h->tot2.as<uint64_t>() + 8 * h->set, nullptr, h->ranges.as<uint2>(), T,
-                                        h->npairs2.as<uint32_t>(), cap, nullptr, 0, sc, nullptr, sel));
+    const uint64_t P1 = h->p1_pairs, Pall = (uint64_t)h->stats.pairs;
+    const uint32_t nfar = (uint32_t)(Pall - P1);
     mark(h, 10, sc);
-    GS_HIP(gs::launch_scan_duplicate(nullptr, rect_lo, rect_hi, h->partials2.as<uint64_t>(), m, (uint32_t)U.tiles_x,
-                                     own.dev, masked, dkey, bits, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                     h->npairs2.as<uint32_t>(), sc, nullptr, gs::PassCounts{}, sel));
     mark(h, 11, sc);
-    bool in_tmp = false;
-    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
-                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap, bits,
-                                 h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(),
-                                 h->npairs2.as<uint32_t>(), false));
+    uint32_t* kept = reinterpret_cast<uint32_t*>(h->tot2.as<uint64_t>() + 8 * h->set);  // (read by gs_last_stats)
+    // the first slab's lists and ranges are free now: its composite is done
+    GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), sc));
+    uint32_t *sk = h->keys.as<uint32_t>(), *sv = h->vals.as<uint32_t>();
+    uint32_t *tk = h->tkeys.as<uint32_t>(), *tv = h->tvals.as<uint32_t>();
+    if (nfar == 0) {
+        GS_HIP(hipMemsetAsync(kept, 0, 4, sc));
+    } else {
+        GS_HIP(h->scratch2.reserve(gs::radix_sort_scratch_words(nfar) * 4));
+        gs::SortFilter flt;
+        flt.open = h->open4.as<const uint32_t>();  // (any of a bin's 4 tiles open)
+        flt.bmask = (1u << bits) - 1u;
+        flt.kept = kept;
+        // input [P1, P_all) of keys / vals; the passes write from offset 0 of
+        // the other arrays first, so no pass writes a range another tile of
+        // the same pass still reads (an odd pass count ends in tkeys)
+        if (gs::make_sort_plan(bits).passes % 2 == 1) {
+            std::swap(sk, tk);
+            std::swap(sv, tv);
+        }
+        bool in_tmp = false;
+        GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>() + P1, h->vals.as<uint32_t>() + P1, sk, sv, tk, tv, nfar,
+                                     bits, h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(), nullptr,
+                                     false, flt));
+        if (in_tmp) return fail(GS_ERR_DEVICE, "second slab: unexpected sort buffer");
+    }
     mark(h, 12, sc);
-    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
-    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
-    uint32_t* tk = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
-    uint32_t* tv = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
     GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), T, sk, sv, tk, tv, bits, nullptr, sc));
     mark(h, 13, sc);
     ca.vals = sv;
@@ -811,7 +807,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         }
         if (two) {
             mark(h, 9, sc);
-            if ((s = second_slab(h, m, dkey, rect_lo, rect_hi, U, own, ca, sc)) != GS_OK) return s;
+            if ((s = second_slab(h, U, ca, sc)) != GS_OK) return s;
         }
         mark(h, 7, sc);
         if (!two) h->stats.pairs = (int64_t)P;  // (two slabs: both slabs' pairs, build_bin_lists)
@@ -912,7 +908,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         const int64_t P1 = (int64_t)h->p1_pairs;
         s.pairs_sorted = P1;
         s.bytes_scan = N * 12 + T * 8;
-        s.bytes_duplicate = N * 12 + P1 * 8;
+        s.bytes_duplicate = N * 12 + Pi * 8;  // (both slabs' pairs)
         s.bytes_sort = P1 * 20 * (int64_t)s.sort_passes;
         s.bytes_depth_sort = P1 * 12;
         h->stats_fixed_bytes += 4 * T * 8;  // the second composite reads its ranges too
@@ -1310,22 +1306,22 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
         h->stats.records_fetched = (int64_t)v;
         h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
         if (h->stats.two_slab) {
-            // the second slab: its pairs (the scan's total), the open tiles
-            // (each resumed from and written back as 16-B pixel states), the cut
+            // the second slab: the pairs its filtered sort kept (of all it
+            // read), the open tiles (each resumed from and written back as
+            // 16-B pixel states), the cut
             unsigned long long open = 0;
-            uint64_t p2 = 0;
-            uint32_t K = 0;
+            uint32_t kept = 0, K = 0;
             GS_HIP(hipMemcpy(&open, h->fetch.as<unsigned long long>() + 2 + h->stats_set, 8, hipMemcpyDeviceToHost));
-            GS_HIP(hipMemcpy(&p2, h->tot2.as<uint64_t>() + 8 * h->stats_set, 8, hipMemcpyDeviceToHost));
+            GS_HIP(hipMemcpy(&kept, h->tot2.as<uint64_t>() + 8 * h->stats_set, 4, hipMemcpyDeviceToHost));
             GS_HIP(hipMemcpy(&K, h->kcut.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
             gs_stats& s = h->stats;
-            const int64_t P2 = (int64_t)p2, N = s.splats, T = s.tiles;
+            const int64_t P2 = (int64_t)kept, Pfar = s.pairs - s.pairs_sorted;
             s.open_tiles = (int64_t)open;
             s.depth_cut = K;
             s.pairs_sorted += P2;
-            s.bytes_scan += N * 12 + T * 8;
-            s.bytes_duplicate += N * 12 + P2 * 8;
-            s.bytes_sort += P2 * 20 * (int64_t)s.sort_passes;
+            // filtered first pass: every second-slab key counted and read
+            // with its value, the kept pairs written; the later passes as usual
+            s.bytes_sort += Pfar * 12 + P2 * 8 + P2 * 20 * (int64_t)(s.sort_passes - 1);
             s.bytes_depth_sort += P2 * 12;
             s.bytes_composite += (int64_t)open * gs::kTileThreads * 32;
         }

@@ -190,35 +190,20 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, co
 // Two-slab frames: the second slab's pairs go only to bins
 // the first slab's composite left open, open[bin] != 0 (a bin's four tile
 // flags as one word).  (splat, bin) pairs of the rect in such bins.
-__device__ __forceinline__ uint32_t rect_open_count(uint32_t lo, uint32_t hi, const RowOwnership& o, bool masked,
-                                                    const uint32_t* __restrict__ open, uint32_t tiles_x) {
-    const BinRect r = bin_rect(lo, hi, masked);
-    if (r.empty) return 0u;
-    uint32_t n = 0;
-    for (uint32_t by = r.by0; by <= r.by1; ++by) {
-        if (o.owner && o.owner[by] != o.rank) continue;
-        for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx)
-            n += (!bin_excluded(r, by, bx) && open[by * tiles_x + bx] != 0u) ? 1u : 0u;
-    }
-    return n;
-}
-
 // The (bin, splat) pairs of one splat, from pair offset `off` on: one per bin
 // of its rect in an owned bin row, minus the bins its ellipse provably misses
-// (row-major bin order), and with `open` set only bins open after the first
-// slab.  key = key_hi | bin id.
+// (row-major bin order).  key = key_hi | bin id.
 // on_pair(offset, bin) is called for every pair written.
 template <typename F>
 __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
                                                uint32_t key_hi, uint32_t val, uint32_t off,
                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                               F&& on_pair, const uint32_t* __restrict__ open = nullptr) {
+                                               F&& on_pair) {
     for (uint32_t by = r.by0; by <= r.by1; ++by) {
         if (!owns_bin_row(by, own)) continue;
         for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx) {
             if (bin_excluded(r, by, bx)) continue;  // the ellipse misses this bin
             const uint32_t bin = by * tiles_x + bx;
-            if (open && open[bin] == 0u) continue;  // every pixel of the bin saturated in the first slab
             keys[off] = key_hi | bin;
             vals[off] = val;
             on_pair(off, bin);
@@ -228,9 +213,8 @@ __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_
 }
 __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
                                                uint32_t key_hi, uint32_t val, uint32_t off,
-                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                               const uint32_t* __restrict__ open = nullptr) {
-    emit_bin_pairs(r, tiles_x, own, key_hi, val, off, keys, vals, [](uint32_t, uint32_t) {}, open);
+                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    emit_bin_pairs(r, tiles_x, own, key_hi, val, off, keys, vals, [](uint32_t, uint32_t) {});
 }
 
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to

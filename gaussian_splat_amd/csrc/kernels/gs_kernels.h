@@ -61,20 +61,20 @@ constexpr int kScanItems = 4096;  // per block
 // Two-slab frames: the frame's pairs in two passes split at a
 // depth-key cut K (S1 order composites ascending dkey, so every pair of the
 // first slab precedes every pair of the second in every bin list).
-//   mode 1: items with dkey < K only; the reduce takes K from the preprocess
-//           histogram (the bucket boundary where the pair share first reaches
-//           `frac`), stores it in *kcut and zeroes the histogram; total[4] =
-//           the pairs of both slabs (partials: 3 * nblocks words)
-//   mode 2: items with dkey >= K, and only into bins with open[bin] != 0
-//           (the first slab's composite left a pixel of the bin unsaturated)
+//   mode 1: the reduce takes K from the preprocess histogram (the bucket
+//           boundary where the pair share first reaches `frac`), stores it in
+//           *kcut and counts the first slab (dkey < K) per block, plus the
+//           pairs of both slabs (partials: 3 * nblocks words); the scan gives
+//           the second slab's pairs offsets after all of the first's (total[4]
+//           = both slabs' pairs) and the duplicate writes both: the first
+//           slab's lists are sorted and composited, then the second slab's
+//           pairs of the bins left open (launch_radix_sort's `open` filter)
 struct SlabSel {
     int mode = 0;
     const uint32_t* dkey = nullptr;  // per item (index order)
     uint32_t* kcut = nullptr;
-    uint32_t* hist = nullptr;        // mode 1
-    const uint32_t* open = nullptr;  // mode 2: per bin
-    uint32_t tiles_x = 0;            // mode 2: bins per row
-    float frac = 0.3f;               // mode 1
+    uint32_t* hist = nullptr;
+    float frac = 0.3f;
     unsigned long long* zero64 = nullptr;  // mode 1 (optional): cleared once the cut is taken (open-tile counter)
 };
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
@@ -156,10 +156,20 @@ uint32_t radix_sort_tile_items();
 // n_dev (optional): the item count is read on the device from *n_dev (<= n;
 // n sizes the grids and the scratch), so the sort can be queued before the
 // host knows it.
+// Filter (a two-slab frame's second slab, SlabSel): only items whose bin
+// (key & bmask) has open[bin] != 0 are counted and sorted, the others are
+// dropped in the first pass, which stores the number kept in *kept (the
+// later passes read it, as n_dev); the result holds the kept items.
+struct SortFilter {
+    const uint32_t* open = nullptr;  // null: every item
+    uint32_t bmask = 0;
+    uint32_t* kept = nullptr;
+};
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
                              bool* result_in_tmp, hipStream_t st, uint2* ranges = nullptr,
-                             const uint32_t* n_dev = nullptr, bool first_counted = false);
+                             const uint32_t* n_dev = nullptr, bool first_counted = false,
+                             const SortFilter& flt = SortFilter{});
 // Same with three value arrays (vals_in[0] may be null: value = index).
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,

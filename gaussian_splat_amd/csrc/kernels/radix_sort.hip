@@ -82,7 +82,7 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
 template <int NV>
 __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                         uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles,
-                                                        const uint32_t* __restrict__ n_dev) {
+                                                        const uint32_t* __restrict__ n_dev, const SortFilter flt) {
     constexpr uint32_t TILE = tile_items(NV);
     if (n_dev) n = *n_dev;  // tiles past it count zeros
     __shared__ uint32_t h[kRsWaves][kSortBins];
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
         for (int k = 0; k < K; ++k) kk[k] = keys[min(t0 + k * kRsThreads + tid, n - 1u)];
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (t0 + k * kRsThreads + tid < n) atomicAdd(&h[wave][(kk[k] >> shift) & mask], 1u);
+            if (t0 + k * kRsThreads + tid < n && (!flt.open || flt.open[kk[k] & flt.bmask]))
+                atomicAdd(&h[wave][(kk[k] >> shift) & mask], 1u);
     }
     __syncthreads();
     if (tid <= mask) {
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
                                                        const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
                                                        uint2* __restrict__ ranges, uint32_t rmask,
-                                                       const uint32_t* __restrict__ n_dev) {
+                                                       const uint32_t* __restrict__ n_dev, const SortFilter flt) {
     constexpr int IPT = ipt_for(NV);
     constexpr uint32_t TILE = tile_items(NV);
     if (n_dev) n = *n_dev;
@@ -222,14 +223,20 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     uint32_t all;
     const uint32_t dstart = block512_exclusive_scan(tid <= mask ? totals[tid] : 0u, tmp, &all);
     if (tid <= mask) gbase[tid] = dstart + C[(size_t)tid * ntiles + tile];
+    if (flt.kept && tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
+    uint32_t keep = 0;  // (filtered: bit k = slot k is kept)
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const uint32_t idx = base + k * 64 + lane;
+        keep |= (idx < n && (!flt.open || flt.open[key[k] & flt.bmask])) ? 1u << k : 0u;
+    }
     // Stable ranks: slot k of every lane in order, a wave's lanes matched by
     // digit (ballots), the wave's running count per digit in LDS.  (A second,
     // independent counting chain over half the slots was measured: the per-bin
     // sort unchanged, this pass slower.)
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-        const uint32_t idx = base + k * 64 + lane;
-        const bool valid = idx < n;
+        const bool valid = (keep >> k) & 1u;
         const uint32_t d = (key[k] >> shift) & mask;
         const uint64_t peers = match_digit<BITS>(d, valid);
         const uint32_t below = mbcnt(peers);
@@ -253,22 +260,19 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     block_lds_sync();
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-        const uint32_t idx = base + k * 64 + lane;
-        if (idx < n) {
+        if ((keep >> k) & 1u) {
             const uint32_t d = (key[k] >> shift) & mask;
             pos[k] += blk_start[d] + wh[wave][d];
         }
     }
     const uint32_t t0 = tile * TILE;
-    const uint32_t cnt = n - t0 < TILE ? n - t0 : TILE;
+    const uint32_t cnt = flt.open ? tot : (n - t0 < TILE ? n - t0 : TILE);  // (the tile's kept items)
     // keys: stage in tile-local sorted order, write out; each slot's global
     // destination (from its staged key's digit) stays in registers for the
     // value arrays
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const uint32_t idx = base + k * 64 + lane;
-        if (idx < n) stage[pos[k]] = key[k];
-    }
+    for (int k = 0; k < IPT; ++k)
+        if ((keep >> k) & 1u) stage[pos[k]] = key[k];
     block_lds_sync();
     uint32_t gdst[IPT];
 #pragma unroll
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t idx = base + k * 64 + lane;
-            if (idx < n) stage[pos[k]] = (NV == 1 || io.vin[a]) ? val[a][k] : idx;
+            if ((keep >> k) & 1u) stage[pos[k]] = (NV == 1 || io.vin[a]) ? val[a][k] : idx;
         }
         block_lds_sync();
 #pragma unroll
@@ -356,7 +360,8 @@ template <int NV>
 static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
-                                  const uint32_t* n_dev, bool first_counted) {
+                                  const uint32_t* n_dev, bool first_counted, const SortFilter& flt = SortFilter{}) {
+    if (flt.open && (first_counted || !flt.kept)) return hipErrorInvalidValue;
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -377,13 +382,17 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     for (int p = 0; p < plan.passes; ++p) {
         io.kout = to_final ? keys : tmp_keys;
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
+        // (the filter drops items in pass 0; later passes sort what it kept)
+        const SortFilter f = p == 0 ? flt : SortFilter{};
         if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
-            rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev);
+            rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev,
+                                                              f);
         rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
         const hipError_t e = launch_pass<NV>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
                                              tiles, p + 1 == plan.passes ? ranges : nullptr,
-                                             bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev);
+                                             bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev, f);
         if (e != hipSuccess) return e;
+        if (p == 0 && flt.open) n_dev = flt.kept;
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;
@@ -394,19 +403,19 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
                              bool* result_in_tmp, hipStream_t st, uint2* ranges, const uint32_t* n_dev,
-                             bool first_counted) {
+                             bool first_counted, const SortFilter& flt) {
     const uint32_t* vi[1] = {vals_in};
     uint32_t* vo[1] = {vals};
     uint32_t* vt[1] = {tmp_vals};
     return radix_sort_impl<1>(keys_in, vi, keys, vo, tmp_keys, vt, n, bits, scratch, result_in_tmp, ranges, st,
-                              n_dev, first_counted);
+                              n_dev, first_counted, flt);
 }
 
 hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* vals_in, uint32_t* keys,
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                               int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
     return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp,
-                              nullptr, st, nullptr, false);
+                              nullptr, st, nullptr, false, SortFilter{});
 }
 
 }  // namespace gs

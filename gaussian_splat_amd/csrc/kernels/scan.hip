@@ -46,16 +46,6 @@ __device__ __forceinline__ uint32_t slab_cut(const SlabSel& sel, uint32_t* tmp4,
     return *kres;
 }
 
-// The item's slab filter: does it take part, and are its bins limited to the open ones?
-__device__ __forceinline__ bool slab_item(const SlabSel& sel, uint32_t dk, uint32_t K) {
-    return sel.mode == 0 || (sel.mode == 1 ? dk < K : dk >= K);
-}
-__device__ __forceinline__ uint32_t item_count(const CountSrc& src, uint32_t lo, uint32_t hi, uint32_t dk, uint32_t K) {
-    if (!slab_item(src.sel, dk, K)) return 0u;
-    return src.sel.mode == 2 ? rect_open_count(lo, hi, src.own, src.masked, src.sel.open, src.sel.tiles_x)
-                             : rect_tile_count(lo, hi, src.own, src.masked);
-}
-
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b];
 // two-slab mode 1 also the pairs of both slabs -> partials[2 nb + b].
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
@@ -81,18 +71,19 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
     if (src.sel.mode == 1) {
         K = slab_cut(src.sel, ctmp, &kres);
         if (blockIdx.x == 0 && threadIdx.x == 0) *src.sel.kcut = K;
-    } else if (src.sel.mode == 2) {
-        K = *src.sel.kcut;
     }
     // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
     uint32_t s = 0, vis = 0, all = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const bool in = base + k * 256 + threadIdx.x < n;
-        const uint32_t c = in ? item_count(src, lo[k], hi[k], dk[k], K) : 0u;
+        // (two-slab mode 1: the first slab's pairs, and the pairs and visible
+        // splats of both slabs)
+        const uint32_t ca = in ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
+        const uint32_t c = src.sel.mode == 1 && dk[k] >= K ? 0u : ca;
         s += c;
-        vis += c > 0;
-        if (src.sel.mode == 1) all += in ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
+        vis += ca > 0;
+        all += ca;
     }
     // the frame's bin ranges start empty and the first sort pass's digit
     // counts at zero (saves two fill dispatches; stored after the loads, which
@@ -169,7 +160,7 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         for (uint32_t i = threadIdx.x; i < (uint32_t)(kCutCopies * kCutBuckets); i += kPartThreads) hist[i] = 0u;
     __shared__ uint64_t tmp[kPartThreads / 64];
     constexpr uint32_t CH = kPartThreads * kPartIpt;
-    uint64_t carry = 0, vis = 0, all = 0;
+    uint64_t carry = 0, vis = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
         const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
         uint64_t v[kPartIpt], s = 0;
@@ -184,7 +175,6 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
                 vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
             }
             s += v[k];
-            if (hist) all += i0 + k < nb ? partials[2 * nb + i0 + k] : 0u;
         }
         uint64_t t;
         uint64_t run = carry + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
@@ -197,12 +187,42 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
     }
     uint64_t vt, at = 0;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
-    if (hist) block1024_exclusive_scan<uint64_t>(all, tmp, &at);
+    if (hist) {
+        // two-slab frames: the second slab's pairs (all - first) of every
+        // block get offsets after all of the first slab's, so one duplicate
+        // writes both slabs' pairs (partials[2 nb + b], in place)
+        uint64_t run_far = carry;
+        for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
+            const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
+            uint64_t f[kPartIpt], s = 0;
+#pragma unroll
+            for (int k = 0; k < kPartIpt; ++k) {
+                // (the first slab's counts are scanned already: its sums are
+                // the differences of consecutive offsets)
+                const uint64_t a = i0 + k < nb ? partials[2 * nb + i0 + k] : 0u;
+                const uint64_t nr = i0 + k < nb ? (i0 + k + 1 < nb ? partials[i0 + k + 1] : carry) - partials[i0 + k]
+                                                : 0u;
+                f[k] = a - nr;
+                s += f[k];
+            }
+            uint64_t t;
+            uint64_t run = run_far + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
+            __syncthreads();  // every lane has read the block sums it rewrites
+#pragma unroll
+            for (int k = 0; k < kPartIpt; ++k) {
+                if (i0 + k < nb) partials[2 * nb + i0 + k] = run;
+                run += f[k];
+            }
+            run_far += t;
+        }
+        at = run_far;
+    }
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
         if (hist) total[4] = at;  // the pairs of both slabs
-        if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
+        // 0: the pair buffers are too small (for both slabs' pairs when split)
+        if (npairs) *npairs = (hist ? at : carry) <= cap ? (uint32_t)carry : 0u;
     }
 }
 
@@ -247,14 +267,21 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
+    __shared__ uint32_t stn[kScanItems + kScanItems / 32];  // (two-slab frames: first-slab offsets)
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    // Two-slab frames (sel mode 1): every item emits, a first-slab item (depth
+    // key below the cut) at the first slab's offsets, the others after all of
+    // them at the second slab's (scan_partials_kernel); only the first slab's
+    // pairs are counted for its sort.
+    const bool split = src.sel.mode == 1;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
     // issued between stores would wait for them
     // (absent arrays read a stand-in, so no load sits in a branch, where its
     // value would be waited for at once)
     const uint64_t part = partials[blockIdx.x];
+    const uint64_t fpart = split ? partials[2 * gridDim.x + blockIdx.x] : 0u;
     const uint32_t K = src.sel.mode ? *src.sel.kcut : 0u;
     const uint32_t* dsrc = dkey ? dkey : src.lo;
     const uint32_t* osrc = order ? order : src.lo;
@@ -276,29 +303,41 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        if (!slab_item(src.sel, dk[k], K)) {  // (two-slab frames: the other slab's items emit nothing)
-            rlo[k] = kEmptyRectLo;
-            rhi[k] = 0u;
-        }
-        st[pad32(i)] = src.sel.mode == 2
-                           ? rect_open_count(rlo[k], rhi[k], src.own, src.masked, src.sel.open, src.sel.tiles_x)
-                           : rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        const uint32_t c = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        st[pad32(i)] = c;
+        if (split) stn[pad32(i)] = dk[k] < K ? c : 0u;
     }
     block_lds_sync();
-    uint32_t v[kDupIpt];
-    uint32_t s = 0;
+    uint32_t v[kDupIpt], vn[kDupIpt];
+    uint32_t s = 0, sn = 0;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         v[k] = st[pad32(tid * kDupIpt + k)];
         s += v[k];
+        vn[k] = split ? stn[pad32(tid * kDupIpt + k)] : 0u;
+        sn += vn[k];
     }
     uint32_t t;
     const uint32_t ex = block_dup_exclusive_scan(s, tmp, &t);  // (ends with a barrier)
-    uint32_t run = (uint32_t)part + ex;
+    if (split) {
+        // the block's first-slab offsets (from part) and second-slab offsets
+        // (from fpart: every pair of an item before it, minus its first-slab ones)
+        const uint32_t exn = block_dup_exclusive_scan(sn, tmp, &t);
+        uint32_t run = ex, runn = exn;
 #pragma unroll
-    for (int k = 0; k < kDupIpt; ++k) {
-        st[pad32(tid * kDupIpt + k)] = run;
-        run += v[k];
+        for (int k = 0; k < kDupIpt; ++k) {
+            const bool first = vn[k] == v[k];  // (an item with no pairs takes either)
+            st[pad32(tid * kDupIpt + k)] = first ? (uint32_t)part + runn : (uint32_t)fpart + (run - runn);
+            run += v[k];
+            runn += vn[k];
+        }
+    } else {
+        uint32_t run = (uint32_t)part + ex;
+#pragma unroll
+        for (int k = 0; k < kDupIpt; ++k) {
+            st[pad32(tid * kDupIpt + k)] = run;
+            run += v[k];
+        }
     }
     block_lds_sync();
     // the first sort pass's digit counts per tile of pc.tile pairs (rts_count
@@ -313,8 +352,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         const uint32_t off = st[pad32(i)];
         const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t val = order ? ord[k] : j;
-        const uint32_t* open = src.sel.mode == 2 ? src.sel.open : nullptr;
-        if (pc.C) {
+        if (pc.C && (!split || dk[k] < K)) {  // (the first sort pass counts the first slab only)
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
             emit_bin_pairs(
                 r, tiles_x, src.own, key_hi, val, off, keys, vals,
@@ -326,10 +364,9 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                     const uint32_t d = bin & pc.mask;
                     if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
                     else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
-                },
-                open);
+                });
         } else {
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals, open);
+            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals);
         }
     }
     if (pc.C) {
@@ -499,7 +536,7 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
                                     uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done,
                                     const SlabSel& sel) {
-    if (sel.mode && (!sel.dkey || !sel.kcut || (sel.mode == 1 && !sel.hist) || (sel.mode == 2 && !sel.open)))
+    if (sel.mode && (sel.mode != 1 || !sel.dkey || !sel.kcut || !sel.hist))
         return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked, sel};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
@@ -540,7 +577,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
-    if (sel.mode && (order || !dkey || sel.dkey != dkey || !sel.kcut || (sel.mode == 2 && !sel.open)))
+    if (sel.mode && (sel.mode != 1 || order || !dkey || sel.dkey != dkey || !sel.kcut))
         return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked, sel};
     if (order) {  // depth order: per-item offsets, then one splat per lane

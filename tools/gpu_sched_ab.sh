@@ -1,13 +1,13 @@
 #!/bin/bash
 # A/B of pipeline schedules: each entry of CFGS is a comma-separated env list
 # ("-" = defaults), e.g. CFGS="- GS_PIPE_SCHED=pc,GS_PRE_GRID=4".  Bench each ROUNDS
-# times interleaved, optional PARITY (pytest -k expr) under the LAST config, then a
+# times interleaved, optional PARITY (pytest -k expr, under PARITY_ENV or the defaults), then a
 # kernel-trace timeline of each config in TL (indices into CFGS).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 read -ra C <<< "${CFGS:--}"
 envof() { [ "$1" = "-" ] && return; echo "$1" | tr ',' ' '; }
 if [ -n "$PARITY" ]; then
-  env $(envof "${C[-1]}") timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "$PARITY" --timeout 200 --timeout-method thread > gpurun_out/sch_parity.log 2>&1
+  env $(envof "${PARITY_ENV:--}") timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "$PARITY" --timeout 200 --timeout-method thread > gpurun_out/sch_parity.log 2>&1
   rc=$?; echo "parity rc=$rc $(tail -1 gpurun_out/sch_parity.log)"; [ $rc -eq 0 ] || exit $rc
 fi
 for r in $(seq ${ROUNDS:-2}); do
