@@ -299,7 +299,9 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 // resolution; with no history the frame goes depth-first.
 // Bin-first needs the depth key to fit above the bin id in a 32-bit pair key.
 // GS_BINNING=depth|bin overrides the option (A/B timing).
-bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
+// nrows: the bin rows this frame composites (multi-GPU ranks own a band of
+// them; the per-bin sort's fixed cost is paid for those only; -1: all).
+bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nrows = -1) {
     static const char* env = std::getenv("GS_BINNING");
     int b = h->opt.binning;
     if (env && std::strcmp(env, "depth") == 0) b = GS_BINNING_DEPTH_FIRST;
@@ -318,7 +320,8 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
     o.n = (int64_t)m;  // items of this frame (the scan that follows reads its P)
     if (!known) return false;
     const double f = o.long_share;
-    const double bin_ps = 6.0 * P * (1.0 - f) + 20.0 * P * f + 4900.0 * T;
+    const double bins = nrows >= 0 ? (double)nrows * U.tiles_x : (double)T;
+    const double bin_ps = 6.0 * P * (1.0 - f) + 20.0 * P * f + 4900.0 * bins;
     return bin_ps < 25.0 * (double)m;
 }
 
@@ -517,10 +520,10 @@ gs_status prepare_lists(gs_handle* h, uint32_t m, bool index_order, const gs::Fr
 
 // Binning order of this frame: decided once, before its preprocess when
 // that fuses the scan (render_frame), else here.
-bool pick_bin_first(gs_handle* h, const gs::FrameUniforms& U, uint32_t m) {
+bool pick_bin_first(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nrows) {
     const int p = h->order_pick;
     h->order_pick = -1;
-    return p >= 0 ? p == 1 : bin_first_order(h, U, m);
+    return p >= 0 ? p == 1 : bin_first_order(h, U, m, nrows);
 }
 
 // Bin lists from m splats visited in `order` (nullptr = index order) with
@@ -737,7 +740,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         h->stats.pairs = (int64_t)P;
         return GS_OK;
     }
-    if (!mlab && pick_bin_first(h, U, m)) {
+    if (!mlab && pick_bin_first(h, U, m, own.dev.owner ? own.nrows : -1)) {
         // Bin-first: bin lists in arrival (index) order with
         // the depth key carried in the pair keys, then each list stably
         // sorted by depth key -> (depth, index) order, the same lists as the
@@ -1478,29 +1481,39 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
 gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, void* send, int64_t send_cap_bytes,
                         int64_t* send_counts, hipStream_t st) {
     const uint32_t n = (uint32_t)h->n;
-    const uint32_t nb = (n + gs::kScanItems - 1) / gs::kScanItems;
+    const uint32_t nb = (n + gs::kShardItems - 1) / gs::kShardItems;
     GS_HIP(h->xmask.reserve((size_t)std::max<uint32_t>(n, 1) * 4));
     GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
     GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
     if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
-    GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
+    // (the scan writes every destination's total; with no splats it does not run)
+    if (nb == 0) GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
     GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, rule, masked,
                                   h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
+    auto pack = [&]() -> hipError_t {
+        return gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
+                                     h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
+                                     static_cast<float4*>(send), st);
+    };
+    // A send buffer that holds every splat once per rank cannot overflow: the
+    // pack is queued before the host waits for the counts (one round trip,
+    // under the pack); a smaller one is checked against them first.
+    const bool roomy = send && send_cap_bytes >= (int64_t)n * h->world * gs_exchange_record_bytes();
+    if (roomy) GS_HIP(pack());
     GS_HIP(hipStreamSynchronize(st));
     int64_t total = 0;
     for (int d = 0; d < h->world; ++d) {
         send_counts[d] = h->host_xtotal[d];
         total += h->host_xtotal[d];
     }
+    if (roomy) return GS_OK;
     if (total * gs_exchange_record_bytes() > send_cap_bytes)
         return fail(GS_ERR_OOM, "exchange: send buffer too small (" +
                                     std::to_string(total * gs_exchange_record_bytes()) + " bytes needed)");
     if (total > 0 && !send) return fail(GS_ERR_INVALID_ARG, "exchange: null send buffer");
-    GS_HIP(gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
-                                 h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
-                                 static_cast<float4*>(send), st));
+    GS_HIP(pack());
     return GS_OK;
 }
 

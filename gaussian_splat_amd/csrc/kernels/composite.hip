@@ -28,6 +28,7 @@ namespace gs {
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
 __device__ unsigned long long g_cc[16];
+__device__ uint32_t g_tile_fetch[1u << 16];  // per tile (bin * 4 + tile of the bin): records fetched
 #define GS_CC(i, v) (void)atomicAdd(&g_cc[i], (unsigned long long)(v))
 #else
 #define GS_CC(i, v) (void)0
@@ -584,6 +585,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     }
 #endif
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
+#ifdef GS_COMPOSITE_COUNTERS
+    if (tid == 0 && MODE == 0 && tile_flag < (1u << 16)) g_tile_fetch[tile_flag] = fetched;
+#endif
     bool keep_state = false;
     if constexpr (PASS == 1) {
         // does any pixel of the tile remain open for the second slab?
@@ -679,6 +683,10 @@ extern "C" int gs_debug_composite_trace(void* out, unsigned n) {  // n uint4 ent
 }
 #endif
 #ifdef GS_COMPOSITE_COUNTERS
+extern "C" int gs_debug_composite_tile_fetch(uint32_t* out, unsigned n) {
+    if (n > (1u << 16)) n = 1u << 16;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_tile_fetch), (size_t)n * 4) != hipSuccess;
+}
 extern "C" int gs_debug_composite_counters(unsigned long long* out) {
     unsigned long long zero[16] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cc), sizeof zero) != hipSuccess) return 1;

@@ -244,7 +244,8 @@ struct DestRule {
 };
 // dest_mask[i]: bit r set iff splat i goes to rank r (a bin row of its rect
 // owned by r, or its depth key in r's slab).
-// counts: [world][nblocks] per-block destination counts (kScanItems splats per block).
+// counts: [world][nblocks] per-block destination counts (kShardItems splats per block).
+constexpr int kShardItems = 1024;
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
                               const DestRule& rule, bool masked,
                               uint32_t* dest_mask, uint32_t* counts, uint32_t nblocks, hipStream_t st);

@@ -24,9 +24,13 @@ __device__ __forceinline__ uint32_t xrect_pack(uint32_t xy, uint32_t key8) {
 }
 __device__ __forceinline__ uint32_t xrect_unpack(uint32_t p) { return (p & 0xFFFu) | (((p >> 12) & 0xFFFu) << 16); }
 
+// kShardItems splats per 256-lane workgroup: 4 rounds of 64 per wave, so a
+// rank's shard spreads over many workgroups (750k splats: 733; blocks of
+// 4096 left 183 workgroups on 256 CUs, pack 75 us)
 constexpr int kShWaves = 4;
-constexpr int kShIpt = kScanItems / 256;  // 16 rounds of 64 per wave
+constexpr int kShIpt = kShardItems / 256;
 constexpr int kShWaveItems = 64 * kShIpt;
+static_assert(kShIpt * 256 == kShardItems, "shard block");
 
 // Ranks owning any of the bin rows ty0..ty1.
 __device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const uint8_t* __restrict__ owner) {
@@ -49,7 +53,7 @@ __global__ __launch_bounds__(256) void shard_count_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ counts, uint32_t nblocks) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t base = blockIdx.x * kScanItems + wave * kShWaveItems;
+    const uint32_t base = blockIdx.x * kShardItems + wave * kShWaveItems;
     uint32_t cnt = 0;  // lane d holds this wave's count for destination d
     for (int k = 0; k < kShIpt; ++k) {
         uint32_t i = base + k * 64 + lane;
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
     __shared__ uint32_t wc[kShWaves][kMaxWorld];   // per-wave counts -> per-wave offsets
     __shared__ uint32_t base_d[kMaxWorld];         // this block's start in destination d
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t base = blockIdx.x * kScanItems + wave * kShWaveItems;
+    const uint32_t base = blockIdx.x * kShardItems + wave * kShWaveItems;
     uint32_t cnt = 0;
     for (int k = 0; k < kShIpt; ++k) {
         uint32_t i = base + k * 64 + lane;

@@ -76,3 +76,12 @@ print(f"per wave walk steps: now {c[3] / waves:.1f}  4x4 groups {c[10] / waves:.
 print(f"per wave, summed per-batch maxima: exact 4x4 groups {c[1] / waves:.1f}  per-lane {c[2] / waves:.1f}  "
       f"rect 4x4 groups {c[14] / waves:.1f}  ellipse 4x4 groups {c[15] / waves:.1f}")
 print(f"per wg: batches {c[5] / wg:.2f}  list {c[6] / wg:.0f}  batches if no exit {c[6] / wg / 256:.2f}")
+tf = lib().gs_debug_composite_tile_fetch
+tf.argtypes = [C.POINTER(C.c_uint32), C.c_uint]
+nt = int(st["tiles"]) * 4
+arr = (C.c_uint32 * nt)()
+tf(arr, nt)
+import numpy as np  # noqa: E402
+f = np.frombuffer(arr, dtype=np.uint32).reshape(-1, 4).astype(np.int64)
+print(f"records fetched: per tile (sum) {f.sum()}  per bin if a bin's tiles shared one fetch (sum of max) "
+      f"{f.max(axis=1).sum()}  ratio {f.max(axis=1).sum() / max(f.sum(), 1):.3f}")
