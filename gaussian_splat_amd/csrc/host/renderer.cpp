@@ -334,7 +334,7 @@ gs_status check_ready(gs_handle* h) {
 
 gs_status ensure_frame_scratch(gs_handle* h) {
     const size_t n = (size_t)std::max<int64_t>(h->n, 1);
-    GS_HIP(h->rec.reserve(n * sizeof(gs::Record3)));
+    GS_HIP(h->rec.reserve(n * gs::kRecFloat4 * 16));
     GS_HIP(h->dkey.reserve(n * 4));
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
@@ -1264,7 +1264,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
                                  kernel_event(h, 1), fetch_counter(h), hist, fuse));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
-                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), 3, U, compact,
+                                h->rhi.as<uint32_t>(), h->rec.as<float4>(), gs::kRecFloat4, U, compact,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
                                 bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st,
                                 hist != nullptr)) != GS_OK)
@@ -1363,7 +1363,8 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
     GS_HIP(hipStreamSynchronize(st));
     const size_t n = (size_t)h->n;
     if (records) {
-        GS_HIP(hipMemcpy(records, h->rec.ptr, n * sizeof(gs::Record3), hipMemcpyDeviceToHost));
+        GS_HIP(hipMemcpy2D(records, sizeof(gs::Record3), h->rec.ptr, (size_t)gs::kRecFloat4 * 16, sizeof(gs::Record3),
+                           n, hipMemcpyDeviceToHost));
         if (U.cell_mask) {  // the cell-exclusion mask is internal: export the reference record
             uint32_t* w = static_cast<uint32_t*>(records);
             for (size_t i = 0; i < n; ++i) {

@@ -79,6 +79,14 @@ struct SceneDev {
 struct Record3 {
     float4 a, b, c;
 };
+// float4 slots per record in the frame's record array: 3, or 4 (64-B aligned
+// slots, the 4th zero: a record then lies in one half of a 128-B line;
+// A/B knob GS_REC_F4)
+#ifndef GS_REC_F4
+#define GS_REC_F4 3
+#endif
+constexpr int kRecFloat4 = GS_REC_F4;
+static_assert(kRecFloat4 == 3 || kRecFloat4 == 4, "record slot");
 
 __device__ __forceinline__ float xform_row(const float* m, int r, float x, float y, float z) {
     return __builtin_fmaf(m[8 + r], z, __builtin_fmaf(m[4 + r], y, __builtin_fmaf(m[0 + r], x, m[12 + r])));

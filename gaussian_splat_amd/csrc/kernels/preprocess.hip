@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                     ShCoef<DEG> coef;
                     if constexpr (DEG > 0) sh_load<DEG>(s, i, coef);
                     sh_color<DEG>(coef, px, py, pz, U.campos, a2.w, a3.x, a3.y, cr, cg, cbl);
-                    float4* o = rec + 3 * (size_t)i;
+                    float4* o = rec + kRecFloat4 * (size_t)i;
                     const float4 ra = make_float4(cx, cy, e1x * k1, e1y * k1);
                     const float4 rb = make_float4(e2x * k2, e2y * k2, a0.w, cr);
                     // 8x8 cells of the rect the ellipse provably misses (the
@@ -346,6 +346,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
 #endif
                     o[0] = ra;
                     o[1] = rb;
+                    if constexpr (kRecFloat4 == 4) o[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // (whole 64-B slot)
                     o[2] = make_float4(cg, cbl,
                                        __uint_as_float(rect_with_mask(x0 | (y0 << 16), excl & 0xFu, (excl >> 4) & 0xFu)),
                                        __uint_as_float(rect_with_mask(x1 | (y1 << 16), (excl >> 8) & 0xFu, excl >> 12)));

@@ -234,7 +234,10 @@ __device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }  
 // straight from its rect in registers (striped, one splat per lane per
 // round: neighbouring lanes write neighbouring pair runs).  The rects are
 // read once here and the offsets never leave LDS.
-constexpr int kDupThreads = 1024;                    // 16 waves: many waves to hide the pair stores
+#ifndef GS_DUP_THREADS  // A/B knob
+#define GS_DUP_THREADS 1024
+#endif
+constexpr int kDupThreads = GS_DUP_THREADS;          // 16 waves: many waves to hide the pair stores
 constexpr int kDupIpt = kScanItems / kDupThreads;    // 4 items per lane
 
 // Exclusive scan over a kDupThreads-lane workgroup (LDS-only barriers).
@@ -256,6 +259,7 @@ __device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_
     return base + inc - v;
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
                                                                      const uint64_t* __restrict__ partials,
                                                                      const uint32_t* __restrict__ order,
@@ -267,14 +271,14 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
-    __shared__ uint32_t stn[kScanItems + kScanItems / 32];  // (two-slab frames: first-slab offsets)
+    __shared__ uint32_t stn[SPLIT ? kScanItems + kScanItems / 32 : 1];  // (two-slab frames: first-slab offsets)
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
     // Two-slab frames (sel mode 1): every item emits, a first-slab item (depth
     // key below the cut) at the first slab's offsets, the others after all of
     // them at the second slab's (scan_partials_kernel); only the first slab's
     // pairs are counted for its sort.
-    const bool split = src.sel.mode == 1;
+    constexpr bool split = SPLIT;  // (src.sel.mode == 1)
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
     // issued between stores would wait for them
@@ -591,8 +595,12 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
             duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
         return hipGetLastError();
     }
-    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
-                                                      npairs, pc);
+    if (sel.mode == 1)
+        scan_duplicate_kernel<true><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
+                                                                vals, npairs, pc);
+    else
+        scan_duplicate_kernel<false><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
+                                                                 keys, vals, npairs, pc);
     return hipGetLastError();
 }
 

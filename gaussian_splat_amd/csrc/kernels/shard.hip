@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
             uint32_t run = wc[wave][d];
             if (bit) {
                 uint32_t pos = base_d[d] + run + mbcnt(b);
-                const float4* src = rec + 3 * (size_t)i;
+                const float4* src = rec + kRecFloat4 * (size_t)i;
                 float4* dst = send + (size_t)kXRecFloat4 * pos;
                 const float4 c = src[2];
                 const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w), dk = dkey[i];

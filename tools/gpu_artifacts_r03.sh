@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-3 artifacts: GPU tests, driver-default bench, profiled unpipelined bench + rocprofv3 kernel
+# stats of the same command, PMC summary, other BASELINE configs, heavy-tail scene, 2-rank rehearsal.
+# Every GPU step has its own time limit; the script stops at the first failure.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
+O=gpurun_out/art3; rm -rf $O; mkdir -p $O
+step() { name=$1; shift; echo "== $name"; "$@"; rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+for s in ${STEPS:-tests bench prof pmc configs heavy ranks timeline}; do case $s in
+tests) step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
+       tail -1 $O/pytest_gpu.log ;;
+bench) step bench bash -c "timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err"; cat $O/bench_default.json ;;
+prof)  step prof bash -c "timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
+         python bench.py --frames-in-flight 1 --pmc 0 --cpu-baseline 0 > $O/bench_profiled.json 2> $O/bench_profiled.err"
+       cp $(find $O/prof -name "*kernel_stats.csv" | head -1) $O/bench_profiled_kernel_stats.csv; cat $O/bench_profiled.json ;;
+pmc)   B="python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --pmc 0 --no-stage-timing --frames-in-flight 1"
+       step sq1 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d $O/pmc/sq1 -o run --output-format csv -- $B > $O/pmc_sq1.log 2>&1
+       step sq2 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d $O/pmc/sq2 -o run --output-format csv -- $B > $O/pmc_sq2.log 2>&1
+       step fetch timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- $B > $O/pmc_fetch.log 2>&1
+       step write timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- $B > $O/pmc_write.log 2>&1
+       python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A1 "composite_kernel<0\|preprocess_kernel<3>" $O/pmc_summary.txt ;;
+configs) for c in 1m 4k 50m; do
+         step cfg_$c bash -c "timeout -k 10 600 python bench.py --config $c --steps 30 --cpu-baseline 0 > $O/bench_$c.json 2> $O/bench_$c.err"
+         python -c "import json;d=json.load(open('$O/bench_$c.json'));print('$c', d['ms_per_step'], d['value'], d['config']['binning'], d['roofline']['kernels']['composite']['ms'])"; done ;;
+heavy) step heavy bash -c "timeout -k 10 600 python bench.py --profile heavy --steps 50 --cpu-baseline 0 > $O/bench_heavy.json 2> $O/bench_heavy.err"
+       python -c "import json;d=json.load(open('$O/bench_heavy.json'));print('heavy', d['ms_per_step'], d['value'], d['config']['pairs'])" ;;
+ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
+       cat $O/rehearsal_2rank_gloo.json ;;
+timeline) step timeline bash -c "rm -rf $O/tl && timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --pmc 0 --no-stage-timing > $O/tl.log 2>&1"
+       python tools/trace_timeline.py $(find $O/tl -name "*kernel_trace.csv" | head -1) 4 > $O/timeline_fif2.txt; tail -3 $O/timeline_fif2.txt ;;
+esac; done
