@@ -379,6 +379,25 @@ def radix_sort_pairs(keys, vals, bits: int, stream=None):
     return keys, vals
 
 
+def radix_sort_pairs_filtered(keys, vals, bits: int, open_bins, stream=None):
+    """Stable sort keeping the pairs whose key bits [0, bits) index a nonzero
+    word of open_bins (a CUDA int32 tensor of 2^bits words); returns new
+    (keys, vals) tensors of the kept pairs."""
+    import torch
+
+    n = keys.numel()
+    ko, vo, tk, tv = (torch.empty_like(keys) for _ in range(4))
+    kept = C.c_int64(0)
+    if stream is None:
+        stream = torch.cuda.current_stream(keys.device).cuda_stream
+    check(lib().gs_radix_sort_pairs_filtered(C.c_void_p(keys.data_ptr()), C.c_void_p(vals.data_ptr()),
+                                             C.c_void_p(ko.data_ptr()), C.c_void_p(vo.data_ptr()),
+                                             C.c_void_p(tk.data_ptr()), C.c_void_p(tv.data_ptr()), n, int(bits),
+                                             C.c_void_p(open_bins.data_ptr()), C.byref(kept), C.c_void_p(stream)),
+          "gs_radix_sort_pairs_filtered")
+    return ko[: kept.value], vo[: kept.value]
+
+
 SCHEMES = {"rows": 0, "slabs": 1, "bands": 2}  # gs_scheme
 TRANSPORTS = {"auto": 0, "rccl": 1, "copy": 2}  # gs_transport
 

@@ -1408,6 +1408,36 @@ gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int
     return GS_OK;
 }
 
+gs_status gs_radix_sort_pairs_filtered(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
+                                       uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, int64_t n, int32_t bits,
+                                       const uint32_t* open, int64_t* kept, void* stream) {
+    if (n < 0 || n >= (int64_t)UINT32_MAX || bits < 1 || bits > 16 || !open || !kept ||
+        (n > 0 && (!keys_in || !vals_in || !keys || !vals || !tmp_keys || !tmp_vals)))
+        return fail(GS_ERR_INVALID_ARG, "gs_radix_sort_pairs_filtered: bad arguments");
+    *kept = 0;
+    if (n == 0) return GS_OK;
+    if (keys_in == keys || keys_in == tmp_keys || vals_in == vals || vals_in == tmp_vals)
+        return fail(GS_ERR_INVALID_ARG, "gs_radix_sort_pairs_filtered: the input aliases an output");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint32_t* scratch = nullptr;
+    GS_HIP(hipMalloc(&scratch, (gs::radix_sort_scratch_words((uint32_t)n) + 1) * 4));
+    gs::SortFilter flt;
+    flt.open = open;
+    flt.bmask = (1u << bits) - 1u;
+    flt.kept = scratch + gs::radix_sort_scratch_words((uint32_t)n);
+    bool in_tmp = false;
+    hipError_t e = gs::launch_radix_sort(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, (uint32_t)n, bits, scratch,
+                                         &in_tmp, st, nullptr, nullptr, false, flt);
+    uint32_t k = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&k, flt.kept, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(scratch);
+    GS_HIP(e);
+    if (in_tmp) return fail(GS_ERR_DEVICE, "gs_radix_sort_pairs_filtered: unexpected sort buffer");
+    *kept = k;
+    return GS_OK;
+}
+
 gs_status gs_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, int64_t n,
                               int32_t bits, void* stream) {
     if (n < 0 || n >= (int64_t)UINT32_MAX || bits < 0 || bits > 32 || (n > 0 && (!keys || !vals || !tmp_keys || !tmp_vals)))

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 7
+#define GSPLAT_ABI_VERSION 8
 
 typedef enum {
     GS_OK = 0,
@@ -198,6 +198,14 @@ gs_status gs_sorted_pairs_host(gs_handle *h, uint32_t *keys, uint32_t *vals, int
  * tmp_keys/tmp_vals: n elements each; result ends in keys/vals. */
 gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals,
                               int64_t n, int32_t bits, void *hip_stream);
+/* The same sort keeping only the pairs whose key bits [0, bits) index a
+ * nonzero word of `open` (device, 2^bits words; bits 1..16): the two-slab
+ * frames' second-slab sort.  Reads keys_in/vals_in (n, not
+ * aliasing the other arrays), leaves the *kept pairs, stably sorted, in
+ * keys/vals; tmp_*: n elements each.  Synchronous. */
+gs_status gs_radix_sort_pairs_filtered(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys,
+                                       uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals, int64_t n,
+                                       int32_t bits, const uint32_t *open, int64_t *kept, void *hip_stream);
 
 /* ---- multi-GPU: bin-row ownership across ranks ----- */
 /* No reference counterpart (the reference is single-GPU Metal).
