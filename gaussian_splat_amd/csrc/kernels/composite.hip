@@ -20,8 +20,6 @@
 // one XCD and share the bin's list through its L2.
 #include <hip/hip_ext.h>
 
-#include <cstdlib>
-
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
@@ -626,218 +624,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     }
 }
 
-// Finer footprints: the same tiles, staged
-// records and per-pixel operations as composite_kernel, but every wave's 64
-// lanes are four 4x4 pixel groups (lane >> 4), and each group walks its own
-// list: the records whose conservative rect reaches its 4x4 block and whose
-// 8x8 cell the ellipse does not provably miss.  A wave step composites up to
-// four records (one per group); a group stops at the end of its list or once
-// its 16 pixels are saturated.  Per pixel the covering records are visited
-// in list (S1) order exactly as before, and a skipped record adds an exact
-// zero, so the image is bit-identical.  Tile and live-50 rules, fp32 or BGRA8
-// output, compact bands; no cap, depth slabs or two-slab passes (those take
-// composite_kernel).
-template <int MODE>
-__global__ __launch_bounds__(256, 8) void composite_g4_kernel(CompositeArgs a, uint32_t nwg) {
-    static_assert(MODE == 0 || MODE == 1, "tile / live50 rules");
-    __shared__ StagedRec srec[kTileThreads];
-    __shared__ uint8_t wl4[4][4][kTileThreads];  // per wave and group: record indices of the batch
-    __shared__ uint16_t sbm[kTileThreads];       // per staged record: the tile's 4x4 blocks it may reach
-    __shared__ uint32_t sopen[4];
-
-    const uint32_t orig = blockIdx.x;
-    const uint32_t full = nwg & ~31u;
-    const uint32_t kk = orig >> 3;
-    const uint32_t wg = orig < full ? 32u * (kk >> 2) + 4u * (orig & 7u) + (kk & 3u) : orig;  // (composite_kernel)
-    const uint32_t per_row = 4u * (uint32_t)a.tiles_x;
-    const int owned_row = (int)(wg / per_row);
-    const uint32_t k4 = wg - (uint32_t)owned_row * per_row;
-    const int bx = (int)(k4 >> 2);
-    const int by = a.rows ? (int)a.rows[owned_row] : owned_row;
-    const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
-    const int width = a.width, height = a.height;
-    const int tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t lane = tid & 63u, grp = lane >> 4;
-    // pixel: quadrant of the wave, 4x4 block of the group, position in the block
-    const uint32_t tx0 = (uint32_t)(tx * kTile), ty0 = (uint32_t)(ty * kTile);
-    const uint32_t lxi = (wave & 1u) * 8u + (grp & 1u) * 4u + (lane & 3u);
-    const uint32_t lyi = (wave >> 1) * 8u + (grp >> 1) * 4u + ((lane >> 2) & 3u);
-    // this group's block in the tile's 4x4 grid of 4x4 blocks
-    const uint32_t blk = (lyi >> 2) * 4u + (lxi >> 2);
-    const int px = (int)(tx0 + lxi), py = (int)(ty0 + lyi);
-    const bool inside = px < width && py < height;
-    const float lx = (float)lxi + 0.5f, ly = (float)lyi + 0.5f;
-    const float ftx0 = (float)tx0, fty0 = (float)ty0;
-
-    uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
-    if (tx0 >= (uint32_t)width || ty0 >= (uint32_t)height) rg.y = rg.x;
-    float T = inside ? 1.0f : 0.0f;
-    float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-    const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
-    auto finished = [&]() -> bool {
-        if constexpr (MODE == 0) return T <= kTSat;
-        else return T < kTMin;
-    };
-    auto body = [&](const StagedRec& r, bool have) {
-        const float u = __builtin_fmaf(r.a.z, lx, __builtin_fmaf(r.a.w, ly, r.a.x));
-        const float v = __builtin_fmaf(r.b.x, lx, __builtin_fmaf(r.b.y, ly, r.a.y));
-        const float qq = __builtin_fmaf(v, v, u * u);
-        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= kBoxS && qq <= kQMaxS;
-        if (have && covered && !finished()) {
-            const float alpha = r.b.z * gs_gauss2(qq);
-            if constexpr (MODE == 0) {
-                const float sa = alpha * T;
-                C0 = __builtin_fmaf(r.b.w, sa, C0);
-                C1 = __builtin_fmaf(r.c.x, sa, C1);
-                C2 = __builtin_fmaf(r.c.y, sa, C2);
-                T = T - sa;
-            } else {
-                C0 = __builtin_fmaf(r.b.w, T, C0);
-                C1 = __builtin_fmaf(r.c.x, T, C1);
-                C2 = __builtin_fmaf(r.c.y, T, C2);
-                T = T * (1.0f - alpha);
-            }
-        }
-    };
-
-    // coalesced gathers and the one-batch-ahead pipeline of composite_kernel
-    const uint32_t last = rg.y > rg.x ? rg.y - 1u : rg.x;
-    uint32_t ck[3], cp[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const uint32_t c = lane + 64u * (uint32_t)i;
-        ck[i] = c / 3u;
-        cp[i] = c - 3u * ck[i];
-    }
-    float4 rc[3] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f),
-                    make_float4(0.f, 0.f, 0.f, 0.f)};
-    uint32_t id_cur = 0, id_next = 0;
-    auto gather = [&](uint32_t own_id) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const uint32_t idk = (uint32_t)__shfl((int)own_id, (int)ck[i], 64);
-            rc[i] = a.rec[(size_t)a.rec_stride * idk + cp[i]];
-        }
-    };
-    if (rg.y > rg.x) {
-        const uint32_t j = rg.x + tid;
-        id_cur = a.vals[j < last ? j : last];
-        gather(id_cur);
-        id_next = a.vals[j + kTileThreads < last ? j + kTileThreads : last];
-    }
-    const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;
-    uint32_t fetched = len < (uint32_t)kTileThreads ? len : (uint32_t)kTileThreads;
-    // this wave's four blocks (group g: bit of the tile's 4x4 block grid)
-    uint32_t gbit[4];
-#pragma unroll
-    for (uint32_t g = 0; g < 4; ++g) gbit[g] = ((wave >> 1) * 2u + (g >> 1)) * 4u + (wave & 1u) * 2u + (g & 1u);
-    const uint64_t gmask = 0xFFFFull << (16u * grp);
-    for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
-        if (b != rg.x) {
-            const bool open = __ballot(!finished()) != 0;
-            if (lane == 0) sopen[wave] = open ? 1u : 0u;
-            block_lds_sync();
-            const uint4 o = *reinterpret_cast<const uint4*>(sopen);
-            if ((o.x | o.y | o.z | o.w) == 0u) break;
-        }
-        if (rg.y - b > (uint32_t)kTileThreads) {
-            const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
-            fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-            (cp[i] == 0 ? srec[64u * wave + ck[i]].a : cp[i] == 1 ? srec[64u * wave + ck[i]].b
-                                                                   : srec[64u * wave + ck[i]].c) = rc[i];
-        wave_lds_sync();
-        if (b + tid < rg.y) {
-            StagedRec& st = srec[tid];
-            const float4 r0 = st.a, r1 = st.b, r2 = st.c;
-            const float ax = r0.z * kConicScale, ay = r0.w * kConicScale;
-            const float bxs = r1.x * kConicScale, bys = r1.y * kConicScale;
-            const float ex = ftx0 - r0.x, ey = r0.y - fty0;
-            st.a = make_float4(__builtin_fmaf(ax, ex, ay * ey), __builtin_fmaf(bxs, ex, bys * ey), ax, -ay);
-            st.b = make_float4(bxs, -bys, r1.z, r1.w);
-            st.c = make_float4(r2.x, r2.y, 0.0f, 0.0f);
-            // the tile's 4x4 blocks of 4x4 px the record's rect reaches, minus
-            // the 8x8 cells its ellipse provably misses
-            const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
-            const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
-            const int x0 = (int)(lo & 0xFFFFu) - (int)tx0, x1 = (int)(hi & 0xFFFFu) - (int)tx0;
-            const int y0 = (int)(lo >> 16) - (int)ty0, y1 = (int)(hi >> 16) - (int)ty0;
-            uint32_t cm4 = 0, rm4 = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                cm4 |= (x1 >= 4 * c && x0 <= 4 * c + 3) ? 1u << c : 0u;
-                rm4 |= (y1 >= 4 * c && y0 <= 4 * c + 3) ? 1u << c : 0u;
-            }
-            uint32_t bm = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bm |= ((rm4 >> r) & 1u) ? cm4 << (4 * r) : 0u;
-            if (a.cell_mask && bm) {
-                const uint32_t cmask = rect_cell_mask(wlo, whi);
-                const uint32_t gx0 = (uint32_t)((int)(lo & 0xFFFFu)) >> 3, gy0 = (lo >> 16) >> 3;
-#pragma unroll
-                for (uint32_t w = 0; w < 4; ++w) {  // the tile's 8x8 cells (= the waves' quadrants)
-                    const uint32_t dcx = (tx0 >> 3) + (w & 1u) - gx0, dcy = (ty0 >> 3) + (w >> 1) - gy0;
-                    if (dcx < 4u && dcy < 4u && ((cmask >> (dcy * 4u + dcx)) & 1u))
-                        bm &= ~(0x33u << ((w >> 1) * 8u + (w & 1u) * 2u));
-                }
-            }
-            sbm[tid] = (uint16_t)bm;
-        }
-        __syncthreads();
-        {
-            const uint32_t j = b + 2u * kTileThreads + tid;
-            id_cur = id_next;
-            gather(id_cur);
-            id_next = a.vals[j < last ? j : last];
-        }
-        const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
-        // per group, the batch records reaching its block (index order kept)
-        uint32_t n4[4] = {0u, 0u, 0u, 0u};
-        if (__ballot(!finished()) != 0) {
-            for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
-                const uint32_t k = k0 + lane;
-                const uint32_t m = k < cnt_b ? sbm[k] : 0u;
-#pragma unroll
-                for (uint32_t g = 0; g < 4; ++g) {
-                    const bool hit = (m >> gbit[g]) & 1u;
-                    const uint64_t bl = __ballot(hit);
-                    if (hit) wl4[wave][g][n4[g] + mbcnt(bl)] = (uint8_t)k;
-                    n4[g] += (uint32_t)__popcll(bl);
-                }
-            }
-        }
-        wave_lds_sync();
-        const uint32_t my_n = grp == 0 ? n4[0] : grp == 1 ? n4[1] : grp == 2 ? n4[2] : n4[3];
-        const uint32_t n_max = max(max(n4[0], n4[1]), max(n4[2], n4[3]));
-        const uint8_t* wl = wl4[wave][grp];
-        // two steps per iteration, both records read before either body; the
-        // next pair of indices read one iteration ahead
-        uint32_t kA = wl[0], kB = wl[1];
-        for (uint32_t i = 0; i < n_max; i += 2) {
-            // a group whose 16 pixels are saturated takes no more records
-            const bool gopen = (__ballot(!finished()) & gmask) != 0;
-            const bool hA = gopen && i < my_n, hB = gopen && i + 1 < my_n;
-            if (__ballot(hA) == 0) break;
-            const StagedRec rA = srec[kA], rB = srec[kB];
-            const uint32_t i2 = i + 2u < (uint32_t)kTileThreads - 1u ? i + 2u : (uint32_t)kTileThreads - 2u;
-            kA = wl[i2];
-            kB = wl[i2 + 1u];
-            body(rA, hA);
-            body(rB, hB);
-        }
-    }
-    if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
-    if (!inside) return;
-    const float4 o = make_float4(C0, C1, C2, 1.0f - T);
-    if (a.out_bgra8)
-        a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
-    else
-        a.out[(size_t)orow * width + px] = o;
-}
-
 template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
@@ -872,21 +658,6 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
         return hipErrorInvalidValue;
     }
     if (mode == 2) return cap || !a.dkey ? hipErrorInvalidValue : launch_mode<3, false>(a, st, t0, t1);  // MLAB
-    static const char* g4_env = std::getenv("GS_COMPOSITE_G4");  // 1: four 4x4 groups per wave (A/B)
-    if (!cap && g4_env && g4_env[0] == '1') {
-        if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
-        const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
-        if (nwg == 0) {
-            if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
-            if (t1 && hipEventRecord(t1, st) != hipSuccess) return hipGetLastError();
-            return hipSuccess;
-        }
-        if (mode == 0)
-            hipExtLaunchKernelGGL(composite_g4_kernel<0>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a, nwg);
-        else
-            hipExtLaunchKernelGGL(composite_g4_kernel<1>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a, nwg);
-        return hipGetLastError();
-    }
     if (mode == 0) return cap ? launch_mode<0, true>(a, st, t0, t1) : launch_mode<0, false>(a, st, t0, t1);
     return cap ? launch_mode<1, true>(a, st, t0, t1) : launch_mode<1, false>(a, st, t0, t1);
 }
