@@ -133,9 +133,6 @@ struct gs_handle {
         gs::PassCounts pc;
     } fused_prep;
     DevBuf ppart;
-    DevBuf look[2], look_dbg;  // look-back probe (GS_LOOKBACK)
-    size_t look_words = 0;
-    int look_parity = 0;
     size_t ppart_words = 0;
     bool ppart_dirty = false;  // a fused preprocess ran without its scan (error path): clear first
     bool fused_last = false;   // the frame in `stats` scanned fused block sums
@@ -1260,23 +1257,6 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
             h->fused_prep.ok = true;
             h->ppart_dirty = true;  // (until its scan is queued)
-            static const char* lb_env = std::getenv("GS_LOOKBACK");  // probe: 1 on, 2 on + checked
-            if (lb_env && lb_env[0] != '0') {
-                const size_t nwg = ((size_t)h->n + 255) / 256;
-                if (h->look_words != nwg) {
-                    for (DevBuf* b : {&h->look[0], &h->look[1]}) {
-                        GS_HIP(b->reserve(nwg * 8));
-                        GS_HIP(hipMemset(b->ptr, 0, nwg * 8));
-                    }
-                    GS_HIP(h->look_dbg.reserve((nwg + 3) * 4));
-                    GS_HIP(hipMemset(h->look_dbg.ptr, 0, (nwg + 3) * 4));
-                    h->look_words = nwg;
-                }
-                fuse.look = h->look[h->look_parity].as<unsigned long long>();
-                fuse.look_next = h->look[h->look_parity ^ 1].as<unsigned long long>();
-                fuse.dbg = lb_env[0] == '2' ? h->look_dbg.as<uint32_t>() : nullptr;
-                h->look_parity ^= 1;
-            }
         }
     }
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
@@ -1290,18 +1270,6 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
                                 hist != nullptr)) != GS_OK)
         return s;
     GS_HIP(hipEventRecord(h->set_free[h->set], st));  // this set's last reader
-    if (fuse.dbg) {  // look-back probe check: offsets against the scan's
-        GS_HIP(hipDeviceSynchronize());
-        const uint32_t nb = fuse.nb;
-        std::vector<uint32_t> d(h->look_words + 3);
-        std::vector<uint64_t> part(nb);
-        GS_HIP(hipMemcpy(d.data(), h->look_dbg.ptr, d.size() * 4, hipMemcpyDeviceToHost));
-        GS_HIP(hipMemcpy(part.data(), h->partials.ptr, nb * 8, hipMemcpyDeviceToHost));
-        size_t bad = 0;
-        for (uint32_t b = 0; b < nb; ++b) bad += (uint64_t)d[3 + (size_t)b * (gs::kScanItems / 256)] != part[b];
-        std::fprintf(stderr, "lookback: spin-limit %u, P %u/%llu, visible %u/%lld, block offsets wrong %zu of %u\n",
-                     d[0], d[1], (unsigned long long)h->host_total[0], d[2], (long long)h->host_total[1], bad, nb);
-    }
     const uint64_t P = (uint64_t)h->stats.pairs;
     if (!out_is_device) {
         GS_HIP(hipMemcpyAsync(out_user, out, bytes, hipMemcpyDeviceToHost, st));

@@ -37,12 +37,6 @@ struct PreFuse {
     uint32_t nfill = 0;
     uint32_t* zero = nullptr;
     uint32_t nzero = 0;
-    // decoupled look-back over the workgroups' (visible, pairs) counts
-    // (probe): this frame's status words (zeroed), the next frame's to zero,
-    // dbg[0] = spin-limit hits, dbg[1..2] = totals, dbg[3 + wg] = offsets
-    unsigned long long* look = nullptr;
-    unsigned long long* look_next = nullptr;
-    uint32_t* dbg = nullptr;
 };
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,

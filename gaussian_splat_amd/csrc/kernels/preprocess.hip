@@ -179,62 +179,6 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
 #define GS_PRE_WAVES 8
 #endif
 
-// Decoupled look-back (one wave): status word = flag (2 bits: 1 aggregate,
-// 2 inclusive) | visible (30 bits) | pairs (32 bits).  Workgroup w publishes
-// its own counts, then sums its predecessors' words 64 at a time, nearest
-// first, down to the first inclusive one, and publishes its inclusive sums.
-// A predecessor's word is waited for (agent-scope loads: the words of other
-// XCDs' workgroups are not in this L2); a bounded wait keeps it finite.
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = (1ull << 62) - 1;
-constexpr uint32_t kLbSpinMax = 1u << 16;
-__device__ __forceinline__ void look_back(const PreFuse& fuse, const uint2* wsum) {
-    const uint32_t lane = threadIdx.x, w = blockIdx.x;
-    const uint32_t tp = wsum[0].x + wsum[1].x + wsum[2].x + wsum[3].x;
-    const uint32_t tv = wsum[0].y + wsum[1].y + wsum[2].y + wsum[3].y;
-    const unsigned long long own = ((unsigned long long)tv << 32) | tp;
-    if (lane == 0)
-        __hip_atomic_store(&fuse.look[w], (w == 0 ? kLbIncl : kLbAgg) | own, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t ep = 0, ev = 0;  // exclusive pairs, visible
-    int32_t top = (int32_t)w - 1;
-    uint32_t spins = 0;
-    while (top >= 0) {
-        const int32_t j = top - (int32_t)lane;
-        const unsigned long long sw =
-            j >= 0 ? __hip_atomic_load(&fuse.look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-        const uint32_t flag = (uint32_t)(sw >> 62);
-        const uint64_t incl = __ballot(flag == 2u);
-        const uint32_t fi = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
-        const uint64_t upto = fi >= 63u ? ~0ull : (2ull << fi) - 1ull;  // lanes 0..fi
-        if (__ballot(flag == 0u) & upto) {
-            if (++spins > kLbSpinMax) {
-                if (lane == 0 && fuse.dbg) atomicAdd(&fuse.dbg[0], 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const bool in = lane <= fi;
-        const uint32_t sp = in ? (uint32_t)sw : 0u, sv = in ? (uint32_t)((sw & kLbVal) >> 32) : 0u;
-        ep += (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(sp), 63);
-        ev += (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(sv), 63);
-        if (fi < 64u) break;
-        top -= 64;
-    }
-    if (lane == 0) {
-        if (w > 0)
-            __hip_atomic_store(&fuse.look[w], kLbIncl | (((unsigned long long)(ev + tv) << 32) | (ep + tp)),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (fuse.dbg) {
-            fuse.dbg[3 + w] = ep;
-            if (w + 1 == gridDim.x) {
-                fuse.dbg[1] = ep + tp;
-                fuse.dbg[2] = ev + tv;
-            }
-        }
-    }
-}
-
 template <int DEG>
 __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
@@ -453,10 +397,6 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
             const uint32_t pv = wsum[0].y + wsum[1].y + wsum[2].y + wsum[3].y;
             if (ps) atomicAdd(&fuse.part[b], (unsigned long long)ps);
             if (pv) atomicAdd(&fuse.part[fuse.nb + b], (unsigned long long)pv);
-        }
-        if (fuse.look) {
-            for (uint32_t z = g; z < gridDim.x; z += gridDim.x * 256u) fuse.look_next[z] = 0ull;
-            if (threadIdx.x < 64) look_back(fuse, wsum);
         }
     }
 }
