@@ -179,7 +179,11 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
 #define GS_PRE_WAVES 8
 #endif
 
-template <int DEG>
+// EPI: what follows the per-splat work.  0: nothing (each lane returns on its
+// own); 1: the scan's reduce half and fills (PreFuse); 2: the two-slab depth
+// histogram.  Each epilogue is compiled only into its own instance, so the
+// plain kernel keeps its registers (63 VGPRs, no scratch).
+template <int DEG, int EPI>
 __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
@@ -188,6 +192,8 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                                                          uint32_t* __restrict__ hist, const PreFuse fuse) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i == 0 && zero8) *zero8 = 0ull;
+    if constexpr (EPI == 0)
+        if (i >= s.n) return;
     uint32_t rlo = kEmptyRectLo, rhi = 0u;
     uint32_t key = 0;
     if (i < s.n) {
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
     rect_lo[i] = rlo;
     rect_hi[i] = rhi;
     }
-    if (hist) {
+    if constexpr (EPI == 2) {
         // two-slab cut (SlabSel): the workgroup's depth histogram, weighted by
         // the bins of each rect, added into this XCD's copy (after every load
         // and store of the kernel, so the barriers cost it nothing)
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
         const uint32_t v = wh[threadIdx.x];
         if (v) atomicAdd(&hist[(blockIdx.x & (kCutCopies - 1u)) * kCutBuckets + threadIdx.x], v);
     }
-    if (fuse.part) {
+    if constexpr (EPI == 1) {
         // the scan's reduce half: this workgroup's pairs and visible splats
         // into its scan block's sums (the counts scan_duplicate recomputes)
         __shared__ uint2 wsum[4];
@@ -422,11 +428,18 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     dim3 grid((s.n + 255) / 256), block(256);
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
-    switch (sh_degree) {
-    case 0: hipExtLaunchKernelGGL(preprocess_kernel<0>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
-    case 1: hipExtLaunchKernelGGL(preprocess_kernel<1>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
-    case 2: hipExtLaunchKernelGGL(preprocess_kernel<2>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
-    case 3: hipExtLaunchKernelGGL(preprocess_kernel<3>, grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, rect_hi, zero8, hist, fuse); break;
+    const int epi = fuse.part ? 1 : hist ? 2 : 0;
+    switch (sh_degree * 3 + epi) {
+#define GS_PRE_CASE(D, E)                                                                                          \
+    case D * 3 + E:                                                                                                \
+        hipExtLaunchKernelGGL((preprocess_kernel<D, E>), grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, \
+                              rect_hi, zero8, hist, fuse);                                                         \
+        break;
+        GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1) GS_PRE_CASE(0, 2)
+        GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1) GS_PRE_CASE(1, 2)
+        GS_PRE_CASE(2, 0) GS_PRE_CASE(2, 1) GS_PRE_CASE(2, 2)
+        GS_PRE_CASE(3, 0) GS_PRE_CASE(3, 1) GS_PRE_CASE(3, 2)
+#undef GS_PRE_CASE
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -79,7 +79,10 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
-template <int NV>
+// FILT: the open-bin filter (two-slab frames' second slab) is compiled in
+// only where it is used; without it the kernels keep round 2's registers
+// (the pass at 80 VGPRs, 6 waves per SIMD, instead of 98 and 4).
+template <int NV, bool FILT>
 __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                         uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles,
                                                         const uint32_t* __restrict__ n_dev, const SortFilter flt) {
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
         for (int k = 0; k < K; ++k) kk[k] = keys[min(t0 + k * kRsThreads + tid, n - 1u)];
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (t0 + k * kRsThreads + tid < n && (!flt.open || flt.open[kk[k] & flt.bmask]))
+            if (t0 + k * kRsThreads + tid < n && (!FILT || flt.open[kk[k] & flt.bmask]))
                 atomicAdd(&h[wave][(kk[k] >> shift) & mask], 1u);
     }
     __syncthreads();
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __re
 // the caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
 // Bits above rmask ride along unsorted (the bin-first binning carries each
 // pair's depth key there, bin_depth_sort.hip).
-template <int NV, int BITS>
+template <int NV, int BITS, bool FILT>
 __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
@@ -223,20 +226,27 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     uint32_t all;
     const uint32_t dstart = block512_exclusive_scan(tid <= mask ? totals[tid] : 0u, tmp, &all);
     if (tid <= mask) gbase[tid] = dstart + C[(size_t)tid * ntiles + tile];
-    if (flt.kept && tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
     uint32_t keep = 0;  // (filtered: bit k = slot k is kept)
+    if constexpr (FILT) {
+        if (tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const uint32_t idx = base + k * 64 + lane;
-        keep |= (idx < n && (!flt.open || flt.open[key[k] & flt.bmask])) ? 1u << k : 0u;
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t idx = base + k * 64 + lane;
+            keep |= (idx < n && flt.open[key[k] & flt.bmask]) ? 1u << k : 0u;
+        }
     }
+    // slot k of this lane holds an item to sort
+    auto kept = [&](int k) -> bool {
+        if constexpr (FILT) return (keep >> k) & 1u;
+        else return base + k * 64 + lane < n;
+    };
     // Stable ranks: slot k of every lane in order, a wave's lanes matched by
     // digit (ballots), the wave's running count per digit in LDS.  (A second,
     // independent counting chain over half the slots was measured: the per-bin
     // sort unchanged, this pass slower.)
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-        const bool valid = (keep >> k) & 1u;
+        const bool valid = kept(k);
         const uint32_t d = (key[k] >> shift) & mask;
         const uint64_t peers = match_digit<BITS>(d, valid);
         const uint32_t below = mbcnt(peers);
@@ -260,19 +270,19 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     block_lds_sync();
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-        if ((keep >> k) & 1u) {
+        if (kept(k)) {
             const uint32_t d = (key[k] >> shift) & mask;
             pos[k] += blk_start[d] + wh[wave][d];
         }
     }
     const uint32_t t0 = tile * TILE;
-    const uint32_t cnt = flt.open ? tot : (n - t0 < TILE ? n - t0 : TILE);  // (the tile's kept items)
+    const uint32_t cnt = FILT ? tot : (n - t0 < TILE ? n - t0 : TILE);  // (the tile's kept items)
     // keys: stage in tile-local sorted order, write out; each slot's global
     // destination (from its staged key's digit) stays in registers for the
     // value arrays
 #pragma unroll
     for (int k = 0; k < IPT; ++k)
-        if ((keep >> k) & 1u) stage[pos[k]] = key[k];
+        if (kept(k)) stage[pos[k]] = key[k];
     block_lds_sync();
     uint32_t gdst[IPT];
 #pragma unroll
@@ -300,7 +310,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t idx = base + k * 64 + lane;
-            if ((keep >> k) & 1u) stage[pos[k]] = (NV == 1 || io.vin[a]) ? val[a][k] : idx;
+            if (kept(k)) stage[pos[k]] = (NV == 1 || io.vin[a]) ? val[a][k] : idx;
         }
         block_lds_sync();
 #pragma unroll
@@ -340,17 +350,17 @@ size_t radix_sort_scratch_words(uint32_t n) {
 }
 
 // rts_pass_kernel for a digit width (the ballot match unrolled per width)
-template <int NV, typename... A>
+template <int NV, bool FILT, typename... A>
 static hipError_t launch_pass(int width, uint32_t tiles, hipStream_t st, A... args) {
     switch (width) {
-    case 1: rts_pass_kernel<NV, 1><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 2: rts_pass_kernel<NV, 2><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 3: rts_pass_kernel<NV, 3><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 4: rts_pass_kernel<NV, 4><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 5: rts_pass_kernel<NV, 5><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 6: rts_pass_kernel<NV, 6><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 7: rts_pass_kernel<NV, 7><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 8: rts_pass_kernel<NV, 8><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 1: rts_pass_kernel<NV, 1, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 2: rts_pass_kernel<NV, 2, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 3: rts_pass_kernel<NV, 3, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 4: rts_pass_kernel<NV, 4, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 5: rts_pass_kernel<NV, 5, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 6: rts_pass_kernel<NV, 6, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 7: rts_pass_kernel<NV, 7, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 8: rts_pass_kernel<NV, 8, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -384,13 +394,23 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
         // (the filter drops items in pass 0; later passes sort what it kept)
         const SortFilter f = p == 0 ? flt : SortFilter{};
-        if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
-            rts_count_kernel<NV><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C, tiles, n_dev,
-                                                              f);
+        const bool filt = f.open != nullptr;
+        if (p > 0 || !first_counted) {  // (pass 0's counts may come from the producer)
+            if (filt)
+                rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                        tiles, n_dev, f);
+            else
+                rts_count_kernel<NV, false><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                         tiles, n_dev, f);
+        }
         rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
-        const hipError_t e = launch_pass<NV>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
-                                             tiles, p + 1 == plan.passes ? ranges : nullptr,
-                                             bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u, n_dev, f);
+        uint2* const rg = p + 1 == plan.passes ? ranges : nullptr;
+        const uint32_t rmask = bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+        const hipError_t e =
+            filt ? launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals, tiles,
+                                         rg, rmask, n_dev, f)
+                 : launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+                                          tiles, rg, rmask, n_dev, f);
         if (e != hipSuccess) return e;
         if (p == 0 && flt.open) n_dev = flt.kept;
         io.kin = io.kout;
