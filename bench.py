@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle", type=int, default=60,
+                    help="untimed frames before the warmup, run after the CPU-side scene build so the GPU "
+                         "leaves its idle clocks (reported in the JSON; 0 = none)")
     ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
     ap.add_argument("--splats", type=int, default=0, help="global splats (0 = the config's)")
     ap.add_argument("--width", type=int, default=0)
@@ -167,7 +170,7 @@ def pmc_passes(args):
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not found"
-    bench = [sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--cpu-baseline", "0",
+    bench = [sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--settle", "0", "--cpu-baseline", "0",
              "--pmc", "0", "--no-stage-timing", "--frames-in-flight", "1", "--splats", str(args.splats),
              "--width", str(args.width), "--height", str(args.height), "--sh", str(args.sh), "--mode", args.mode,
              "--seed", str(args.seed), "--profile", args.profile]
@@ -257,7 +260,19 @@ def main():
     opts = Options(mode=args.mode, sh_degree=args.sh, crop=False, stage_timing=timing,
                    frames_in_flight=args.frames_in_flight if world == 1 else 1)
 
+    settled = {"frames": 0, "ms": 0.0}
+
     def timed(step, steps, warmup):
+        # Settle, untimed: the GPU idles through the scene build, and the
+        # frame time then falls for ~40 frames as it leaves idle (5-frame
+        # blocks 0.89 -> 0.78 ms at 1080p; tools/warm_probe.py).
+        # Every rank runs the same count, so collectives stay matched.
+        t_s = time.perf_counter()
+        for _ in range(args.settle):
+            step()
+        torch.cuda.synchronize()
+        settled["frames"] += args.settle
+        settled["ms"] += (time.perf_counter() - t_s) * 1e3
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
@@ -352,6 +367,8 @@ def main():
             if args.config == "1080p" else f"Msplats/sec + achieved HBM GB/s ({args.label})",
             "value": round(value, 2), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "settle": {"frames": settled["frames"], "ms": round(settled["ms"], 1),
+                       "note": "untimed frames before the warmup, per timed scheme (GPU leaves idle clocks)"},
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)",
             "hbm_gbs": round(frame_bytes / (ms * 1e6), 1) if frame_bytes else None,

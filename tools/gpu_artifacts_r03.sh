@@ -23,7 +23,7 @@ configs) for c in 1m 4k 50m; do
          python -c "import json;d=json.load(open('$O/bench_$c.json'));print('$c', d['ms_per_step'], d['value'], d['config']['binning'], d['roofline']['kernels']['composite']['ms'])"; done ;;
 heavy) step heavy bash -c "timeout -k 10 600 python bench.py --profile heavy --steps 50 --cpu-baseline 0 > $O/bench_heavy.json 2> $O/bench_heavy.err"
        python -c "import json;d=json.load(open('$O/bench_heavy.json'));print('heavy', d['ms_per_step'], d['value'], d['config']['pairs'])" ;;
-ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
+ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --settle 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
        cat $O/rehearsal_2rank_gloo.json ;;
 timeline) step timeline bash -c "rm -rf $O/tl && timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --pmc 0 --no-stage-timing > $O/tl.log 2>&1"
        python tools/trace_timeline.py $(find $O/tl -name "*kernel_trace.csv" | head -1) 4 > $O/timeline_fif2.txt; tail -3 $O/timeline_fif2.txt ;;
