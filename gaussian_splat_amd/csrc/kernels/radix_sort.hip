@@ -371,7 +371,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
                                   const uint32_t* n_dev, bool first_counted, const SortFilter& flt = SortFilter{}) {
-    if (flt.open && (first_counted || !flt.kept)) return hipErrorInvalidValue;
+    if (flt.open && (NV != 1 || first_counted || !flt.kept)) return hipErrorInvalidValue;
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -394,23 +394,28 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
         // (the filter drops items in pass 0; later passes sort what it kept)
         const SortFilter f = p == 0 ? flt : SortFilter{};
-        const bool filt = f.open != nullptr;
-        if (p > 0 || !first_counted) {  // (pass 0's counts may come from the producer)
-            if (filt)
-                rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
-                                                                        tiles, n_dev, f);
-            else
-                rts_count_kernel<NV, false><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
-                                                                         tiles, n_dev, f);
-        }
-        rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
+        const bool filt = f.open != nullptr;  // (one value array only: the two-slab bin sort)
         uint2* const rg = p + 1 == plan.passes ? ranges : nullptr;
         const uint32_t rmask = bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
-        const hipError_t e =
-            filt ? launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals, tiles,
-                                         rg, rmask, n_dev, f)
-                 : launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+        hipError_t e = hipSuccess;
+        if constexpr (NV == 1) {
+            if (filt) {
+                if (p > 0 || !first_counted)
+                    rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p],
+                                                                            C, tiles, n_dev, f);
+                rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
+                e = launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
                                           tiles, rg, rmask, n_dev, f);
+            }
+        }
+        if (!filt) {
+            if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
+                rts_count_kernel<NV, false><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                         tiles, n_dev, f);
+            rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
+            e = launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals, tiles,
+                                       rg, rmask, n_dev, f);
+        }
         if (e != hipSuccess) return e;
         if (p == 0 && flt.open) n_dev = flt.kept;
         io.kin = io.kout;
