@@ -93,6 +93,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=-1)
     ap.add_argument("--profile", default="uniform", choices=["uniform", "heavy"],
                     help="scale distribution: uniform 3DGS statistics or the heavy-tailed stress variant")
+    ap.add_argument("--camera", default="fixed", choices=["fixed", "orbit"],
+                    help="fixed: the reference app's camera every frame; orbit (N=1): a new view every frame, "
+                         "the eye turning 0.01 rad about the target per frame (splats leave and enter the view)")
     ap.add_argument("--mode", default="tile")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU baseline duration")
@@ -218,6 +221,8 @@ def kernel_entry(ms, nbytes, pmc):
 
 def main():
     args = parse()
+    if args.camera == "orbit" and args.gpus > 1:
+        sys.exit("bench.py: --camera orbit is a single-GPU workload")
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -297,7 +302,18 @@ def main():
         r = InstancedSplatRenderer(scene, opts)
         r.initialize(local)
         out = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-        step = lambda: r.render(view, proj, W, H, out=out)
+        if args.camera == "orbit":
+            views = []
+            for _ in range(720):  # (cycled: 7.2 rad of orbit)
+                views.append(cam.getViewMatrix())
+                cam.orbit(0.01)
+            frame = [0]
+
+            def step():
+                r.render(views[frame[0] % len(views)], proj, W, H, out=out)
+                frame[0] += 1
+        else:
+            step = lambda: r.render(view, proj, W, H, out=out)
         rh = r
         ms = timed(step, args.steps, args.warmup)
     else:
@@ -370,7 +386,8 @@ def main():
             "settle": {"frames": settled["frames"], "ms": round(settled["ms"], 1),
                        "note": "untimed frames before the warmup, per timed scheme (GPU leaves idle clocks)"},
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)",
+            "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)"
+                    + ("; orbiting camera, a new view every frame" if args.camera == "orbit" else ""),
             "hbm_gbs": round(frame_bytes / (ms * 1e6), 1) if frame_bytes else None,
             "config": {"workload": args.label, "global_splats": N, "width": W, "height": H, "sh_degree": args.sh,
                        "parallelism": ((f"rows: {world} ranks, splat-index shards of one global scene, 32-px bin-row "

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/art3; rm -rf $O; mkdir -p $O
 step() { name=$1; shift; echo "== $name"; "$@"; rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-for s in ${STEPS:-tests bench prof pmc configs heavy ranks timeline}; do case $s in
+for s in ${STEPS:-tests bench prof pmc configs heavy orbit ranks timeline}; do case $s in
 tests) step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
        tail -1 $O/pytest_gpu.log ;;
 bench) step bench bash -c "timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err"; cat $O/bench_default.json ;;
@@ -21,6 +21,9 @@ pmc)   B="python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --pmc 0 --no-sta
 configs) for c in 1m 4k 50m; do
          step cfg_$c bash -c "timeout -k 10 600 python bench.py --config $c --steps 30 --cpu-baseline 0 > $O/bench_$c.json 2> $O/bench_$c.err"
          python -c "import json;d=json.load(open('$O/bench_$c.json'));print('$c', d['ms_per_step'], d['value'], d['config']['binning'], d['roofline']['kernels']['composite']['ms'])"; done ;;
+orbit) for p in uniform heavy; do
+         step orbit_$p bash -c "timeout -k 10 600 python bench.py --camera orbit --profile $p --cpu-baseline 0 --pmc 0 > $O/bench_orbit_$p.json 2> $O/bench_orbit_$p.err"
+         python -c "import json;d=json.load(open('$O/bench_orbit_$p.json'));print('orbit $p', d['ms_per_step'], d['config']['visible'], d['config']['pairs'])"; done ;;
 heavy) step heavy bash -c "timeout -k 10 600 python bench.py --profile heavy --steps 50 --cpu-baseline 0 > $O/bench_heavy.json 2> $O/bench_heavy.err"
        python -c "import json;d=json.load(open('$O/bench_heavy.json'));print('heavy', d['ms_per_step'], d['value'], d['config']['pairs'])" ;;
 ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --settle 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
