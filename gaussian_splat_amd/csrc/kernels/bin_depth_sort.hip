@@ -226,12 +226,6 @@ __device__ void sort_list_global(uint32_t s, uint32_t m, uint32_t* keys, uint32_
     }
 }
 
-#ifndef GS_SEG_NT  // A/B knobs (tools/build_variant.py): the common size class
-#define GS_SEG_NT 512
-#endif
-#ifndef GS_SEG_IPT
-#define GS_SEG_IPT 16
-#endif
 #ifndef GS_SEG_MINW  // min waves per SIMD (launch bounds: caps the VGPRs)
 #define GS_SEG_MINW 6
 #endif

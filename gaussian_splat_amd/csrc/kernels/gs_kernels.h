@@ -125,7 +125,13 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
 // sample (2 words, zeroed by the next scan): [0] += pairs of the lists longer
 // than kSegLdsMax (sorted through global memory, ~3x the cost per pair),
 // [1] |= kSegSampleValid once the sort ran.
-constexpr uint32_t kSegLdsMax = 8192;  // = the kernel's NT * IPT (bin_depth_sort.hip)
+#ifndef GS_SEG_NT  // A/B knobs (tools/build_variant.py): the per-bin sort's common size class
+#define GS_SEG_NT 512
+#endif
+#ifndef GS_SEG_IPT
+#define GS_SEG_IPT 16
+#endif
+constexpr uint32_t kSegLdsMax = GS_SEG_NT * GS_SEG_IPT;  // lists sorted inside one workgroup (bin_depth_sort.hip)
 constexpr uint32_t kSegSampleValid = 0x80000000u;
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
