@@ -27,7 +27,7 @@ namespace gs {
 
 #ifdef GS_COMPOSITE_COUNTERS
 // Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
-__device__ unsigned long long g_cc[16];
+__device__ unsigned long long g_cc[20];
 __device__ uint32_t g_tile_fetch[1u << 16];  // per tile (bin * 4 + tile of the bin): records fetched
 #define GS_CC(i, v) (void)atomicAdd(&g_cc[i], (unsigned long long)(v))
 #else
@@ -495,6 +495,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                         }
                     cc_bmr[tid] = (uint16_t)bmr;
                     cc_bme[tid] = (uint16_t)bme;
+                    // staged records, and those whose rect reaches the tile at all
+                    GS_CC(16, 1);
+                    if (qm) GS_CC(17, 1);
                 }
 #endif
             }
@@ -688,7 +691,7 @@ extern "C" int gs_debug_composite_tile_fetch(uint32_t* out, unsigned n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_tile_fetch), (size_t)n * 4) != hipSuccess;
 }
 extern "C" int gs_debug_composite_counters(unsigned long long* out) {
-    unsigned long long zero[16] = {};
+    unsigned long long zero[20] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cc), sizeof zero) != hipSuccess) return 1;
     return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_cc), zero, sizeof zero) != hipSuccess;
 }

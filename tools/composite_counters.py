@@ -51,7 +51,7 @@ if hasattr(lib(), "gs_debug_composite_timers"):  # -DGS_COMPOSITE_TIMERS build: 
     sys.exit(0)
 f = lib().gs_debug_composite_counters
 f.argtypes = [C.POINTER(C.c_uint64)]
-buf = (C.c_uint64 * 16)()
+buf = (C.c_uint64 * 20)()
 r.render(V, P, W, H, out=out)
 torch.cuda.synchronize()
 f(buf)
@@ -75,6 +75,8 @@ print(f"per wave walk steps: now {c[3] / waves:.1f}  4x4 groups {c[10] / waves:.
       f"per-lane max {c[12] / waves:.1f}  per-lane mean {c[13] / waves / 64:.1f}")
 print(f"per wave, summed per-batch maxima: exact 4x4 groups {c[1] / waves:.1f}  per-lane {c[2] / waves:.1f}  "
       f"rect 4x4 groups {c[14] / waves:.1f}  ellipse 4x4 groups {c[15] / waves:.1f}")
+print(f"staged records {c[16]}  reaching the tile {c[17]} ({c[17] / max(c[16], 1):.3f})  "
+      f"per wg: staged {c[16] / wg:.0f}  reaching {c[17] / wg:.0f}")
 print(f"per wg: batches {c[5] / wg:.2f}  list {c[6] / wg:.0f}  batches if no exit {c[6] / wg / 256:.2f}")
 tf = lib().gs_debug_composite_tile_fetch
 tf.argtypes = [C.POINTER(C.c_uint32), C.c_uint]
