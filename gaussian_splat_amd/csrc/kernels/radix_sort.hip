@@ -181,6 +181,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     __shared__ uint32_t gbase[ND];         // global start of this tile's digit run
     __shared__ uint32_t stage[TILE];
     __shared__ uint32_t tmp[kRsWaves];
+    __shared__ uint32_t rflag[ND];         // (ranges, shift > 0: run-end merges this tile skips)
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -226,6 +227,37 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     uint32_t all;
     const uint32_t dstart = block512_exclusive_scan(tid <= mask ? totals[tid] : 0u, tmp, &all);
     if (tid <= mask) gbase[tid] = dstart + C[(size_t)tid * ntiles + tile];
+    // Run-end merges (ranges, a last pass above lower digits).  The input is
+    // sorted by its low `shift` bits (LSD), so a key's run starts in the first
+    // tile that holds the key's low value with its digit.  When the previous
+    // tile lies wholly inside this tile's first low value and holds digit d,
+    // no run of (d, that low value) starts here: bit 0 of rflag[d] skips the
+    // start merge; bit 1 the end merge, mirrored with the next tile.  Any
+    // other run end still merges with atomicMin (an extra merge is harmless),
+    // so only tiles at a low value's edges merge: each merge is a memory-side
+    // atomic on a few contended lines (measured 14 us per frame unskipped).
+    const bool rskip = ranges && shift > 0;
+    const uint32_t lm = (1u << shift) - 1u;
+    uint32_t lo_first = 0, lo_last = 0;
+    if (rskip) {
+        const uint32_t t0 = tile * TILE, t1 = min(t0 + TILE, n);
+        lo_first = io.kin[t0] & lm;
+        lo_last = io.kin[t1 - 1] & lm;
+        if (tid <= mask) {
+            const uint32_t* Cd = C + (size_t)tid * ntiles;
+            uint32_t f = 0;
+            if (tile > 0 && (io.kin[t0 - TILE] & lm) == lo_first && (io.kin[t0 - 1] & lm) == lo_first &&
+                Cd[tile] != Cd[tile - 1])
+                f |= 1u;
+            if (t1 < n) {  // (tile + 1 < ntiles)
+                const uint32_t t2 = min(t1 + TILE, n);
+                const uint32_t after = tile + 2 < ntiles ? Cd[tile + 2] : totals[tid];
+                if ((io.kin[t1] & lm) == lo_last && (io.kin[t2 - 1] & lm) == lo_last && after != Cd[tile + 1])
+                    f |= 2u;
+            }
+            rflag[tid] = f;
+        }
+    }
     uint32_t keep = 0;  // (filtered: bit k = slot k is kept)
     if constexpr (FILT) {
         if (tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
@@ -294,12 +326,22 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
             const uint32_t g = gbase[d] + (j - blk_start[d]);
             gdst[k] = g;
             io.kout[g] = key;
+#ifdef GS_RS_ABL_NORANGES  // ablation (timing only): no run ends
+            if (false) {
+#else
             if (ranges) {
+#endif
                 // run ends of this key inside the tile (the tile's output is a
                 // contiguous, fully sorted slice of the final order per digit)
                 const uint32_t rk = key & rmask;
-                if (j == 0 || (stage[j - 1] & rmask) != rk) atomicMin(&ranges[rk].x, g);
-                if (j + 1 == cnt || (stage[j + 1] & rmask) != rk) atomicMin(&ranges[rk].y, ~(g + 1u));
+                const bool s0 = j == 0 || (stage[j - 1] & rmask) != rk;
+                const bool s1 = j + 1 == cnt || (stage[j + 1] & rmask) != rk;
+                if (s0 || s1) {
+                    const uint32_t lo = key & lm;
+                    const uint32_t fl = rskip ? rflag[d] : 0u;
+                    if (s0 && !(lo == lo_first && (fl & 1u))) atomicMin(&ranges[rk].x, g);
+                    if (s1 && !(lo == lo_last && (fl & 2u))) atomicMin(&ranges[rk].y, ~(g + 1u));
+                }
             }
         }
     }
