@@ -33,6 +33,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -43,6 +45,7 @@
 #include <vector>
 
 #include "../kernels/gs_kernels.h"
+#include "comm_set.h"
 #include "gs_internal.h"
 #include "gsplat.h"
 
@@ -223,6 +226,7 @@ struct gs_group {
     hipEvent_t frame_done = nullptr;  // on devices[0]: everything of the last frame
     DevMem fb;                        // host-output frames
     int64_t timeout_ms = 60000;       // bound of every host wait (gs_group_set_timeout)
+    bool timeout_set = false;         // set by gs_group_set_timeout (GS_COMM_TIMEOUT_MS then ignored)
     bool failed = false;              // communicators aborted: the group is unusable
     ~gs_group() {
         delete pool;
@@ -234,8 +238,8 @@ struct gs_group {
             if (k.ev_done) (void)hipEventDestroy(k.ev_done);
             gs_destroy(k.h);
         }
-        for (ncclComm_t c : comms)
-            if (c) (void)(failed ? g_rccl.comm_abort(c) : g_rccl.comm_destroy(c));
+        // (a failure has aborted and cleared every handle already)
+        gscomm::destroy_all(comms, [](ncclComm_t c) { return g_rccl.comm_destroy(c); });
         if (frame_done) (void)hipEventDestroy(frame_done);
         fb.release();
     }
@@ -277,9 +281,8 @@ gs_status run_ranks(gs_group* g, const std::function<gs_status(Rank&, int)>& f) 
 
 // Abort every communicator after a peer error or an expired wait.
 gs_status comm_failure(gs_group* g, const std::string& why) {
-    if (g->transport == GS_TRANSPORT_RCCL && !g->failed)
-        for (ncclComm_t c : g->comms)
-            if (c) (void)g_rccl.comm_abort(c);
+    if (g->transport == GS_TRANSPORT_RCCL)
+        gscomm::abort_all(g->comms, [](ncclComm_t c) { return g_rccl.comm_abort(c); });
     g->failed = true;
     return gfail(GS_ERR_COMM, why);
 }
@@ -641,6 +644,16 @@ gs_status gs_create_sharded(const char* ply_path, const gs_options* opt, int32_t
 gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t transport) {
     if (!g) return gfail(GS_ERR_INVALID_ARG, "null group");
     if (g->initialized) return gfail(GS_ERR_STATE, "group already initialized");
+    // the environment's default wait bound, unless gs_group_set_timeout set one;
+    // a value that is not a positive integer is rejected, not clamped
+    if (const char* t = std::getenv("GS_COMM_TIMEOUT_MS"); t && !g->timeout_set) {
+        char* end = nullptr;
+        errno = 0;
+        const long long v = std::strtoll(t, &end, 10);
+        if (end == t || *end != '\0' || errno == ERANGE || v <= 0)
+            return gfail(GS_ERR_INVALID_ARG, std::string("GS_COMM_TIMEOUT_MS is not a positive integer: '") + t + "'");
+        g->timeout_ms = v;
+    }
     int count = 0;
     GG_HIP(hipGetDeviceCount(&count));
     std::vector<int> dev((size_t)g->world);
@@ -679,9 +692,7 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
             k.own_stream = false;
             k.ev_ready = k.ev_done = nullptr;
         }
-        for (ncclComm_t c : g->comms)
-            if (c) (void)g_rccl.comm_destroy(c);
-        g->comms.clear();
+        gscomm::destroy_all(g->comms, [](ncclComm_t c) { return g_rccl.comm_destroy(c); });
         return gfail(st, msg);
     };
     for (int i = 0; i < g->world; ++i) {
@@ -724,7 +735,6 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
         gs_set_last_error("gs_group_initialize: frame event");
         return rollback(GS_ERR_DEVICE);
     }
-    if (const char* t = std::getenv("GS_COMM_TIMEOUT_MS")) g->timeout_ms = std::max<int64_t>(1, std::atoll(t));
     g->transport = transport;
     g->pool = new Pool(g->world);
     g->initialized = true;
@@ -734,6 +744,7 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
 gs_status gs_group_set_timeout(gs_group* g, int32_t timeout_ms) {
     if (!g || timeout_ms <= 0) return gfail(GS_ERR_INVALID_ARG, "gs_group_set_timeout: bad arguments");
     g->timeout_ms = timeout_ms;
+    g->timeout_set = true;
     return GS_OK;
 }
 

@@ -40,7 +40,7 @@ struct SortIO {
 };
 
 #ifndef GS_RS_IPT1  // A/B knobs (tools/build_variant.py)
-#define GS_RS_IPT1 12  // 6144-pair tiles: 148 vs 157 us (8: 150, 16: 157, 24: 200) at the bench config
+#define GS_RS_IPT1 8  // 4096-pair tiles: sort stage 115.7 vs 119.6 us for 6144 (16: 129) after the run-end merge skip (profiles/r03/ab_sort_tile_ipt.txt)
 #endif
 #ifndef GS_RS_PASS_WAVES  // min waves per SIMD of the pass kernel (HIP launch bounds)
 #define GS_RS_PASS_WAVES 1

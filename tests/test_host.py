@@ -105,3 +105,17 @@ def test_scene_from_points_roundtrip():
     np.testing.assert_array_equal(sc.pos, pts[:, 0:3])
     np.testing.assert_array_equal(sc.rot, pts[:, 13:17])
     np.testing.assert_array_equal(sc.opacity, pts[:, 9])
+
+
+def test_comm_release_rule_aborts_each_communicator_once(tmp_path):
+    """after a collective failure aborts every RCCL
+    communicator, the group's teardown must not release them again.  The rule
+    lives in csrc/host/comm_set.h; stub handles count each release."""
+    import subprocess
+    src = ROOT / "tests" / "host" / "comm_set_test.cpp"
+    exe = tmp_path / "comm_set_test"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    f"-I{ROOT / 'gaussian_splat_amd' / 'csrc' / 'host'}", str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "comm_set: ok" in r.stdout

@@ -143,3 +143,26 @@ def test_sharded_group_host_side(built):
         g.render_host(np.eye(4), np.eye(4), 16, 16)
     with pytest.raises(GsError):
         ShardedGroup(r, 0)
+
+
+def test_group_timeout_env_is_validated(built, monkeypatch):
+    """GS_COMM_TIMEOUT_MS: a value that is not a positive integer
+    is rejected by gs_group_initialize instead of becoming a 1 ms bound; the
+    check runs before any device is touched, so it holds on the CPU."""
+    from gaussian_splat_amd import GsError, InstancedSplatRenderer, Options, ShardedGroup
+    from gaussian_splat_amd import _lib
+    from gaussian_splat_amd import scene as S
+    r = InstancedSplatRenderer(S.synthetic_scene(64, seed=3), Options(crop=False))
+    for bad in ("abc", "10ms", "0", "-5", ""):
+        monkeypatch.setenv("GS_COMM_TIMEOUT_MS", bad)
+        g = ShardedGroup(r, 2)
+        with pytest.raises(GsError):
+            g.initialize([0, 0], transport="copy")
+        assert "GS_COMM_TIMEOUT_MS" in _lib.last_error()
+    # an explicit gs_group_set_timeout wins over the environment
+    monkeypatch.setenv("GS_COMM_TIMEOUT_MS", "abc")
+    g = ShardedGroup(r, 2)
+    g.set_timeout(5000)
+    with pytest.raises(GsError):
+        g.initialize([0, 0], transport="copy")  # (no device here)
+    assert "GS_COMM_TIMEOUT_MS" not in _lib.last_error()
