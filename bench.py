@@ -82,9 +82,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--settle", type=int, default=60,
-                    help="untimed frames before the warmup, run after the CPU-side scene build so the GPU "
-                         "leaves its idle clocks (reported in the JSON; 0 = none)")
+    ap.add_argument("--settle", type=int, default=0,
+                    help="untimed frames before the warmup (0 = the warmup alone, as the driver runs it)")
+    ap.add_argument("--settled-probe", type=int, default=60,
+                    help="after the timed region: this many more untimed frames, then the same K frames timed "
+                         "again, reported beside the value as 'settled' (0 = skip)")
     ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
     ap.add_argument("--splats", type=int, default=0, help="global splats (0 = the config's)")
     ap.add_argument("--width", type=int, default=0)
@@ -270,16 +272,16 @@ def main():
 
     settled = {"frames": 0, "ms": 0.0}
 
-    def timed(step, steps, warmup):
-        # Settle, untimed: the GPU idles through the scene build, and the
-        # frame time then falls for ~40 frames as it leaves idle (5-frame
-        # blocks 0.89 -> 0.78 ms at 1080p; tools/warm_probe.py).
-        # Every rank runs the same count, so collectives stay matched.
+    def timed(step, steps, warmup, settle=None):
+        # --settle: untimed frames before the warmup (default none, the
+        # driver's --warmup governs).  Every rank runs the same count, so
+        # collectives stay matched.
+        settle = args.settle if settle is None else settle
         t_s = time.perf_counter()
-        for _ in range(args.settle):
+        for _ in range(settle):
             step()
         torch.cuda.synchronize()
-        settled["frames"] += args.settle
+        settled["frames"] += settle
         settled["ms"] += (time.perf_counter() - t_s) * 1e3
         for _ in range(warmup):
             step()
@@ -300,6 +302,19 @@ def main():
             dt = float(t.item())
         return dt * 1e3 / steps
 
+    def settled_probe(step, steps):
+        # The value is the driver's protocol (its --warmup only).  The GPU
+        # leaves idle clocks over the first ~40 frames (5-frame blocks 0.89 ->
+        # 0.78 ms at 1080p, tools/warm_probe.py), so the same K
+        # frames are timed once more after --settled-probe further frames and
+        # reported beside it, never as the value.
+        if args.settled_probe <= 0:
+            return None
+        for _ in range(args.settled_probe):
+            step()
+        return {"extra_frames": args.settled_probe, "ms_per_step": round(timed(step, steps, 0, settle=0), 4),
+                "note": "the same frames timed again after the value's run and these extra untimed frames"}
+
     schemes = {}
     if world == 1:
         r = InstancedSplatRenderer(scene, opts)
@@ -319,6 +334,7 @@ def main():
             step = lambda: r.render(view, proj, W, H, out=out)
         rh = r
         ms = timed(step, args.steps, args.warmup)
+        settled_line = settled_probe(step, args.steps)
     else:
         from gaussian_splat_amd.distributed import (BandRenderer, HipBandBackend, HipShardBackend, HipSlabBackend,
                                                     ShardedRenderer, SlabRenderer)
@@ -344,6 +360,7 @@ def main():
         # the splat-sharded exact scheme is the headline whenever it ran
         head = "rows" if "rows" in schemes else order[0]
         ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
+        settled_line = settled_probe(step, args.steps)
     value = N / (ms * 1e-3) / 1e6
 
     s0 = rh.last_stats()
@@ -391,7 +408,8 @@ def main():
             "value": round(value, 2), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "settle": {"frames": settled["frames"], "ms": round(settled["ms"], 1),
-                       "note": "untimed frames before the warmup, per timed scheme (GPU leaves idle clocks)"},
+                       "note": "untimed frames before the warmup (--settle), per timed scheme"},
+            "settled": settled_line,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)"
                     + ("; orbiting camera, a new view every frame" if args.camera == "orbit" else ""),

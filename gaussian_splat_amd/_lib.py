@@ -72,8 +72,6 @@ SIGNATURES = {
     "gs_project_host": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, _P, _P]),
     "gs_sorted_pairs_host": (C.c_int, [_P, _P, _P, C.c_int64, _I64P]),
     "gs_radix_sort_pairs": (C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32, _P]),
-    "gs_radix_sort_pairs_filtered": (C.c_int, [_P, _P, _P, _P, _P, _P, C.c_int64, C.c_int32, _P,
-                                               C.POINTER(C.c_int64), _P]),
     "gs_shard_configure": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int64]),
     "gs_shard_set_rows": (C.c_int, [_P, _P, C.c_int32]),
     "gs_shard_project": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int64, _I64P, _P]),

@@ -257,7 +257,9 @@ class InstancedSplatRenderer:
         self.options.cap = int(cap)
 
     def set_depth_split(self, on: bool):
-        """Two depth slabs for bin-first frames (gs_set_depth_split): same image, less sorting."""
+        """Per-bin depth cuts (gs_set_depth_split): bin lists cut behind the depth
+        where each bin saturated two frames back, open tiles finished by fallback
+        lists; same image, bit for bit, less sorting."""
         check(lib().gs_set_depth_split(self._h, 1 if on else 0), "gs_set_depth_split")
         self.options.depth_split = bool(on)
 
@@ -377,25 +379,6 @@ def radix_sort_pairs(keys, vals, bits: int, stream=None):
                                     C.c_void_p(tk.data_ptr()), C.c_void_p(tv.data_ptr()), n, int(bits),
                                     C.c_void_p(stream)), "gs_radix_sort_pairs")
     return keys, vals
-
-
-def radix_sort_pairs_filtered(keys, vals, bits: int, open_bins, stream=None):
-    """Stable sort keeping the pairs whose key bits [0, bits) index a nonzero
-    word of open_bins (a CUDA int32 tensor of 2^bits words); returns new
-    (keys, vals) tensors of the kept pairs."""
-    import torch
-
-    n = keys.numel()
-    ko, vo, tk, tv = (torch.empty_like(keys) for _ in range(4))
-    kept = C.c_int64(0)
-    if stream is None:
-        stream = torch.cuda.current_stream(keys.device).cuda_stream
-    check(lib().gs_radix_sort_pairs_filtered(C.c_void_p(keys.data_ptr()), C.c_void_p(vals.data_ptr()),
-                                             C.c_void_p(ko.data_ptr()), C.c_void_p(vo.data_ptr()),
-                                             C.c_void_p(tk.data_ptr()), C.c_void_p(tv.data_ptr()), n, int(bits),
-                                             C.c_void_p(open_bins.data_ptr()), C.byref(kept), C.c_void_p(stream)),
-          "gs_radix_sort_pairs_filtered")
-    return ko[: kept.value], vo[: kept.value]
 
 
 SCHEMES = {"rows": 0, "slabs": 1, "bands": 2}  # gs_scheme

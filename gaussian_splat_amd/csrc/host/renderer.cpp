@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../kernels/gs_kernels.h"
@@ -96,10 +97,8 @@ struct gs_handle {
     // stage_timing 2: packet events (preprocess start/stop, composite start/stop)
     // in a ring of per-frame slots, read without stalling the frames
     static constexpr int kKevRing = 64;
-    // [0, 1] preprocess start/stop, [2, 3] composite start/stop; two-slab
-    // frames: [4] first composite stop, [5] second composite start
-    hipEvent_t kev[kKevRing][6] = {};
-    bool kev_two[kKevRing] = {};
+    // [0, 1] preprocess start/stop, [2, 3] composite start/stop
+    hipEvent_t kev[kKevRing][4] = {};
     int64_t kev_frames = 0;    // frames recorded since stage timing was (re)set
     int kev_slot = 0;          // slot of the frame being enqueued
     bool kev_pending = false;  // last frame's kernel times not yet copied into stats
@@ -113,7 +112,7 @@ struct gs_handle {
     bool bin_first_frame = false;       // the last frame used the bin-first order
     DevBuf seg_sample;                  // per-bin depth sort sample (launch_bin_depth_sort)
     DevBuf npairs;                      // P on the device (0 when it overflows the pair buffers)
-    DevBuf fetch;                       // per buffer set: records the composite fetched (u64)
+    DevBuf fetch;                       // per buffer set: [2 set] records the composite fetched, [2 set + 1] open tiles (u64)
     int stats_set = -1;                 // buffer set of the frame in `stats` (its fetch counter)
     int64_t stats_fixed_bytes = 0;      // composite bytes besides the records: range words + output
     hipEvent_t totals_ev = nullptr;     // P is in host_total
@@ -151,17 +150,31 @@ struct gs_handle {
     hipEvent_t set_free[2] = {};           // last use of each buffer set on a composite stream
     int set = 0;
     bool last_pipe = false;  // the last frame ran pipelined (a switch into pipelining waits for the caller's stream)
-    DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr;
-    // Two-slab frames (gs_options.depth_split): the depth
-    // histogram of the cut (filled by the preprocess, cleared by the first
-    // slab's scan), the cut per buffer set, the composite's open-tile flags,
-    // the second slab's own sort scratch (its lists are sorted on the
-    // composite stream while the side stream builds the next frame's) and,
-    // per set, the number of its pairs the filtered sort kept.
-    DevBuf ghist, kcut, open4, scratch2, tot2;
-    bool two_slab_frame = false;
-    uint64_t p1_pairs = 0;   // first-slab pairs of the frame in `stats`
-    uint32_t pair_cap = 0;   // pair capacity of the set of the last build_bin_lists
+    DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr, alt_rlo, alt_rhi,
+        alt_qrec;
+    // Depth cuts (gs_options.depth_split).  cutbuf, per buffer
+    // set, two per-bin cut tables: a frame's front lists keep the pairs at or
+    // ahead of the cuts its set's previous frame (two frames back) left in
+    // one; its composite writes the quadrant records (qrec: cut positions and
+    // open flags, one set each, swapped) and launch_cut_finalize turns them
+    // into the other table; then the roles swap.  cstate: the open quadrants'
+    // pixel states; the fallback lists' scan sums, pair count, sort scratch
+    // (composite stream only) and totals (per set, for gs_last_stats); kept:
+    // the front lists' pair count per set.
+    DevBuf qrec, cutbuf, cstate, fpart, fnpairs, scratch2, tot2, kept;
+    uint32_t cut_bins = 0;       // bins per table in cutbuf
+    int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
+    int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
+    bool cut_valid[2] = {false, false};
+    bool cut_frame = false;      // the frame in `stats` used depth cuts
+    bool cut_pending = false;    // the frame being enqueued is a depth-cut frame (render_frame)
+    const uint32_t* cut_in = nullptr;  // (its cuts; null: none yet, every pair in its lists)
+    uint32_t* cut_out = nullptr;
+    bool cut_lists = false;      // the frame in `stats` filtered its lists at the cuts (front pairs: kept[set])
+    uint32_t pair_cap = 0;       // pair capacity of the set of the last build_bin_lists
+    uint32_t* cut_table(int set, int role) const {
+        return cutbuf.as<uint32_t>() + (size_t)(2 * set + ((cut_phase[set] + role) & 1)) * cut_bins;
+    }
     void swap_sets() {
         std::swap(rec, alt_rec);
         std::swap(dkey, alt_dkey);
@@ -171,6 +184,9 @@ struct gs_handle {
         std::swap(tvals, alt_tvals);
         std::swap(ranges, alt_ranges);
         std::swap(thr, alt_thr);
+        std::swap(rlo, alt_rlo);
+        std::swap(rhi, alt_rhi);
+        std::swap(qrec, alt_qrec);
         set ^= 1;
     }
     int64_t index_base = 0;
@@ -179,8 +195,9 @@ struct gs_handle {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
-                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &seg_sample, &npairs, &fetch,
-                          &ghist, &kcut, &open4, &scratch2, &tot2, &ppart})
+                          &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &alt_rlo,
+                          &alt_rhi, &alt_qrec, &seg_sample, &npairs, &fetch, &qrec, &cutbuf, &cstate, &fpart,
+                          &fnpairs, &scratch2, &tot2, &kept, &ppart})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -274,11 +291,22 @@ gs::FrameUniforms make_uniforms(const float* V, const float* P, int W, int H) {
     return u;
 }
 
-// Two-slab frames: the first slab's share of the frame's
-// pairs.  The composite reads ~1/4 of each bin list before its tiles
-// saturate (6M @ 1080p); 30 % leaves ~20 % of the bins open, whose second
-// slab is then ~13 % of the pairs (measured on the oracle's lists).
-constexpr float kDepthSplitFrac = 0.3f;
+// Depth cuts: a tile's cut is the depth key of the last
+// record it staged before its pixels finished, plus this margin (dkey units:
+// one is 2^-10 of relative depth), so that the next frames' views, which move,
+// still find their tiles' saturation inside the front lists.
+constexpr uint32_t kCutMargin = 64;
+uint32_t cut_margin() {  // GS_CUT_MARGIN overrides (A/B, tests)
+    static const char* env = std::getenv("GS_CUT_MARGIN");
+    static const uint32_t m = env ? (uint32_t)std::strtoul(env, nullptr, 10) : kCutMargin;
+    return m;
+}
+
+// Depth cuts on (gs_options.depth_split; GS_DEPTH_SPLIT=0|1 overrides, A/B).
+bool depth_cuts_on(const gs_handle* h) {
+    static const char* env = std::getenv("GS_DEPTH_SPLIT");
+    return env ? env[0] == '1' : h->opt.depth_split == 1;
+}
 
 int bits_for(uint32_t v) {  // bits needed to represent values < v
     int b = 0;
@@ -338,17 +366,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->dkey.reserve(n * 4));
     GS_HIP(h->rlo.reserve(n * 4));
     GS_HIP(h->rhi.reserve(n * 4));
-    // (3 words per scan block: the two-slab first pass also sums both slabs' pairs)
-    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 24));
-    static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
-    if (ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1) {  // two-slab frames
-        if (!h->ghist.ptr) {
-            GS_HIP(h->ghist.reserve((size_t)gs::kCutCopies * gs::kCutBuckets * 4));
-            GS_HIP(hipMemset(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4));
-        }
-        GS_HIP(h->kcut.reserve(8));
-        GS_HIP(h->tot2.reserve(2 * 64));
-    }
+    GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 24));  // (3 rows: depth-cut front lists)
     if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
         GS_HIP(hipHostMalloc((void**)&h->host_total, 64, hipHostMallocMapped | hipHostMallocCoherent));
         GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
@@ -358,7 +376,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 16));
     }
     GS_HIP(h->npairs.reserve(4));
-    GS_HIP(h->fetch.reserve(32));  // per buffer set: [set] records fetched, [2 + set] open tiles (two-slab)
+    GS_HIP(h->fetch.reserve(32));  // per buffer set: [2 set] records fetched, [2 set + 1] open tiles (depth cuts)
     if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
     if (h->opt.stage_timing && !h->events) {
         for (auto& e : h->ev) GS_HIP(hipEventCreate(&e));
@@ -395,7 +413,9 @@ float elapsed(gs_handle* h, int a, int b) {
 
 // The frame's composite fetch counter (one per buffer set; the preprocess of
 // the frame clears it).
-unsigned long long* fetch_counter(gs_handle* h) { return h->fetch.as<unsigned long long>() + h->set; }
+unsigned long long* fetch_counter(gs_handle* h) { return h->fetch.as<unsigned long long>() + 2 * h->set; }
+// Its open tile count (depth cuts), cleared with it.
+unsigned long long* open_counter(gs_handle* h) { return h->fetch.as<unsigned long long>() + 2 * h->set + 1; }
 
 hipEvent_t kernel_event(gs_handle* h, int k) {
     return h->opt.stage_timing == 2 && h->events ? h->kev[h->kev_slot][k] : nullptr;
@@ -412,14 +432,7 @@ void begin_frame(gs_handle* h, hipStream_t st) {
 gs_status slot_times(gs_handle* h, int k, float* pre, float* comp, float* total) {
     GS_HIP(hipEventSynchronize(h->kev[k][3]));
     GS_HIP(hipEventElapsedTime(pre, h->kev[k][0], h->kev[k][1]));
-    if (h->kev_two[k]) {  // two-slab frame: both composite launches, not the second slab's lists between them
-        float a = 0.0f, b = 0.0f;
-        GS_HIP(hipEventElapsedTime(&a, h->kev[k][2], h->kev[k][4]));
-        GS_HIP(hipEventElapsedTime(&b, h->kev[k][5], h->kev[k][3]));
-        *comp = a + b;
-    } else {
-        GS_HIP(hipEventElapsedTime(comp, h->kev[k][2], h->kev[k][3]));
-    }
+    GS_HIP(hipEventElapsedTime(comp, h->kev[k][2], h->kev[k][3]));
     if (total) GS_HIP(hipEventElapsedTime(total, h->kev[k][0], h->kev[k][3]));
     return GS_OK;
 }
@@ -514,6 +527,10 @@ gs_status prepare_lists(gs_handle* h, uint32_t m, bool index_order, const gs::Fr
     if (!index_order) GS_HIP(h->offsets.reserve((size_t)std::max<uint32_t>(m, 1) * 4));
     lp->cap = reserve_pairs(h, h->order.frame_pairs);
     if (!lp->cap) return fail(GS_ERR_OOM, "pair buffers");
+    // the sort scratch holds the first pass's digit counts (pc.C, taken just
+    // below) and the depth sort's over m items: sized for both here, so no
+    // later reserve of this frame can move it
+    GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words(std::max<uint32_t>(std::max<uint32_t>(m, 1), lp->cap)) * 4));
     lp->pc = pass_counts(h, m, index_order, gs::make_sort_plan(list_key_bits(U)), lp->cap, h->order.frame_pairs);
     return GS_OK;
 }
@@ -534,19 +551,23 @@ bool pick_bin_first(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nr
 // read the pair count on the device and are sized by the pair buffers'
 // capacity (grown to the last frame's P); a frame whose P exceeds it runs
 // them as no-ops, and they are queued again once the buffers have grown.
-// sel (two-slab frames): the first slab's filter; *pairs is then that slab's
-// pair count, h->stats.pairs both slabs', and the buffers hold both.
+// Depth-cut frames with cuts (h->cut_pending, h->cut_in): every pair is
+// emitted and the bin sort's first pass keeps the front lists' (dkey <=
+// cut[bin], SortFilter), their count left on the device (h->kept, read by
+// gs_last_stats); *pairs and h->stats.pairs are every pair of the frame.
+// tail (optional): queues what reads the lists (per-bin sort, composite ...)
+// right behind them, before the host waits for P, so that the GPU never waits
+// for the host; called again, with the lists, if they are queued again.
+using ListTail = std::function<gs_status(const uint32_t* sorted_vals)>;
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
-                          const uint32_t* carry_dkey = nullptr, const gs::SlabSel* sel = nullptr) {
-    const gs::SlabSel no_sel;
-    const gs::SlabSel& fs = sel ? *sel : no_sel;
+                          const uint32_t* carry_dkey = nullptr, const ListTail* tail = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     const int bits = list_key_bits(U);
     const gs::SortPlan plan = gs::make_sort_plan(bits);
     // the preprocess already summed the scan blocks (render_frame, PreFuse)
-    const bool fused = h->fused_prep.ok && !order && !sel && own.dev.owner == nullptr;
+    const bool fused = h->fused_prep.ok && !order && own.dev.owner == nullptr;
     gs_handle::ListPrep lp = h->fused_prep;
     h->fused_prep.ok = false;
     h->fused_last = fused;
@@ -556,6 +577,16 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     }
     uint32_t cap = lp.cap;
     gs::PassCounts pc = lp.pc;
+    const bool cut_frame = h->cut_pending && h->cut_in && !order && own.dev.owner == nullptr && carry_dkey;
+    gs::SortFilter flt;  // front lists: the pairs at or ahead of their bin's cut
+    if (cut_frame) {
+        GS_HIP(h->kept.reserve(8));
+        flt.cut = h->cut_in;
+        flt.bmask = (1u << bits) - 1u;
+        flt.dshift = bits;
+        flt.kept = h->kept.as<uint32_t>() + h->set;
+        pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
+    }
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
                                               h->partials.as<uint64_t>(), h->dev_total,
@@ -566,7 +597,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                             h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set,
                                             h->ranges.as<uint2>(), T, h->npairs.as<uint32_t>(), cap, pc.C,
-                                            pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, h->totals_ev, fs));
+                                            pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, h->totals_ev));
     }
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
@@ -577,19 +608,33 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc, fs);
+                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
                                      h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap,
                                      bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>(),
-                                     h->npairs.as<uint32_t>(), pc.C != nullptr);
+                                     h->npairs.as<uint32_t>(), pc.C != nullptr, flt);
+    };
+    auto lists_done = [&]() -> gs_status {
+        uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+        uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+        h->last_keys = sk;
+        h->last_vals = sv;
+        h->last_tmp_keys = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
+        h->last_tmp_vals = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+        h->last_key_bits = bits;
+        h->pair_cap = cap;
+        if (timed) mark(h, 5, st);
+        if (timed && !carry_dkey) mark(h, 6, st);  // (ranges come out of the last sort pass)
+        *vals_out = sv;
+        return tail ? (*tail)(sv) : GS_OK;
     };
     GS_HIP(enqueue_lists());
+    gs_status ts = lists_done();
+    if (ts != GS_OK) return ts;
     GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
-    const uint64_t P = h->host_total[0];
-    // two-slab: the pairs of both slabs (the buffers must hold the second's too)
-    const uint64_t P_all = sel ? h->host_total[4] : P;
+    const uint64_t P = h->host_total[0], P_all = P;
     h->stats.visible = (int64_t)h->host_total[1];
     h->stats.pairs = (int64_t)P_all;
     // the last per-bin depth sort's share of pairs in lists too long for LDS
@@ -603,74 +648,74 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
-        pc = pass_counts(h, m, order == nullptr, plan, cap, P);
+        pc = cut_frame ? gs::PassCounts{} : pass_counts(h, m, order == nullptr, plan, cap, P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
+        if (tail) {  // (the no-op frame's composite counted into these)
+            GS_HIP(hipStreamSynchronize(st));
+            GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));
+        }
         GS_HIP(enqueue_lists());
+        if ((ts = lists_done()) != GS_OK) return ts;
     }
-    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
-    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
-    h->last_keys = sk;
-    h->last_vals = sv;
-    h->last_tmp_keys = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
-    h->last_tmp_vals = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
-    h->last_key_bits = bits;
-    if (timed) mark(h, 5, st);
-    if (timed && !carry_dkey) mark(h, 6, st);  // (ranges come out of the last sort pass)
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
-    h->pair_cap = cap;
-    *vals_out = sv;
     *pairs = P;
     return GS_OK;
 }
 
-// Two-slab frames, after the first slab's composite on sc:
-// the duplicate wrote the second slab's pairs (depth keys >= the cut) after
-// all of the first's, [P1, P_all) of the pair arrays.  Those of the bins the
-// first composite left open are kept by the first pass of their sort (the
-// others are dropped), sorted by bin, put in depth order per bin and
-// composited from the saved state.  Nothing here waits for the host: the
-// kept count stays on the device.
-gs_status second_slab(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, hipStream_t sc) {
-    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+// Grows a buffer that kernels queued on `st` may still use: waits for them
+// first (growth frees the old allocation).  Rare: the buffers only grow.
+hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
+    if (bytes <= b.bytes) return hipSuccess;
+    const hipError_t e = hipStreamSynchronize(st);
+    return e != hipSuccess ? e : b.reserve(bytes);
+}
+
+// Depth-cut frames, after the front lists' composite on sc:
+// the fallback lists of the tiles it left open (their bins' pairs behind the
+// cut, dkey > cut[bin]) are emitted, sorted by bin, put in depth order per
+// bin and composited from the saved states.  Nothing waits for the host:
+// every kernel here returns at once when the open tile count is zero, the
+// usual case.  The front lists' buffers are free by then (same stream).
+gs_status cut_fallback(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, hipStream_t sc) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y), m = (uint32_t)h->n;
     const int bits = h->last_key_bits;
-    const uint64_t P1 = h->p1_pairs, Pall = (uint64_t)h->stats.pairs;
-    const uint32_t nfar = (uint32_t)(Pall - P1);
-    mark(h, 10, sc);
-    mark(h, 11, sc);
-    uint32_t* kept = reinterpret_cast<uint32_t*>(h->tot2.as<uint64_t>() + 8 * h->set);  // (read by gs_last_stats)
-    // the first slab's lists and ranges are free now: its composite is done
-    GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), sc));
-    uint32_t *sk = h->keys.as<uint32_t>(), *sv = h->vals.as<uint32_t>();
-    uint32_t *tk = h->tkeys.as<uint32_t>(), *tv = h->tvals.as<uint32_t>();
-    if (nfar == 0) {
-        GS_HIP(hipMemsetAsync(kept, 0, 4, sc));
-    } else {
-        GS_HIP(h->scratch2.reserve(gs::radix_sort_scratch_words(nfar) * 4));
-        gs::SortFilter flt;
-        flt.open = h->open4.as<const uint32_t>();  // (any of a bin's 4 tiles open)
-        flt.bmask = (1u << bits) - 1u;
-        flt.kept = kept;
-        // input [P1, P_all) of keys / vals; the passes write from offset 0 of
-        // the other arrays first, so no pass writes a range another tile of
-        // the same pass still reads (an odd pass count ends in tkeys)
-        if (gs::make_sort_plan(bits).passes % 2 == 1) {
-            std::swap(sk, tk);
-            std::swap(sv, tv);
-        }
-        bool in_tmp = false;
-        GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>() + P1, h->vals.as<uint32_t>() + P1, sk, sv, tk, tv, nfar,
-                                     bits, h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(), nullptr,
-                                     false, flt));
-        if (in_tmp) return fail(GS_ERR_DEVICE, "second slab: unexpected sort buffer");
-    }
-    mark(h, 12, sc);
-    GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), T, sk, sv, tk, tv, bits, nullptr, sc));
-    mark(h, 13, sc);
+    const uint32_t cap = h->pair_cap;
+    const uint32_t nb = (m + gs::kScanItems - 1) / gs::kScanItems;
+    GS_HIP(reserve_after(h->fpart, ((size_t)nb + 1) * 16, sc));
+    GS_HIP(reserve_after(h->fnpairs, 4, sc));
+    GS_HIP(reserve_after(h->scratch2, gs::radix_sort_scratch_words(cap) * 4, sc));
+    GS_HIP(h->tot2.reserve(2 * 64));
+    gs::CutSel fs;
+    fs.mode = 2;
+    fs.dkey = h->dkey.as<uint32_t>();
+    fs.cut = h->cut_in;
+    fs.qrec = h->qrec.as<const uint32_t>();  // (any of a bin's 16 quadrants open)
+    fs.guard = open_counter(h);
+    uint64_t* tot = h->tot2.as<uint64_t>() + 8 * h->set;  // (read by gs_last_stats)
+    uint32_t* np = h->fnpairs.as<uint32_t>();
+    GS_HIP(gs::launch_tile_count_totals(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), m, gs::RowOwnership{nullptr, 0},
+                                        U.cell_mask != 0, h->fpart.as<uint64_t>(), tot, nullptr, h->ranges.as<uint2>(),
+                                        T, np, cap, nullptr, 0, sc, nullptr, fs, (uint32_t)U.tiles_x));
+    GS_HIP(gs::launch_scan_duplicate(nullptr, h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), h->fpart.as<uint64_t>(), m,
+                                     (uint32_t)U.tiles_x, gs::RowOwnership{nullptr, 0}, U.cell_mask != 0,
+                                     h->dkey.as<uint32_t>(), bits, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), np,
+                                     sc, nullptr, gs::PassCounts{}, fs));
+    bool in_tmp = false;
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
+                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap, bits,
+                                 h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(), np, false));
+    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+    uint32_t* tk = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
+    uint32_t* tv = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+    GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), T, sk, sv, tk, tv, bits, nullptr, sc, nullptr,
+                                     open_counter(h)));
     ca.vals = sv;
     ca.ranges = h->ranges.as<uint2>();
     ca.pass = 2;
-    GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 5), kernel_event(h, 3)));
+    ca.fetched = nullptr;
+    GS_HIP(gs::launch_composite(ca, h->opt.mode, sc));
     return GS_OK;
 }
 
@@ -681,9 +726,7 @@ gs_status second_slab(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArg
 gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, const uint32_t* rect_lo,
                              const uint32_t* rect_hi, const float4* rec, int rec_stride, const gs::FrameUniforms& U,
                              int compact, float4* out, uint32_t* out_bgra8, hipStream_t st, float* slab_t = nullptr,
-                             const hipStream_t* composite_stream = nullptr, bool cut_hist = false) {
-    // cut_hist: the preprocess of these items filled the two-slab depth
-    // histogram (local frames with depth_split 0)
+                             const hipStream_t* composite_stream = nullptr) {
     // the composite runs on *composite_stream when given (frames_in_flight 2:
     // the caller's stream, while st is the handle's side stream) once the
     // lists are ready on st.  A pointer, since the caller's stream may be the
@@ -701,7 +744,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
     for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth})
         GS_HIP(b->reserve(mm * 4));
-    GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 16));
+    GS_HIP(h->partials.reserve(((mm + gs::kScanItems - 1) / gs::kScanItems + 1) * 24));
     GS_HIP(h->sort_scratch.reserve(gs::radix_sort_scratch_words((uint32_t)mm) * 4));
     gs::CompositeArgs ca{};
     ca.rec = rec;
@@ -721,13 +764,14 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* vals = nullptr;
     uint64_t P = 0;
     const bool mlab = h->opt.mode == GS_MODE_MLAB;
-    h->two_slab_frame = false;
+    // depth cuts: decided with the fused scan (render_frame); only a bin-first
+    // frame of local splats can carry them
+    const bool cut_ok = h->cut_pending && !slab_t && !compact;
+    h->cut_frame = false;
     if (mlab && (ca.cap > 0 || slab_t))
         return fail(GS_ERR_UNSUPPORTED, "MLAB mode has no fragment cap and no depth slabs");
     if (mlab) {
         // MLAB k-buffer: arrival (index) order per pixel, no depth sort
-        h->kev_two[h->kev_slot] = false;
-        if (cut_hist) GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
         mark(h, 2, st);
         gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P);
         if (s != GS_OK) return s;
@@ -746,80 +790,76 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         // sorted by depth key -> (depth, index) order, the same lists as the
         // depth-first order below.
         h->bin_first_frame = true;
-        // Two depth slabs: first the pairs of the splats below
-        // a depth-key cut, composited with each tile's state kept where a
-        // pixel stays open; then the rest, only for the bins left open.  The
-        // per-pixel operation sequence is the one-slab sequence (same image).
-        static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
-        const bool split_on = ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1;
-        const bool two = split_on && cut_hist && ca.cap == 0 && !slab_t && !out_bgra8 && out &&
-                         (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) && h->ghist.ptr;
-        gs::SlabSel sel1;
-        if (two) {
-            GS_HIP(h->open4.reserve((size_t)U.tiles_x * U.tiles_y * 4));
-            sel1.mode = 1;
-            sel1.dkey = dkey;
-            sel1.kcut = h->kcut.as<uint32_t>() + h->set;
-            sel1.hist = h->ghist.as<uint32_t>();
-            static const char* fr_env = std::getenv("GS_DEPTH_SPLIT_FRAC");
-            sel1.frac = fr_env ? (float)std::atof(fr_env) : kDepthSplitFrac;
-            sel1.zero64 = h->fetch.as<unsigned long long>() + 2 + h->set;
-        }
-        h->two_slab_frame = two;
-        h->kev_two[h->kev_slot] = two;
-        if (cut_hist && !two)  // filled but unused: cleared for the next frame's cut
-            GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
+        // Depth cuts: the lists hold the pairs at or in front
+        // of their bin's cut; the composite keeps the state of each tile they
+        // leave open and raises the bins' cuts for the frame after next, and
+        // the fallback lists finish the open tiles.  The per-pixel operation
+        // sequence is the full lists' (same image, bit for bit).
+        const bool cutf = cut_ok && (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) && ca.cap == 0;
+        h->cut_frame = cutf;
         mark(h, 2, st);
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey,
-                                      two ? &sel1 : nullptr);
-        if (s != GS_OK) return s;
-        h->order.sample_pairs = P;
-        h->p1_pairs = P;
-        ca.vals = vals;
-        ca.ranges = h->ranges.as<uint2>();
         // (the per-bin sort stays on the side stream: on the composite stream,
         // beside the next frame's projection, it was starved)
         const hipStream_t sd = st;
-        if (ca.cap > 0) {  // per-pixel cap thresholds from the lists in arrival order
-            GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
-            ca.thr_out = h->thr.as<uint32_t>();
-            GS_HIP(gs::launch_cap_threshold(ca, sd));
-            ca.thr = h->thr.as<uint32_t>();
-        }
-        // (one sample word pair per buffer set)
-        GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
-                                         h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
-                                         h->seg_sample.as<uint32_t>() + 2 * h->set, sd,
-                                         sc != st ? h->sorted_ev : nullptr));
-        mark(h, 6, sd);
         if (slab_t) {
             ca.slab = 1;
             ca.t_out = slab_t;
         }
-        GS_HIP(handoff(true));
         ca.fetched = fetch_counter(h);
-        if (two) {
+        if (cutf) {
             ca.pass = 1;
-            ca.open4 = h->open4.as<uint8_t>();
-            ca.open_tiles = h->fetch.as<unsigned long long>() + 2 + h->set;
+            ca.qrec = h->qrec.as<uint32_t>();
+            ca.open_q_count = open_counter(h);
+            ca.state = h->cstate.as<float4>();
+            ca.cut_in = h->cut_in;
         }
-        GS_HIP(gs::launch_composite(ca, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, two ? 4 : 3)));
-        if (slab_t) {
-            h->slab_ca = ca;
-            h->slab_lists = true;
+        // everything that reads the lists, queued before the host waits for P
+        const ListTail tail = [&](const uint32_t* sv) -> gs_status {
+            gs::CompositeArgs c = ca;
+            c.vals = sv;
+            c.ranges = h->ranges.as<uint2>();
+            if (c.cap > 0) {  // per-pixel cap thresholds from the lists in arrival order
+                GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
+                c.thr_out = h->thr.as<uint32_t>();
+                GS_HIP(gs::launch_cap_threshold(c, sd));
+                c.thr = h->thr.as<uint32_t>();
+            }
+            // (one sample word pair per buffer set; a depth-cut frame's per-bin
+            // sort also clears the table its composite raises)
+            GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
+                                             h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
+                                             h->seg_sample.as<uint32_t>() + 2 * h->set, sd,
+                                             sc != st ? h->sorted_ev : nullptr));
+            mark(h, 6, sd);
+            GS_HIP(handoff(true));
+            GS_HIP(gs::launch_composite(c, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
+            if (slab_t) {
+                h->slab_ca = c;
+                h->slab_lists = true;
+            }
+            // the next cuts of this set, then the fallback lists, only if some
+            // list was cut (null cuts: every pair is in the front lists, no
+            // quadrant can be left open)
+            if (cutf)
+                GS_HIP(gs::launch_cut_finalize(c.qrec, sv, dkey, h->cut_out, (uint32_t)(U.tiles_x * U.tiles_y),
+                                               cut_margin(), sc));
+            if (cutf && h->cut_in) {
+                gs_status fs_ = cut_fallback(h, U, c, sc);
+                if (fs_ != GS_OK) return fs_;
+            }
+            mark(h, 7, sc);
+            return GS_OK;
+        };
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey, &tail);
+        if (s != GS_OK) return s;
+        h->order.sample_pairs = P;
+        if (cutf) {  // this frame's cuts are read by its set's next frame
+            h->cut_phase[h->set] ^= 1;
+            h->cut_valid[h->set] = true;
         }
-        if (two) {
-            mark(h, 9, sc);
-            if ((s = second_slab(h, U, ca, sc)) != GS_OK) return s;
-        }
-        mark(h, 7, sc);
-        if (!two) h->stats.pairs = (int64_t)P;  // (two slabs: both slabs' pairs, build_bin_lists)
         return GS_OK;
     }
     h->bin_first_frame = false;
-    h->kev_two[h->kev_slot] = false;
-    if (cut_hist)  // (depth-first frames take no cut: the histogram is cleared for the next frame's)
-        GS_HIP(hipMemsetAsync(h->ghist.ptr, 0, (size_t)gs::kCutCopies * gs::kCutBuckets * 4, st));
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
@@ -903,19 +943,10 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_composite = h->stats_fixed_bytes + 4 * Pi * (4 + 48);
     s.records_fetched = -1;
     s.pairs_sorted = Pi;
-    s.two_slab = h->two_slab_frame ? 1 : 0;
-    if (h->two_slab_frame) {
-        // first slab: its pairs through duplicate, sort and per-bin sort; the
-        // scan also reads the depth keys.  The second slab's share (read
-        // lazily with the fetch counter, gs_last_stats) is added there.
-        const int64_t P1 = (int64_t)h->p1_pairs;
-        s.pairs_sorted = P1;
-        s.bytes_scan = N * 12 + T * 8;
-        s.bytes_duplicate = N * 12 + Pi * 8;  // (both slabs' pairs)
-        s.bytes_sort = P1 * 20 * (int64_t)s.sort_passes;
-        s.bytes_depth_sort = P1 * 12;
-        h->stats_fixed_bytes += 4 * T * 8;  // the second composite reads its ranges too
-    }
+    s.two_slab = h->cut_frame ? 1 : 0;
+    h->cut_lists = h->cut_frame && h->cut_in;
+    // (depth-cut frames with cuts: the first sort pass reads every pair, keeps
+    // the front lists' P1; the rest runs on P1 -- set by gs_last_stats)
     // stage_timing 2: read lazily (gs_last_stats / gs_kernel_times), so a
     // frame never waits for itself
     if (h->opt.stage_timing == 2 && h->events) {
@@ -937,13 +968,6 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         }
         s.ms_composite = elapsed(h, 6, 7);
         s.ms_total = elapsed(h, 0, 7);
-        if (h->two_slab_frame) {  // the second slab's lists ran between the two composites
-            s.ms_composite = elapsed(h, 6, 9) + elapsed(h, 13, 7);
-            s.ms_scan += elapsed(h, 9, 10);
-            s.ms_duplicate += elapsed(h, 10, 11);
-            s.ms_sort += elapsed(h, 11, 12);
-            s.ms_depth_sort += elapsed(h, 12, 13);
-        }
     }
 }
 
@@ -1225,10 +1249,6 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     }
     h->last_pipe = pipe;
     begin_frame(h, sp);
-    // (two-slab frames: the depth histogram of the cut rides on the preprocess)
-    static const char* ds_env = std::getenv("GS_DEPTH_SPLIT");
-    const bool split_on = ds_env ? ds_env[0] == '1' : h->opt.depth_split == 1;
-    uint32_t* hist = split_on && !bgra8 && h->ghist.ptr ? h->ghist.as<uint32_t>() : nullptr;
     // Bin-first frames of one GPU: the preprocess also sums every scan
     // block's pairs, fills the empty bin ranges and zeroes the first sort
     // pass's counts (PreFuse), so the chain starts at the scan of the block
@@ -1236,11 +1256,42 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     // GS_FUSED_SCAN=0: the separate reduce pass (A/B).
     static const char* fs_env = std::getenv("GS_FUSED_SCAN");
     gs::PreFuse fuse;
-    h->fused_prep.ok = false;
+    h->fused_prep = gs_handle::ListPrep{};
     h->order_pick = -1;
-    if (!band && h->world == 1 && !hist && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
+    // A set's cut tables hold cuts only from a depth-cut frame at this frame
+    // size and composite rule; any other frame on the set invalidates them.
+    const bool cut_on = depth_cuts_on(h) && !band && h->world == 1 && h->opt.cap == 0 &&
+                        (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50);
+    if (h->cut_w != W || h->cut_h != H || h->cut_mode != h->opt.mode) {
+        h->cut_valid[0] = h->cut_valid[1] = false;
+        h->cut_w = W;
+        h->cut_h = H;
+        h->cut_mode = h->opt.mode;
+    }
+    bool cut_frame = false;
+    h->cut_pending = false;
+    h->cut_in = h->cut_out = nullptr;
+    if (!band && h->world == 1 && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
         const bool bf = bin_first_order(h, U, (uint32_t)h->n);
         h->order_pick = bf ? 1 : 0;
+        cut_frame = bf && cut_on;
+        if (cut_frame) {
+            // two tables per set (cutbuf), the per-tile open flags of the set,
+            // the open tiles' pixel states (composite stream)
+            if (h->cut_bins < T) {
+                GS_HIP(hipStreamSynchronize(st));
+                GS_HIP(hipStreamSynchronize(sp));
+                GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
+                h->cut_bins = T;
+                h->cut_valid[0] = h->cut_valid[1] = false;
+            }
+            GS_HIP(h->qrec.reserve((size_t)T * gs::kQrecWords * 4));
+            GS_HIP(reserve_after(h->cstate, (size_t)W * H * 16, st));
+            h->cut_in = h->cut_valid[h->set] ? h->cut_table(h->set, 0) : nullptr;
+            h->cut_out = h->cut_table(h->set, 1);
+            h->cut_valid[h->set] = false;  // (true again once this frame's composite is queued)
+            h->cut_pending = true;
+        }
         if (bf) {
             if ((s = prepare_lists(h, (uint32_t)h->n, true, U, &h->fused_prep)) != GS_OK) return s;
             const uint32_t nb = (uint32_t)((h->n + gs::kScanItems - 1) / gs::kScanItems);
@@ -1253,21 +1304,22 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             fuse.nb = nb;
             fuse.fill = h->ranges.as<uint2>();
             fuse.nfill = T;
+            if (h->cut_in) h->fused_prep.pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
             fuse.zero = h->fused_prep.pc.C;
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
             h->fused_prep.ok = true;
             h->ppart_dirty = true;  // (until its scan is queued)
         }
     }
+    if (!cut_frame) h->cut_valid[h->set] = false;
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h), hist, fuse));
+                                 kernel_event(h, 1), fetch_counter(h), fuse));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), gs::kRecFloat4, U, compact,
                                 bgra8 ? nullptr : static_cast<float4*>(out),
-                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st,
-                                hist != nullptr)) != GS_OK)
+                                bgra8 ? static_cast<uint32_t*>(out) : nullptr, sp, nullptr, &st)) != GS_OK)
         return s;
     GS_HIP(hipEventRecord(h->set_free[h->set], st));  // this set's last reader
     const uint64_t P = (uint64_t)h->stats.pairs;
@@ -1305,28 +1357,39 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
         unsigned long long v = 0;
         GS_HIP(hipSetDevice(h->device));
         GS_HIP(hipEventSynchronize(h->set_free[h->stats_set]));
-        GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + h->stats_set, 8, hipMemcpyDeviceToHost));
+        GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + 2 * h->stats_set, 8, hipMemcpyDeviceToHost));
         h->stats.records_fetched = (int64_t)v;
         h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
         if (h->stats.two_slab) {
-            // the second slab: the pairs its filtered sort kept (of all it
-            // read), the open tiles (each resumed from and written back as
-            // 16-B pixel states), the cut
-            unsigned long long open = 0;
-            uint32_t kept = 0, K = 0;
-            GS_HIP(hipMemcpy(&open, h->fetch.as<unsigned long long>() + 2 + h->stats_set, 8, hipMemcpyDeviceToHost));
-            GS_HIP(hipMemcpy(&kept, h->tot2.as<uint64_t>() + 8 * h->stats_set, 4, hipMemcpyDeviceToHost));
-            GS_HIP(hipMemcpy(&K, h->kcut.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
+            // depth cuts: the front lists' pairs (the first sort pass reads all
+            // P, counting and scattering, and writes the kept P1; the second
+            // pass and the per-bin sort run on P1); the tiles those lists left
+            // open and the pairs of their fallback lists (emitted, sorted,
+            // per-bin sorted; each open tile's 256 pixel states written and
+            // read back)
             gs_stats& s = h->stats;
-            const int64_t P2 = (int64_t)kept, Pfar = s.pairs - s.pairs_sorted;
+            if (h->cut_lists) {
+                uint32_t k1 = 0;
+                GS_HIP(hipMemcpy(&k1, h->kept.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
+                const int64_t P = s.pairs, P1 = (int64_t)k1;
+                s.pairs_sorted = P1;
+                s.bytes_sort = P * 12 + P1 * 8 + P1 * 20 * (int64_t)(s.sort_passes - 1);
+                s.bytes_depth_sort = P1 * 12;
+            }
+            unsigned long long open = 0;
+            uint64_t P2 = 0;
+            GS_HIP(hipMemcpy(&open, h->fetch.as<unsigned long long>() + 2 * h->stats_set + 1, 8,
+                             hipMemcpyDeviceToHost));
+            if (open) GS_HIP(hipMemcpy(&P2, h->tot2.as<uint64_t>() + 8 * h->stats_set, 8, hipMemcpyDeviceToHost));
             s.open_tiles = (int64_t)open;
-            s.depth_cut = K;
-            s.pairs_sorted += P2;
-            // filtered first pass: every second-slab key counted and read
-            // with its value, the kept pairs written; the later passes as usual
-            s.bytes_sort += Pfar * 12 + P2 * 8 + P2 * 20 * (int64_t)(s.sort_passes - 1);
-            s.bytes_depth_sort += P2 * 12;
-            s.bytes_composite += (int64_t)open * gs::kTileThreads * 32;
+            s.pairs_sorted += (int64_t)P2;
+            if (open) {
+                s.bytes_scan += s.splats * 12;
+                s.bytes_duplicate += s.splats * 12 + (int64_t)P2 * 8;
+                s.bytes_sort += (int64_t)P2 * 20 * (int64_t)s.sort_passes;
+                s.bytes_depth_sort += (int64_t)P2 * 12;
+                s.bytes_composite += (int64_t)open * 64 * 32;  // (8x8 quadrants)
+            }
         }
     }
     *out = h->stats;
@@ -1390,8 +1453,8 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
 
 gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int64_t cap, int64_t* count) {
     if (!h || !count) return fail(GS_ERR_INVALID_ARG, "null argument");
-    if (h->two_slab_frame)
-        return fail(GS_ERR_UNSUPPORTED, "the last frame's lists were built in two depth slabs (depth_split = 1 keeps one)");
+    if (h->cut_frame)
+        return fail(GS_ERR_UNSUPPORTED, "the last frame's lists were cut at per-bin depths (depth_split = 0 keeps them whole)");
     int64_t P = h->stats.pairs;
     *count = P;
     if (!h->last_keys || P == 0) return GS_OK;
@@ -1405,36 +1468,6 @@ gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int
         for (int64_t i = 0; i < m; ++i) keys[i] &= mask;
     }
     if (vals) GS_HIP(hipMemcpy(vals, h->last_vals, (size_t)m * 4, hipMemcpyDeviceToHost));
-    return GS_OK;
-}
-
-gs_status gs_radix_sort_pairs_filtered(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
-                                       uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, int64_t n, int32_t bits,
-                                       const uint32_t* open, int64_t* kept, void* stream) {
-    if (n < 0 || n >= (int64_t)UINT32_MAX || bits < 1 || bits > 16 || !open || !kept ||
-        (n > 0 && (!keys_in || !vals_in || !keys || !vals || !tmp_keys || !tmp_vals)))
-        return fail(GS_ERR_INVALID_ARG, "gs_radix_sort_pairs_filtered: bad arguments");
-    *kept = 0;
-    if (n == 0) return GS_OK;
-    if (keys_in == keys || keys_in == tmp_keys || vals_in == vals || vals_in == tmp_vals)
-        return fail(GS_ERR_INVALID_ARG, "gs_radix_sort_pairs_filtered: the input aliases an output");
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    uint32_t* scratch = nullptr;
-    GS_HIP(hipMalloc(&scratch, (gs::radix_sort_scratch_words((uint32_t)n) + 1) * 4));
-    gs::SortFilter flt;
-    flt.open = open;
-    flt.bmask = (1u << bits) - 1u;
-    flt.kept = scratch + gs::radix_sort_scratch_words((uint32_t)n);
-    bool in_tmp = false;
-    hipError_t e = gs::launch_radix_sort(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, (uint32_t)n, bits, scratch,
-                                         &in_tmp, st, nullptr, nullptr, false, flt);
-    uint32_t k = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(&k, flt.kept, 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(scratch);
-    GS_HIP(e);
-    if (in_tmp) return fail(GS_ERR_DEVICE, "gs_radix_sort_pairs_filtered: unexpected sort buffer");
-    *kept = k;
     return GS_OK;
 }
 

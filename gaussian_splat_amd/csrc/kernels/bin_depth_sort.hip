@@ -236,10 +236,12 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
                                                                   uint32_t* __restrict__ vals,
                                                                   uint32_t* __restrict__ tmp_keys,
                                                                   uint32_t* __restrict__ tmp_vals, int bin_bits,
-                                                                  uint32_t* __restrict__ sample) {
+                                                                  uint32_t* __restrict__ sample,
+                                                                  const unsigned long long* __restrict__ guard) {
     static_assert((uint32_t)NT * IPT <= (1u << kSegPosBits), "position field");
     __shared__ SegRankLds<NT> L;
     __shared__ uint32_t stage[NT * IPT];
+    if (guard && *guard == 0ull) return;  // (whole grid: the fallback lists of a frame with no open tile)
     const uint2 rg = decode_range(ranges[blockIdx.x]);
     const uint32_t m = rg.y > rg.x ? rg.y - rg.x : 0u;
     if (sample && threadIdx.x == 0) {  // for the host's choice of binning order
@@ -312,13 +314,13 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
 
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
-                                 hipStream_t st, hipEvent_t done) {
+                                 hipStream_t st, hipEvent_t done, const unsigned long long* guard) {
     if (nbins == 0) return done ? hipEventRecord(done, st) : hipSuccess;
     if (bin_bits < 0 || bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     // one workgroup per bin
     static_assert(GS_SEG_NT * GS_SEG_IPT == kSegLdsMax, "gs_kernels.h");
     hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>), dim3(nbins), dim3(GS_SEG_NT), 0,
-                          st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample);
+                          st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample, guard);
     return hipGetLastError();
 }
 

@@ -20,62 +20,11 @@
 // one XCD and share the bin's list through its L2.
 #include <hip/hip_ext.h>
 
+
 #include "gs_kernels.h"
 #include "gs_wave.h"
 
 namespace gs {
-
-#ifdef GS_COMPOSITE_COUNTERS
-// Debug build only (-DGS_COMPOSITE_COUNTERS): per-wave work counters.
-__device__ unsigned long long g_cc[20];
-__device__ uint32_t g_tile_fetch[1u << 16];  // per tile (bin * 4 + tile of the bin): records fetched
-#define GS_CC(i, v) (void)atomicAdd(&g_cc[i], (unsigned long long)(v))
-#else
-#define GS_CC(i, v) (void)0
-#endif
-#ifdef GS_COMPOSITE_TIMERS
-// Debug build only (-DGS_COMPOSITE_TIMERS): shader-clock cycles per wave
-// spent in each phase of the batch loop, summed over waves (tools/composite_counters.py).
-__device__ unsigned long long g_ct[8];
-#define GS_CT_DECL unsigned long long ct_acc[6] = {0, 0, 0, 0, 0, 0}, ct_t = clock64(), ct_t0 = ct_t
-#define GS_CT(i)                                   \
-    do {                                           \
-        const unsigned long long ct_n = clock64(); \
-        ct_acc[i] += ct_n - ct_t;                  \
-        ct_t = ct_n;                               \
-    } while (0)
-#define GS_CT_FLUSH()                                                                            \
-    do {                                                                                         \
-        if (lane == 0) {                                                                         \
-            for (int ci = 0; ci < 6; ++ci) (void)atomicAdd(&g_ct[ci], ct_acc[ci]);               \
-            (void)atomicAdd(&g_ct[6], clock64() - ct_t0);                                        \
-            (void)atomicAdd(&g_ct[7], 1ull);                                                     \
-        }                                                                                        \
-    } while (0)
-#else
-#define GS_CT_DECL (void)0
-#define GS_CT(i) (void)0
-#define GS_CT_FLUSH() (void)0
-#endif
-#ifdef GS_COMPOSITE_TRACE
-// Debug build only (-DGS_COMPOSITE_TRACE): per wave {start, end} realtime
-// (100 MHz), HW_ID and XCC_ID, for the occupancy / tail analysis of
-// tools/composite_trace.py.
-constexpr uint32_t kTraceMax = 1u << 18;
-__device__ uint4 g_trace[kTraceMax];
-#define GS_TR_DECL const uint32_t tr_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime()
-#define GS_TR_FLUSH()                                                                                    \
-    do {                                                                                                 \
-        const uint32_t tr_t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();                              \
-        const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);                                      \
-        if ((threadIdx.x & 63u) == 0 && slot < kTraceMax)                                                \
-            g_trace[slot] = make_uint4(tr_t0, tr_t1, __builtin_amdgcn_s_getreg((31 << 11) | 4),          \
-                                       __builtin_amdgcn_s_getreg((31 << 11) | 20));                      \
-    } while (0)
-#else
-#define GS_TR_DECL (void)0
-#define GS_TR_FLUSH() (void)0
-#endif
 
 // MLAB k-buffer (gaussian_splat.metal:201-361): six premultiplied half
 // layers + half depths per pixel in registers, updated per covering fragment
@@ -171,36 +120,39 @@ __device__ __forceinline__ const StagedRec& staged_at(const StagedRec* base, uin
     return *reinterpret_cast<const StagedRec*>(reinterpret_cast<const char*>(base) + off);
 }
 
-// PASS (two-slab frames; modes 0/1, no cap, fp32 output):
-// 1 = the first slab, leaving the state (C, T) of every tile with an open
-// pixel; 2 = the second slab, resuming those tiles only.
+// PASS (depth-cut frames, gs_options.depth_split; modes 0/1,
+// no cap, no slabs): 1 = the front lists (CompositeArgs: a tile left open
+// with a cut list keeps its per-pixel state, every tile raises its bin's next
+// cut); 2 = the fallback lists, resuming the open tiles only.
+//
+// SGPR budget: at most 62 (TotalSGPRs <= 64, tests/test_kernel_resources.py).
+// gfx950 allocates a wave's SGPRs in blocks of 16 (plus 16), from 800 per
+// SIMD, and the composite shares its SIMDs with the preprocess kernel
+// (96-SGPR class) in the pipelined frame.  Left alone the pass-1 kernel takes
+// 68-76 SGPRs (the 96 class, against 80 for pass 0): standalone no slower,
+// but in the co-run with the preprocess its span grew 0.445 -> 0.527 ms and
+// the frame 0.687 -> 0.738 ms (profiles/r04/ab_composite_sgpr.txt).  The cap
+// costs pass 1 one spilled dword (stored at entry, reloaded at the end).
+#define GS_COMPOSITE_SGPRS 62
 template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
-__global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(CompositeArgs a, uint32_t nwg) {
+__global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_sgpr(GS_COMPOSITE_SGPRS))) void composite_kernel(CompositeArgs a, uint32_t nwg) {
     constexpr bool kIds = CAP || MODE == 2;  // the body needs the splat id
-    static_assert(PASS == 0 || ((MODE == 0 || MODE == 1) && !CAP && SLAB == 0), "two-slab passes: tile/live50 rules");
+    static_assert(PASS == 0 || ((MODE == 0 || MODE == 1) && !CAP && SLAB == 0), "depth-cut passes: tile/live50 rules");
     __shared__ StagedRec srec[kTileThreads];
     __shared__ uint16_t wlist[4][kTileThreads];  // per wave: slot byte offsets
     __shared__ uint8_t sqm[kTileThreads];  // per staged record: the quadrants it may reach
     __shared__ uint32_t sopen[4];          // per wave: pixels still open after its last walk
-    __shared__ uint32_t sopen_end[4];      // (PASS 1) the same at the end of the list
 
     // XCD-aware bijective remap (blocks b and b+8 share an XCD,
-    // cdna_hip_programming.md §5, T1).
-    GS_TR_DECL;
+    // cdna_hip_programming.md §5, T1): bins dealt round-robin over the XCDs,
+    // a bin's 4 tiles on one XCD (they share its list through that L2).
+    // Measured against giving each XCD a contiguous band of bin rows: -2 %
+    // composite, since the bands' costs differ and the launch ends with the
+    // slowest XCD.
     const uint32_t orig = blockIdx.x;
-#if defined(GS_XCD_MAP) && GS_XCD_MAP == 0
-    // A/B: each XCD a contiguous run of tiles (a band of bin rows)
-    const uint32_t xcd = orig & 7u, q8 = nwg >> 3, r8 = nwg & 7u;
-    const uint32_t wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-#else
-    // Bins dealt round-robin over the XCDs, a bin's 4 tiles on one XCD (they
-    // share its list through that L2).  Measured against giving each XCD a
-    // contiguous band of bin rows: -2 % composite, since the bands' costs
-    // differ and the launch ends with the slowest XCD.
     const uint32_t full = nwg & ~31u;
     const uint32_t kk = orig >> 3;
     const uint32_t wg = orig < full ? 32u * (kk >> 2) + 4u * (orig & 7u) + (kk & 3u) : orig;
-#endif
 
     // Grid covers only the owned bin rows.  The four 16x16
     // tiles of a bin are consecutive workgroups (same XCD / L2).
@@ -211,13 +163,21 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     const int by = a.rows ? (int)a.rows[owned_row] : owned_row;
     const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
     const int width = a.width, height = a.height;
-    const uint32_t tile_flag = (uint32_t)(by * a.tiles_x + bx) * 4u + (k4 & 3u);  // (two-slab open4 slot)
+    const uint32_t bin = (uint32_t)(by * a.tiles_x + bx);
+    // (depth cuts: the bin's 128-B quadrant record, CompositeArgs::qrec; this
+    // tile's quadrants are [4 (k4 & 3), +4))
+    uint32_t* const qr = a.qrec ? a.qrec + (size_t)bin * kQrecWords : nullptr;
+    const uint32_t tq = (k4 & 3u) * 4u;
+    uint4 oq = make_uint4(0u, 0u, 0u, 0u);  // (PASS 2) the tile's open quadrants
     if constexpr (PASS == 2) {
-        if (a.open4[tile_flag] == 0) return;  // (whole workgroup) every pixel finished in the first slab
+        oq = *reinterpret_cast<const uint4*>(qr + 16u + tq);
+        if ((oq.x | oq.y | oq.z | oq.w) == 0u) return;  // (whole workgroup) the front list finished the tile
     }
     const int tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63;
+    // PASS 1: the bin's list was cut (a quadrant left open keeps its state)
+    const bool trunc = PASS == 1 && a.cut_in && a.cut_in[bin] < kDepthInf;
     // this wave's quadrant: pixels [tx0 + ox, +7] x [ty0 + oy, +7]
     const uint32_t tx0 = (uint32_t)(tx * kTile), ty0 = (uint32_t)(ty * kTile);
     const uint32_t lxi = (wave & 1u) * 8u + (lane & 7u), lyi = (wave >> 1) * 8u + (lane >> 3);
@@ -230,7 +190,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
 
     // (a tile wholly outside the frame, the last bin row's lower half, has
     // nothing to composite)
-    uint2 rg = decode_range(a.ranges[by * a.tiles_x + bx]);
+    uint2 rg = decode_range(a.ranges[bin]);
     if (tx0 >= (uint32_t)width || ty0 >= (uint32_t)height) rg.y = rg.x;
     // Pixels outside the frame start finished (T = 0): for the tile and live50
     // rules "finished" is then just the break test on T itself, so no
@@ -239,9 +199,14 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     // compact = owned bin rows stacked (multi-GPU band buffer)
     const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
+    const size_t pix = (size_t)py * width + px;
+    // PASS 2: this quadrant was left open by the front list (else its pixels
+    // start finished, and were written already)
+    const bool resumed = PASS == 2 && (wave == 0 ? oq.x : wave == 1 ? oq.y : wave == 2 ? oq.z : oq.w) != 0u;
     if constexpr (PASS == 2) {
-        if (inside) {  // the state the first slab left: the same registers, resumed
-            const float4 st = a.out[(size_t)orow * width + px];
+        T = 0.0f;
+        if (inside && resumed) {  // the state the front list left: the same registers, resumed
+            const float4 st = a.state[pix];
             C0 = st.x;
             C1 = st.y;
             C2 = st.z;
@@ -249,19 +214,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         }
     }
     bool done = !inside;  // MODE 2 / 3
-#ifdef GS_COMPOSITE_COUNTERS
-    uint32_t cc_n4 = 0, cc_n2 = 0, cc_nl = 0;
-    uint32_t cc_b4 = 0, cc_bl = 0, cc_br = 0, cc_be = 0;  // per batch
-    __shared__ uint16_t cc_bmr[kTileThreads], cc_bme[kTileThreads];
-    // this lane's 4x4 block of the tile (bit row * 4 + column) and its lane group
-    const uint32_t cc_blk = ((wave >> 1) * 2u + (lane >> 5)) * 4u + (wave & 1u) * 2u + ((lane >> 2) & 1u);
-    const uint64_t cc_g4 = ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) &
-                           ((lane & 4u) ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full);
-#endif
     uint32_t thr = 0xFFFFFFFFu;  // CAP: last admitted id; MODE 2: result
     int cnt = 0;                 // MODE 2: covering fragments seen
     if constexpr (CAP) {
-        if (inside) thr = a.thr[(size_t)py * width + px];
+        if (inside) thr = a.thr[pix];
     }
     // slab colour pass: the state the earlier (farther) slabs leave, exactly
     // the ordered product of their transmittance, rank order = depth order
@@ -281,28 +237,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         else if constexpr (MODE == 1) return T < kTMin;
         else return done;
     };
-#ifdef GS_COMPOSITE_COUNTERS
-    auto cc_rec = [&](uint32_t off) {
-        const uint32_t k = off / (uint32_t)sizeof(StagedRec);
-        const bool gopen = (__ballot(!finished()) & cc_g4) != 0;
-        cc_br += (gopen && ((cc_bmr[k] >> cc_blk) & 1u)) ? 1u : 0u;
-        cc_be += (gopen && ((cc_bme[k] >> cc_blk) & 1u)) ? 1u : 0u;
-    };
-    auto cc_batch = [&]() {
-        if constexpr (MODE == 0) {
-            uint32_t x[4] = {cc_b4, cc_bl, cc_br, cc_be};
-            for (int o = 32; o > 0; o >>= 1)
-                for (int q = 0; q < 4; ++q) x[q] = max(x[q], (uint32_t)__shfl_xor((int)x[q], o, 64));
-            if (lane == 0) {
-                GS_CC(1, x[0]);
-                GS_CC(2, x[1]);
-                GS_CC(14, x[2]);
-                GS_CC(15, x[3]);
-            }
-        }
-        cc_b4 = cc_bl = cc_br = cc_be = 0;
-    };
-#endif
 
     // One record at this lane's pixel: coverage (K6 closed form: the quad box
     // |uv| <= 3 and the 0.01 cutoff, tile.metal:142-156,191-195), then the
@@ -327,27 +261,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         } else {
             bool in = !finished() && covered;
             if constexpr (CAP) in = in && id <= thr;
-#ifdef GS_COMPOSITE_COUNTERS
-            {
-                const uint64_t m = __ballot(in);
-                if (lane == 0 && m) GS_CC(4, 1);
-                if (lane == 0) GS_CC(7, __popcll(m));
-                // footprint estimates: open / covered lanes per body, and per
-                // 4x4 / 8x4 lane group the bodies it would walk (covered lane
-                // and an open lane in the group), per lane its own walk
-                const uint64_t mo = __ballot(!finished()), mc = __ballot(covered);
-                if (lane == 0) GS_CC(8, __popcll(mo));
-                if (lane == 0) GS_CC(9, __popcll(mc));
-                const uint64_t g4 = ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull) &
-                                    ((lane & 4u) ? 0xF0F0F0F0F0F0F0F0ull : 0x0F0F0F0F0F0F0F0Full);
-                const uint64_t g2 = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
-                cc_n4 += ((mo & g4) && (mc & g4)) ? 1u : 0u;
-                cc_n2 += ((mo & g2) && (mc & g2)) ? 1u : 0u;
-                cc_nl += in ? 1u : 0u;
-                cc_b4 += ((mo & g4) && (mc & g4)) ? 1u : 0u;
-                cc_bl += in ? 1u : 0u;
-            }
-#endif
             if (in) {
                 const float alpha = bb.z * gs_gauss2(qq);
                 if constexpr (MODE == 0) {
@@ -405,18 +318,12 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         gather(id_cur);
         id_next = a.vals[j + kTileThreads < last ? j + kTileThreads : last];
     }
-    if (lane == 0) GS_CC(0, 1);
-    if (tid == 0) GS_CC(6, rg.y - rg.x);
     // records this workgroup fetched: the first batch, then one prefetched
     // batch per batch it composites (the early-out stops both)
     const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;  // (empty bins: {~0, 0})
     uint32_t fetched = len < (uint32_t)kTileThreads ? len : (uint32_t)kTileThreads;
-    GS_CT_DECL;
+    uint32_t wend = 0u;  // (PASS 1) end of the last batch this wave walked with an open pixel
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
-        GS_CT(5);
-#ifdef GS_AB_SYNC_COUNT
-        if (__syncthreads_count(!finished()) == 0) break;
-#else
         // every wave publishes whether it still has open pixels; one LDS
         // barrier both orders that and frees the slots of the last batch
         // (__syncthreads_count takes three)
@@ -427,13 +334,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             const uint4 o = *reinterpret_cast<const uint4*>(sopen);
             if ((o.x | o.y | o.z | o.w) == 0u) break;
         }
-#endif
-        GS_CT(0);
         if (rg.y - b > (uint32_t)kTileThreads) {
             const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
             fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
         }
-        if (tid == 0) GS_CC(5, 1);
         // the wave's gathered chunks into their records' slots (raw layout)
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -454,57 +358,27 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             if constexpr (kIds) sid = id_cur;
             if constexpr (MODE == 3) shd = kDepthInf - a.dkey[id_cur];  // half(zF) (dkey = 0x7C00 - half bits)
             st.c = make_float4(r2.x, r2.y, __uint_as_float(sid), __uint_as_float(shd));
-            {
-                // which of the tile's 8x8 quadrants (wave w: column w & 1, row
-                // w >> 1) the record's rect reaches and its cell mask does not
-                // rule out: computed once here instead of by every wave
-                const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
-                const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
-                const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
-                const bool c0 = !(x1 < tx0 || x0 > tx0 + 7u), c1 = !(x1 < tx0 + 8u || x0 > tx0 + 15u);
-                const bool w0 = !(y1 < ty0 || y0 > ty0 + 7u), w1 = !(y1 < ty0 + 8u || y0 > ty0 + 15u);
-                uint32_t qm = (uint32_t)(c0 && w0) | (uint32_t)(c1 && w0) << 1 | (uint32_t)(c0 && w1) << 2 |
-                              (uint32_t)(c1 && w1) << 3;
-                if (a.cell_mask && qm) {
-                    const uint32_t cm = rect_cell_mask(wlo, whi);
+            // which of the tile's 8x8 quadrants (wave w: column w & 1, row
+            // w >> 1) the record's rect reaches and its cell mask does not
+            // rule out: computed once here instead of by every wave
+            const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
+            const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
+            const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
+            const bool c0 = !(x1 < tx0 || x0 > tx0 + 7u), c1 = !(x1 < tx0 + 8u || x0 > tx0 + 15u);
+            const bool w0 = !(y1 < ty0 || y0 > ty0 + 7u), w1 = !(y1 < ty0 + 8u || y0 > ty0 + 15u);
+            uint32_t qm = (uint32_t)(c0 && w0) | (uint32_t)(c1 && w0) << 1 | (uint32_t)(c0 && w1) << 2 |
+                          (uint32_t)(c1 && w1) << 3;
+            if (a.cell_mask && qm) {
+                const uint32_t cm = rect_cell_mask(wlo, whi);
 #pragma unroll
-                    for (uint32_t w = 0; w < 4; ++w) {
-                        const uint32_t dcx = (tx0 >> 3) + (w & 1u) - (x0 >> 3), dcy = (ty0 >> 3) + (w >> 1) - (y0 >> 3);
-                        if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) qm &= ~(1u << w);
-                    }
+                for (uint32_t w = 0; w < 4; ++w) {
+                    const uint32_t dcx = (tx0 >> 3) + (w & 1u) - (x0 >> 3), dcy = (ty0 >> 3) + (w >> 1) - (y0 >> 3);
+                    if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) qm &= ~(1u << w);
                 }
-                sqm[tid] = (uint8_t)qm;
-#ifdef GS_COMPOSITE_COUNTERS
-                {
-                    const uint32_t cm = a.cell_mask ? rect_cell_mask(wlo, whi) : 0u;
-                    const float eu = 1.5f * (fabsf(st.a.z) + fabsf(st.a.w)), ev = 1.5f * (fabsf(st.b.x) + fabsf(st.b.y));
-                    uint32_t bmr = 0, bme = 0;
-                    for (uint32_t j = 0; j < 4; ++j)
-                        for (uint32_t i = 0; i < 4; ++i) {
-                            const uint32_t bx0 = tx0 + 4u * i, by0 = ty0 + 4u * j;
-                            bool hit = !(x1 < bx0 || x0 > bx0 + 3u) && !(y1 < by0 || y0 > by0 + 3u);
-                            const uint32_t dcx = (bx0 >> 3) - (x0 >> 3), dcy = (by0 >> 3) - (y0 >> 3);
-                            if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) hit = false;
-                            const float cxl = 4.0f * (float)i + 2.0f, cyl = 4.0f * (float)j + 2.0f;
-                            const float uc = st.a.x + st.a.z * cxl + st.a.w * cyl;
-                            const float vc = st.a.y + st.b.x * cxl + st.b.y * cyl;
-                            const float tu = fmaxf(fabsf(uc) - eu, 0.0f), tv = fmaxf(fabsf(vc) - ev, 0.0f);
-                            const bool he = fmaxf(tu, tv) <= kBoxS * 1.001f && tu * tu + tv * tv <= kQMaxS * 1.001f;
-                            bmr |= hit ? 1u << (4u * j + i) : 0u;
-                            bme |= (hit && he) ? 1u << (4u * j + i) : 0u;
-                        }
-                    cc_bmr[tid] = (uint16_t)bmr;
-                    cc_bme[tid] = (uint16_t)bme;
-                    // staged records, and those whose rect reaches the tile at all
-                    GS_CC(16, 1);
-                    if (qm) GS_CC(17, 1);
-                }
-#endif
             }
+            sqm[tid] = (uint8_t)qm;
         }
-        GS_CT(1);
         __syncthreads();
-        GS_CT(2);
         {
             const uint32_t j = b + 2u * kTileThreads + tid;
             id_cur = id_next;
@@ -515,6 +389,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
         // wave-level compaction of the splats reaching this quadrant (index order kept)
         uint32_t nl = 0;
         if (__ballot(!finished()) != 0) {
+            wend = b + cnt_b;
             for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
                 const uint32_t k = k0 + lane;
                 const bool hit = k < cnt_b && ((sqm[k] >> wave) & 1u);
@@ -524,7 +399,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
             }
         }
         wave_lds_sync();  // wlist[wave] is only touched by this wave
-        GS_CT(3);
         uint32_t i = 0;
         if constexpr (MODE == 2 || MODE == 3) {
             for (; i < nl; ++i) {
@@ -546,84 +420,50 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) void composite_kernel(Compo
                 const float2 c1 = make_float2(p1.c.x, p1.c.y);
                 const uint32_t i0 = kIds ? __float_as_uint(p0.c.z) : 0u, i1 = kIds ? __float_as_uint(p1.c.z) : 0u;
                 if (i + 3 < nl) w2 = wl2[(i >> 1) + 1];
-#ifdef GS_COMPOSITE_COUNTERS
-                cc_rec(wlist[wave][i]);
-#endif
                 body_v(a0, b0, c0, i0, (_Float16)0.0f);
-#ifdef GS_COMPOSITE_COUNTERS
-                cc_rec(wlist[wave][i + 1]);
-#endif
                 body_v(a1, b1, c1, i1, (_Float16)0.0f);
             }
-            if (i < nl && __ballot(!finished()) != 0) {
-#ifdef GS_COMPOSITE_COUNTERS
-                cc_rec(wlist[wave][i]);
-#endif
-                body(wlist[wave][i++]);
-            }
-        }
-        if (lane == 0) GS_CC(3, i);
-#ifdef GS_COMPOSITE_COUNTERS
-        cc_batch();
-#endif
-        GS_CT(4);
-    }
-    GS_CT_FLUSH();
-    GS_TR_FLUSH();
-#ifdef GS_COMPOSITE_COUNTERS
-    if constexpr (MODE == 0) {
-        uint32_t x4 = cc_n4, x2 = cc_n2, xl = cc_nl, sl = cc_nl;
-        for (int o = 32; o > 0; o >>= 1) {
-            x4 = max(x4, (uint32_t)__shfl_xor((int)x4, o, 64));
-            x2 = max(x2, (uint32_t)__shfl_xor((int)x2, o, 64));
-            xl = max(xl, (uint32_t)__shfl_xor((int)xl, o, 64));
-            sl += (uint32_t)__shfl_xor((int)sl, o, 64);
-        }
-        if (lane == 0) {
-            GS_CC(10, x4);
-            GS_CC(11, x2);
-            GS_CC(12, xl);
-            GS_CC(13, sl);
+            if (i < nl && __ballot(!finished()) != 0) body(wlist[wave][i++]);
         }
     }
-#endif
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
-#ifdef GS_COMPOSITE_COUNTERS
-    if (tid == 0 && MODE == 0 && tile_flag < (1u << 16)) g_tile_fetch[tile_flag] = fetched;
-#endif
-    bool keep_state = false;
+    // PASS 1, per quadrant (no workgroup barrier, no contended atomic): a
+    // pixel still open at the end of a list that was cut keeps its state for
+    // the fallback lists instead of its final value
+    bool open_w = false, keep = false;
     if constexpr (PASS == 1) {
-        // does any pixel of the tile remain open for the second slab?
-        const bool open_w = __ballot(!finished()) != 0;
-        if (lane == 0) sopen_end[wave] = open_w ? 1u : 0u;
-        __syncthreads();
-        const uint4 o = *reinterpret_cast<const uint4*>(sopen_end);
-        keep_state = (o.x | o.y | o.z | o.w) != 0u;
-        if (tid == 0) {
-            a.open4[tile_flag] = keep_state ? 1 : 0;
-            if (keep_state && a.open_tiles) (void)atomicAdd(a.open_tiles, 1ull);
+        open_w = __ballot(!finished()) != 0;
+        keep = open_w && trunc;
+    }
+    const bool write = inside && (PASS != 2 || resumed);  // (PASS 2: the rest was written by pass 1)
+    if (write) {
+        if (keep) {
+            a.state[pix] = make_float4(C0, C1, C2, T);  // (C, T)
+        } else if constexpr (SLAB == 1) {
+            a.t_out[pix] = T;
+        } else if constexpr (SLAB == 2) {
+            // contributions: colour and the alpha this slab adds (sum over slabs)
+            a.out[pix] = make_float4(C0, C1, C2, T0 - T);
+        } else if constexpr (MODE == 2) {
+            a.thr_out[pix] = thr;
+        } else {
+            const float4 o = MODE == 3 ? kb.resolve() : make_float4(C0, C1, C2, 1.0f - T);
+            if (a.out_bgra8)
+                a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
+            else
+                a.out[(size_t)orow * width + px] = o;
         }
     }
-    if (!inside) return;
+    // the quadrant's record words, after its pixels (a store queued before
+    // them would hold the pixel stores' wait, vmcnt counting stores too): its
+    // cut position (the end of the last batch it walked with an open pixel,
+    // ~0 while one stays open) and its open flag
     if constexpr (PASS == 1) {
-        if (keep_state) {  // (C, T) for the second slab; final pixels otherwise
-            a.out[(size_t)orow * width + px] = make_float4(C0, C1, C2, T);
-            return;
+        if (lane == 0) {
+            qr[tq + wave] = open_w ? 0xFFFFFFFFu : wend;
+            qr[16u + tq + wave] = keep ? 1u : 0u;
+            if (keep) (void)atomicAdd(a.open_q_count, 1ull);
         }
-    }
-    if constexpr (SLAB == 1) {
-        a.t_out[(size_t)py * width + px] = T;
-    } else if constexpr (SLAB == 2) {
-        // contributions: colour and the alpha this slab adds (sum over slabs)
-        a.out[(size_t)py * width + px] = make_float4(C0, C1, C2, T0 - T);
-    } else if constexpr (MODE == 2) {
-        a.thr_out[(size_t)py * width + px] = thr;
-    } else {
-        const float4 o = MODE == 3 ? kb.resolve() : make_float4(C0, C1, C2, 1.0f - T);
-        if (a.out_bgra8)
-            a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
-        else
-            a.out[(size_t)orow * width + px] = o;
     }
 }
 
@@ -646,8 +486,9 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
-    if (a.pass) {  // two-slab frames: tile / live50 rules, fp32 output, no cap, no depth slabs
-        if (cap || a.slab || a.out_bgra8 || !a.out || !a.open4 || (mode != 0 && mode != 1) || a.pass > 2)
+    if (a.pass) {  // depth-cut frames: tile / live50 rules, no cap, no depth slabs, whole frame
+        if (cap || a.slab || a.rows || a.compact || (!a.out && !a.out_bgra8) || !a.qrec || !a.state ||
+            (mode != 0 && mode != 1) || a.pass > 2 || (a.pass == 1 && !a.open_q_count))
             return hipErrorInvalidValue;
         if (a.pass == 1)
             return mode == 0 ? launch_mode<0, false, 0, 1>(a, st, t0, t1) : launch_mode<1, false, 0, 1>(a, st, t0, t1);
@@ -665,34 +506,35 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
     return cap ? launch_mode<1, true>(a, st, t0, t1) : launch_mode<1, false>(a, st, t0, t1);
 }
 
+__global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __restrict__ qrec,
+                                                           const uint32_t* __restrict__ vals,
+                                                           const uint32_t* __restrict__ dkey, uint32_t* __restrict__ cut,
+                                                           uint32_t nbins, uint32_t margin) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b >= nbins) return;
+    uint32_t c = 0u;
+    const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);  // (the bin's 16 positions)
+    uint32_t p = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = q[i];
+        p = max(p, max(max(v.x, v.y), max(v.z, v.w)));
+    }
+    if (p == 0xFFFFFFFFu) c = 0xFFFFu;
+    else if (p > 0u) c = min(dkey[vals[p - 1u]] + margin, 0xFFFFu);
+    cut[b] = c;
+}
+
+hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
+                               uint32_t nbins, uint32_t margin, hipStream_t st) {
+    if (nbins == 0) return hipSuccess;
+    cut_finalize_kernel<<<(nbins + 255) / 256, 256, 0, st>>>(qrec, vals, dkey, cut_out, nbins, margin);
+    return hipGetLastError();
+}
+
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {
     if (a.cap <= 0 || !a.thr_out) return hipErrorInvalidValue;
     return launch_mode<2, false>(a, st);
 }
 
 }  // namespace gs
-
-#ifdef GS_COMPOSITE_TIMERS
-extern "C" int gs_debug_composite_timers(unsigned long long* out) {
-    unsigned long long zero[8] = {};
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_ct), sizeof zero) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_ct), zero, sizeof zero) != hipSuccess;
-}
-#endif
-#ifdef GS_COMPOSITE_TRACE
-extern "C" int gs_debug_composite_trace(void* out, unsigned n) {  // n uint4 entries
-    if (n > gs::kTraceMax) n = gs::kTraceMax;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_trace), (size_t)n * 16) != hipSuccess;
-}
-#endif
-#ifdef GS_COMPOSITE_COUNTERS
-extern "C" int gs_debug_composite_tile_fetch(uint32_t* out, unsigned n) {
-    if (n > (1u << 16)) n = 1u << 16;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_tile_fetch), (size_t)n * 4) != hipSuccess;
-}
-extern "C" int gs_debug_composite_counters(unsigned long long* out) {
-    unsigned long long zero[20] = {};
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cc), sizeof zero) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_cc), zero, sizeof zero) != hipSuccess;
-}
-#endif

@@ -21,6 +21,7 @@ constexpr int kBinShift = 5;
 constexpr int kBinThreads = 1024;
 constexpr int kDepthBits = 15;            // positive half bit patterns are < 0x7C01
 constexpr uint32_t kDepthInf = 0x7C00u;
+
 constexpr float kQMax = 9.21034037197618f;  // 2 ln 100: exp(-q/2) >= 0.01 (tile.metal:193)
 constexpr float kTMin = 0.01f;            // 50layer.metal:219
 // Composite contract.  The conic is scaled by
@@ -195,23 +196,66 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, co
     return n;
 }
 
-// Two-slab frames: the second slab's pairs go only to bins
-// the first slab's composite left open, open[bin] != 0 (a bin's four tile
-// flags as one word).  (splat, bin) pairs of the rect in such bins.
+// Per-bin depth cuts (gs_options.depth_split).  A depth-cut
+// frame's bin lists (the front lists) hold the pairs whose depth key lies at
+// or ahead of their bin's cut in S1 order, dkey <= cut[bin]: every pair is
+// emitted, and the bin sort's first pass drops the others (SortFilter).  The
+// fallback for the tiles those lists leave open emits the other pairs of the
+// bins with an open tile: CutSel mode 2, dkey > cut[bin] and open[bin] != 0
+// (the 16 quadrant flags of the bin's four tiles); every fallback kernel
+// returns at once when *guard (the frame's open quadrant count) is 0.  S1
+// composites ascending dkey, so each bin's front list precedes all its other
+// pairs.  mode 0: every pair.
+constexpr uint32_t kQrecWords = 32;  // per bin: 16 quadrant cut positions, 16 open flags (CompositeArgs)
+struct CutSel {
+    int mode = 0;
+    const uint32_t* dkey = nullptr;  // per item (index order)
+    const uint32_t* cut = nullptr;   // per bin
+    const uint32_t* qrec = nullptr;  // per bin kQrecWords: open flags in words [16, 32)
+    const unsigned long long* guard = nullptr;
+};
+__device__ __forceinline__ bool cut_keep(const CutSel& s, uint32_t dk, uint32_t bin) {
+    if (dk <= s.cut[bin]) return false;
+    const uint4* f = reinterpret_cast<const uint4*>(s.qrec + (size_t)bin * kQrecWords + 16u);
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 o = f[i];
+        any |= o.x | o.y | o.z | o.w;
+    }
+    return any != 0u;
+}
+
+// (splat, bin) pairs of the rect in owned bin rows, minus the excluded bins,
+// for which keep(bin) holds.
+template <typename Keep>
+__device__ __forceinline__ uint32_t rect_count_if(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
+                                                  Keep&& keep) {
+    if (r.empty) return 0u;
+    uint32_t n = 0;
+    for (uint32_t by = r.by0; by <= r.by1; ++by) {
+        if (!owns_bin_row(by, own)) continue;
+        for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx)
+            if (!bin_excluded(r, by, bx) && keep(by * tiles_x + bx)) ++n;
+    }
+    return n;
+}
+
 // The (bin, splat) pairs of one splat, from pair offset `off` on: one per bin
 // of its rect in an owned bin row, minus the bins its ellipse provably misses
-// (row-major bin order).  key = key_hi | bin id.
+// (row-major bin order), for which keep(bin) holds.  key = key_hi | bin id.
 // on_pair(offset, bin) is called for every pair written.
-template <typename F>
-__device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
-                                               uint32_t key_hi, uint32_t val, uint32_t off,
-                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                               F&& on_pair) {
+template <typename Keep, typename F>
+__device__ __forceinline__ void emit_bin_pairs_if(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
+                                                  uint32_t key_hi, uint32_t val, uint32_t off,
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, Keep&& keep,
+                                                  F&& on_pair) {
     for (uint32_t by = r.by0; by <= r.by1; ++by) {
         if (!owns_bin_row(by, own)) continue;
         for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx) {
             if (bin_excluded(r, by, bx)) continue;  // the ellipse misses this bin
             const uint32_t bin = by * tiles_x + bx;
+            if (!keep(bin)) continue;
             keys[off] = key_hi | bin;
             vals[off] = val;
             on_pair(off, bin);
@@ -222,7 +266,8 @@ __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_
 __device__ __forceinline__ void emit_bin_pairs(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
                                                uint32_t key_hi, uint32_t val, uint32_t off,
                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-    emit_bin_pairs(r, tiles_x, own, key_hi, val, off, keys, vals, [](uint32_t, uint32_t) {});
+    emit_bin_pairs_if(r, tiles_x, own, key_hi, val, off, keys, vals, [](uint32_t) { return true; },
+                      [](uint32_t, uint32_t) {});
 }
 
 // fp32 RGBA -> BGRA8Unorm texel: clamp to [0, 1], scale by 255, round to

@@ -14,15 +14,9 @@ namespace gs {
 // pixel rect (empty rect for culled splats).
 // t0/t1: optional events recorded by the kernel's own dispatch (timing
 // without extra packets).
-// zero8 (optional): a 64-bit word the kernel clears (the frame's composite
-// fetch counter, CompositeArgs::fetched), so no memset dispatch is needed.
-// hist (optional): += the depth histogram of the two-slab cut (SlabSel),
-// kCutCopies x kCutBuckets words, bucket dkey >> kCutShift weighted by the
-// bins of the splat's rect, one copy per XCD (workgroup & 7); zeroed by
-// launch_tile_count_totals once the cut is taken.
-constexpr int kCutShift = 7;
-constexpr int kCutBuckets = (1 << kDepthBits) >> kCutShift;  // 256
-constexpr int kCutCopies = 8;
+// zero8 (optional): two 64-bit words the kernel clears (the frame's
+// composite fetch counter and open tile count, CompositeArgs::fetched /
+// open_tiles), so no memset dispatch is needed.
 // Bin-first single-GPU frames: the preprocess also does the
 // reduce half of the scan.  Every workgroup adds its splats' pair counts and
 // visible count into part[b] / part[nb + b] of its scan block b (kScanItems
@@ -41,8 +35,7 @@ struct PreFuse {
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
                              hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr,
-                             unsigned long long* zero8 = nullptr, uint32_t* hist = nullptr,
-                             const PreFuse& fuse = PreFuse{});
+                             unsigned long long* zero8 = nullptr, const PreFuse& fuse = PreFuse{});
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block
@@ -58,35 +51,19 @@ constexpr int kScanItems = 4096;  // per block
 // host re-queues them with larger buffers).  Then launch_scan_duplicate.
 // zero[0..nzero) is cleared on the way (the first sort pass's digit counts,
 // PassCounts).
-// Two-slab frames: the frame's pairs in two passes split at a
-// depth-key cut K (S1 order composites ascending dkey, so every pair of the
-// first slab precedes every pair of the second in every bin list).
-//   mode 1: the reduce takes K from the preprocess histogram (the bucket
-//           boundary where the pair share first reaches `frac`), stores it in
-//           *kcut and counts the first slab (dkey < K) per block, plus the
-//           pairs of both slabs (partials: 3 * nblocks words); the scan gives
-//           the second slab's pairs offsets after all of the first's (total[4]
-//           = both slabs' pairs) and the duplicate writes both: the first
-//           slab's lists are sorted and composited, then the second slab's
-//           pairs of the bins left open (launch_radix_sort's `open` filter)
-struct SlabSel {
-    int mode = 0;
-    const uint32_t* dkey = nullptr;  // per item (index order)
-    uint32_t* kcut = nullptr;
-    uint32_t* hist = nullptr;
-    float frac = 0.3f;
-    unsigned long long* zero64 = nullptr;  // mode 1 (optional): cleared once the cut is taken (open-tile counter)
-};
+// sel (mode 0 or 2): which pairs are counted (CutSel); mode 2
+// also makes both kernels return at once while *sel.guard == 0 (then P = 0).
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
                                     uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr,
-                                    const SlabSel& sel = SlabSel{});
+                                    const CutSel& sel = CutSel{}, uint32_t tiles_x = 0);
 // (done: recorded by the totals kernel's own dispatch packet, not a separate
 // marker packet, which would leave a ~6 us bubble in the stream.)
 // The scan half alone, after a preprocess with PreFuse: the block sums in
-// part (2 nb words) are scanned into partials (as launch_tile_count_totals
-// leaves them) and part is cleared for the next frame.
+// part (2 x nb words: pairs, visible splats) are scanned into partials (as
+// launch_tile_count_totals leaves them) and part is cleared for the next
+// frame.
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
                                       hipEvent_t done = nullptr);
@@ -107,13 +84,14 @@ constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts i
 // Index order runs one fused kernel; depth order (order set) a down-sweep
 // into offsets (n words of scratch) and a one-splat-per-lane duplicate.
 // Nothing is written when *npairs == 0 (see launch_tile_count_totals).
-// sel (index order only): the two-slab filter (mode 1 / 2, as the reduce).
+// sel (index order only): which pairs are emitted (CutSel mode 0 or 2; the
+// counts must be the ones the scan was given).
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
                                  uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
-                                 const SlabSel& sel = SlabSel{});
+                                 const CutSel& sel = CutSel{});
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -133,9 +111,11 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
 #endif
 constexpr uint32_t kSegLdsMax = GS_SEG_NT * GS_SEG_IPT;  // lists sorted inside one workgroup (bin_depth_sort.hip)
 constexpr uint32_t kSegSampleValid = 0x80000000u;
+// guard (optional): nothing is done while *guard == 0 (the fallback lists).
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
-                                 hipStream_t st, hipEvent_t done = nullptr);
+                                 hipStream_t st, hipEvent_t done = nullptr,
+                                 const unsigned long long* guard = nullptr);
 
 // ---- radix_sort.hip --------------------------------------------------------
 constexpr int kSortBins = 256;   // 8-bit digits
@@ -162,14 +142,17 @@ uint32_t radix_sort_tile_items();
 // n_dev (optional): the item count is read on the device from *n_dev (<= n;
 // n sizes the grids and the scratch), so the sort can be queued before the
 // host knows it.
-// Filter (a two-slab frame's second slab, SlabSel): only items whose bin
-// (key & bmask) has open[bin] != 0 are counted and sorted, the others are
-// dropped in the first pass, which stores the number kept in *kept (the
-// later passes read it, as n_dev); the result holds the kept items.
+// Filter (the bin sort of a depth-cut frame): only items whose
+// depth key (key >> dshift) lies at or ahead of their bin's cut (<=
+// cut[key & bmask]) are counted and sorted; the first pass drops the others
+// and stores the number kept in *kept (the later passes read it, as n_dev);
+// the result holds the kept items.
 struct SortFilter {
-    const uint32_t* open = nullptr;  // null: every item
+    const uint32_t* cut = nullptr;  // null: every item
     uint32_t bmask = 0;
+    int dshift = 0;
     uint32_t* kept = nullptr;
+    __device__ __forceinline__ bool keep(uint32_t key) const { return (key >> dshift) <= cut[key & bmask]; }
 };
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
@@ -213,14 +196,23 @@ struct CompositeArgs {
     // prefetched one; each of a bin's four tiles fetches its list itself),
     // the early-out-aware basis of the composite's algorithmic bytes
     unsigned long long* fetched;
-    // Two-slab frames (modes 0/1, no cap, fp32 output).  pass 1: the first
-    // slab's lists; a tile whose pixels all finished writes its final pixels,
-    // any other tile writes its state (C, T) and open4[bin * 4 + tile] = 1
-    // (else 0); open_tiles += open tiles.  pass 2: only open tiles, resuming
-    // from the state with the second slab's lists.
+    // Depth-cut frames (gs_options.depth_split; modes 0/1, no cap, DESIGN.md
+    // §4), per 8x8 quadrant (wave), with plain stores to its own words of its
+    // bin's 128-B record qrec[bin * kQrecWords ...] (no workgroup barrier, no
+    // contended atomic, and a cache line written only by the bin's four tiles,
+    // which run on one XCD).  pass 1, the front lists: every quadrant q (tile
+    // of the bin * 4 + wave) writes its cut position to word q (the end of the
+    // last batch it walked with an open pixel, ~0 while one stays open;
+    // launch_cut_finalize turns them into the next cuts) and its open flag to
+    // word 16 + q: 1 if a pixel stays open at the end of a list that was cut
+    // (cut_in[bin] < kDepthInf); an open quadrant writes its pixels' state
+    // (C, T) into `state` and adds one to open_q_count.  pass 2: the open
+    // quadrants only, resumed from their state with the fallback lists.
     int pass;
-    uint8_t* open4;
-    unsigned long long* open_tiles;
+    uint32_t* qrec;
+    unsigned long long* open_q_count;
+    float4* state;
+    const uint32_t* cut_in;   // may be null: no list was cut
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals
@@ -228,6 +220,12 @@ struct CompositeArgs {
 // id <= thr[pixel] are composited.
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0 = nullptr,
                             hipEvent_t t1 = nullptr);
+// Depth cuts: the next cut of every bin from the largest of its 16 quadrants'
+// cut positions (CompositeArgs::qrec): ~0 -> 0xFFFF (every pair), 0 -> 0,
+// else the depth key of the list record before it plus `margin`, at most
+// 0xFFFF.  vals and dkey: the composited lists and depth keys.
+hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
+                               uint32_t nbins, uint32_t margin, hipStream_t st);
 // Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).

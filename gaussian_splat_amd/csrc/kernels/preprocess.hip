@@ -180,18 +180,18 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, floa
 #endif
 
 // EPI: what follows the per-splat work.  0: nothing (each lane returns on its
-// own); 1: the scan's reduce half and fills (PreFuse); 2: the two-slab depth
-// histogram.  Each epilogue is compiled only into its own instance, so the
-// plain kernel keeps its registers (63 VGPRs, no scratch).
+// own); 1: the scan's reduce half and fills (PreFuse).  The epilogue is
+// compiled only into its own instance, so the plain kernel keeps its
+// registers (63 VGPRs, no scratch).
 template <int DEG, int EPI>
 __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
                                                          uint32_t* __restrict__ rect_hi,
                                                          unsigned long long* __restrict__ zero8,
-                                                         uint32_t* __restrict__ hist, const PreFuse fuse) {
+                                                         const PreFuse fuse) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i == 0 && zero8) *zero8 = 0ull;
+    if (i < 2 && zero8) zero8[i] = 0ull;
     if constexpr (EPI == 0)
         if (i >= s.n) return;
     uint32_t rlo = kEmptyRectLo, rhi = 0u;
@@ -368,22 +368,6 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
     rect_lo[i] = rlo;
     rect_hi[i] = rhi;
     }
-    if constexpr (EPI == 2) {
-        // two-slab cut (SlabSel): the workgroup's depth histogram, weighted by
-        // the bins of each rect, added into this XCD's copy (after every load
-        // and store of the kernel, so the barriers cost it nothing)
-        __shared__ uint32_t wh[kCutBuckets];
-        static_assert(kCutBuckets == 256, "one bucket per lane");
-        wh[threadIdx.x] = 0u;
-        __syncthreads();
-        if (rlo != kEmptyRectLo) {
-            const BinRect r = bin_rect(rlo, rhi, U.cell_mask != 0);
-            atomicAdd(&wh[key >> kCutShift], (r.bx1 - r.bx0 + 1u) * (r.by1 - r.by0 + 1u));
-        }
-        __syncthreads();
-        const uint32_t v = wh[threadIdx.x];
-        if (v) atomicAdd(&hist[(blockIdx.x & (kCutCopies - 1u)) * kCutBuckets + threadIdx.x], v);
-    }
     if constexpr (EPI == 1) {
         // the scan's reduce half: this workgroup's pairs and visible splats
         // into its scan block's sums (the counts scan_duplicate recomputes)
@@ -409,9 +393,8 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
-                             hipEvent_t t1, unsigned long long* zero8, uint32_t* hist, const PreFuse& fuse) {
-    if (fuse.part && (hist || fuse.nb != (s.n + kScanItems - 1) / kScanItems))
-        return hipErrorInvalidValue;  // (a two-slab histogram frame keeps scan_reduce)
+                             hipEvent_t t1, unsigned long long* zero8, const PreFuse& fuse) {
+    if (fuse.part && fuse.nb != (s.n + kScanItems - 1) / kScanItems) return hipErrorInvalidValue;
     if (s.n == 0 && fuse.part) {  // no grid: the fills as copies
         if (fuse.nfill && hipMemsetAsync(fuse.fill, 0xFF, (size_t)fuse.nfill * sizeof(uint2), st) != hipSuccess)
             return hipGetLastError();
@@ -420,7 +403,7 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     }
     if (s.n == 0) {
         // no dispatch: the timing events still mark the (empty) stage
-        if (zero8 && hipMemsetAsync(zero8, 0, 8, st) != hipSuccess) return hipGetLastError();
+        if (zero8 && hipMemsetAsync(zero8, 0, 16, st) != hipSuccess) return hipGetLastError();
         if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
         if (t1 && hipEventRecord(t1, st) != hipSuccess) return hipGetLastError();
         return hipSuccess;
@@ -428,17 +411,17 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     dim3 grid((s.n + 255) / 256), block(256);
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
-    const int epi = fuse.part ? 1 : hist ? 2 : 0;
-    switch (sh_degree * 3 + epi) {
+    const int epi = fuse.part ? 1 : 0;
+    switch (sh_degree * 2 + epi) {
 #define GS_PRE_CASE(D, E)                                                                                          \
-    case D * 3 + E:                                                                                                \
+    case D * 2 + E:                                                                                                \
         hipExtLaunchKernelGGL((preprocess_kernel<D, E>), grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, \
-                              rect_hi, zero8, hist, fuse);                                                         \
+                              rect_hi, zero8, fuse);                                                               \
         break;
-        GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1) GS_PRE_CASE(0, 2)
-        GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1) GS_PRE_CASE(1, 2)
-        GS_PRE_CASE(2, 0) GS_PRE_CASE(2, 1) GS_PRE_CASE(2, 2)
-        GS_PRE_CASE(3, 0) GS_PRE_CASE(3, 1) GS_PRE_CASE(3, 2)
+        GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1)
+        GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1)
+        GS_PRE_CASE(2, 0) GS_PRE_CASE(2, 1)
+        GS_PRE_CASE(3, 0) GS_PRE_CASE(3, 1)
 #undef GS_PRE_CASE
     default: return hipErrorInvalidValue;
     }

@@ -79,15 +79,16 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
-// FILT: the open-bin filter (two-slab frames' second slab) is compiled in
-// only where it is used; without it the kernels keep round 2's registers
-// (the pass at 80 VGPRs, 6 waves per SIMD, instead of 98 and 4).
+// FILT (the first pass of a depth-cut frame's bin sort, SortFilter): only
+// the items at or ahead of their bin's cut are counted and sorted.  Compiled
+// in only where it is used, so the other kernels keep their registers.
 template <int NV, bool FILT>
 __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                         uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles,
                                                         const uint32_t* __restrict__ n_dev, const SortFilter flt) {
     constexpr uint32_t TILE = tile_items(NV);
     if (n_dev) n = *n_dev;  // tiles past it count zeros
+    if (n == 0u) return;    // (nothing to sort: the scan and the pass return at once)
     __shared__ uint32_t h[kRsWaves][kSortBins];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
@@ -100,9 +101,12 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
         uint32_t kk[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) kk[k] = keys[min(t0 + k * kRsThreads + tid, n - 1u)];
+        bool keep[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) keep[k] = !FILT || flt.keep(kk[k]);
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (t0 + k * kRsThreads + tid < n && (!FILT || flt.open[kk[k] & flt.bmask]))
+            if (t0 + k * kRsThreads + tid < n && keep[k])
                 atomicAdd(&h[wave][(kk[k] >> shift) & mask], 1u);
     }
     __syncthreads();
@@ -121,8 +125,13 @@ constexpr int kRsScanThreads = 1024;
 constexpr int kRsScanIpt = 4;
 
 __global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __restrict__ C, uint32_t ntiles,
-                                                                  uint32_t* __restrict__ totals) {
+                                                                  uint32_t* __restrict__ totals,
+                                                                  const uint32_t* __restrict__ n_dev) {
     constexpr int W = kRsScanThreads / 64;
+    if (n_dev && *n_dev == 0u) {  // nothing to sort (the passes return at once too)
+        if (threadIdx.x == 0) totals[blockIdx.x] = 0u;
+        return;
+    }
     constexpr uint32_t CH = kRsScanThreads * kRsScanIpt;
     __shared__ uint32_t tmp[W];
     uint32_t* row = C + (size_t)blockIdx.x * ntiles;
@@ -262,10 +271,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     if constexpr (FILT) {
         if (tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
 #pragma unroll
-        for (int k = 0; k < IPT; ++k) {
-            const uint32_t idx = base + k * 64 + lane;
-            keep |= (idx < n && flt.open[key[k] & flt.bmask]) ? 1u << k : 0u;
-        }
+        for (int k = 0; k < IPT; ++k) keep |= (base + k * 64 + lane < n && flt.keep(key[k])) ? 1u << k : 0u;
     }
     // slot k of this lane holds an item to sort
     auto kept = [&](int k) -> bool {
@@ -413,7 +419,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
                                   const uint32_t* n_dev, bool first_counted, const SortFilter& flt = SortFilter{}) {
-    if (flt.open && (NV != 1 || first_counted || !flt.kept)) return hipErrorInvalidValue;
+    if (flt.cut && (NV != 1 || first_counted || !flt.kept)) return hipErrorInvalidValue;
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -434,32 +440,30 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     for (int p = 0; p < plan.passes; ++p) {
         io.kout = to_final ? keys : tmp_keys;
         for (int a = 0; a < NV; ++a) io.vout[a] = to_final ? vals[a] : tmp_vals[a];
-        // (the filter drops items in pass 0; later passes sort what it kept)
-        const SortFilter f = p == 0 ? flt : SortFilter{};
-        const bool filt = f.open != nullptr;  // (one value array only: the two-slab bin sort)
         uint2* const rg = p + 1 == plan.passes ? ranges : nullptr;
         const uint32_t rmask = bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+        // (the filter drops items in pass 0; the later passes sort what it kept)
+        const bool filt = p == 0 && flt.cut != nullptr;
         hipError_t e = hipSuccess;
         if constexpr (NV == 1) {
             if (filt) {
-                if (p > 0 || !first_counted)
-                    rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p],
-                                                                            C, tiles, n_dev, f);
-                rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
+                rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                        tiles, n_dev, flt);
+                rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
                 e = launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
-                                          tiles, rg, rmask, n_dev, f);
+                                          tiles, rg, rmask, n_dev, flt);
             }
         }
         if (!filt) {
             if (p > 0 || !first_counted)  // (pass 0's counts may come from the producer)
                 rts_count_kernel<NV, false><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
-                                                                         tiles, n_dev, f);
-            rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals);
-            e = launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals, tiles,
-                                       rg, rmask, n_dev, f);
+                                                                         tiles, n_dev, SortFilter{});
+            rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
+            e = launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+                                       tiles, rg, rmask, n_dev, SortFilter{});
         }
         if (e != hipSuccess) return e;
-        if (p == 0 && flt.open) n_dev = flt.kept;
+        if (filt) n_dev = flt.kept;
         io.kin = io.kout;
         for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
         to_final = !to_final;
@@ -482,7 +486,7 @@ hipError_t launch_radix_sort3(const uint32_t* keys_in, const uint32_t* const* va
                               uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                               int bits, uint32_t* scratch, bool* result_in_tmp, hipStream_t st) {
     return radix_sort_impl<3>(keys_in, vals_in, keys, vals, tmp_keys, tmp_vals, n, bits, scratch, result_in_tmp,
-                              nullptr, st, nullptr, false, SortFilter{});
+                              nullptr, st, nullptr, false);
 }
 
 }  // namespace gs

@@ -25,41 +25,39 @@ struct CountSrc {
     const uint32_t* lo;
     const uint32_t* hi;
     RowOwnership own;
-    bool masked;  // rect words carry the bin-exclusion mask
-    SlabSel sel;  // two-slab filter (mode 0: every item)
+    bool masked;       // rect words carry the bin-exclusion mask
+    CutSel sel;        // which pairs (depth cuts, gs_device.h; mode 0: every pair)
+    uint32_t tiles_x;  // (bin ids of the CutSel tables)
 };
 
-// Two-slab cut from the preprocess histogram (one 256-lane workgroup; every
-// workgroup computes the same K): the first bucket boundary at which the
-// share of pairs reaches sel.frac; 0x8000 (every key) for an empty frame.
-__device__ __forceinline__ uint32_t slab_cut(const SlabSel& sel, uint32_t* tmp4, uint32_t* kres) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int c = 0; c < kCutCopies; ++c) v += sel.hist[c * kCutBuckets + threadIdx.x];
-    uint32_t tot;
-    const uint32_t ex = block256_exclusive_scan<uint32_t>(v, tmp4, &tot);
-    const uint32_t thr = (uint32_t)((float)tot * sel.frac) + 1u;  // (ties and empty frames: see below)
-    if (threadIdx.x == 0) *kres = 0x8000u;
-    __syncthreads();
-    if (tot > 0u && ex < thr && ex + v >= thr) *kres = (threadIdx.x + 1u) << kCutShift;
-    __syncthreads();
-    return *kres;
+// Pairs of an item's rect under the selection (dk: its depth key).
+template <int MODE>
+__device__ __forceinline__ uint32_t item_pairs(const CountSrc& src, uint32_t lo, uint32_t hi, uint32_t dk) {
+    if constexpr (MODE == 0) {
+        return rect_tile_count(lo, hi, src.own, src.masked);
+    } else {
+        const CutSel& sel = src.sel;
+        return rect_count_if(bin_rect(lo, hi, src.masked), src.tiles_x, src.own,
+                             [&](uint32_t bin) { return cut_keep(sel, dk, bin); });
+    }
 }
 
-// Per block: pair count -> partials[b], contributing splats -> partials[nb + b];
-// two-slab mode 1 also the pairs of both slabs -> partials[2 nb + b].
+// Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
+// MODE 2 (the depth-cut fallback): nothing while *guard == 0.
+template <int MODE>
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials,
                                                           uint2* __restrict__ fill, uint32_t nfill,
                                                           uint32_t* __restrict__ zero, uint32_t nzero) {
+    if constexpr (MODE == 2)
+        if (*src.sel.guard == 0ull) return;
     __shared__ uint2 tmp[4];
-    __shared__ uint32_t ctmp[4], kres;
     const uint32_t base = blockIdx.x * kScanItems;
     // every rect loaded before the first use (clamped, branch-free): one
     // memory round trip instead of one per item (a conditional load is waited
     // for inside its branch)
     uint32_t lo[kScanIpt], hi[kScanIpt], dk[kScanIpt];
-    const uint32_t* dsrc = src.sel.mode ? src.sel.dkey : src.lo;
+    const uint32_t* dsrc = MODE ? src.sel.dkey : src.lo;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const uint32_t i = min(base + k * 256 + threadIdx.x, n - 1u);
@@ -67,23 +65,14 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
         hi[k] = src.hi[i];
         dk[k] = dsrc[i];
     }
-    uint32_t K = 0;
-    if (src.sel.mode == 1) {
-        K = slab_cut(src.sel, ctmp, &kres);
-        if (blockIdx.x == 0 && threadIdx.x == 0) *src.sel.kcut = K;
-    }
     // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
-    uint32_t s = 0, vis = 0, all = 0;
+    uint32_t s = 0, vis = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const bool in = base + k * 256 + threadIdx.x < n;
-        // (two-slab mode 1: the first slab's pairs, and the pairs and visible
-        // splats of both slabs)
-        const uint32_t ca = in ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
-        const uint32_t c = src.sel.mode == 1 && dk[k] >= K ? 0u : ca;
+        const uint32_t c = in ? item_pairs<MODE>(src, lo[k], hi[k], dk[k]) : 0u;
         s += c;
-        vis += ca > 0;
-        all += ca;
+        vis += c > 0;
     }
     // the frame's bin ranges start empty and the first sort pass's digit
     // counts at zero (saves two fill dispatches; stored after the loads, which
@@ -96,16 +85,10 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
     vis = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(vis), 63);
     const uint32_t wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 0) tmp[wave] = make_uint2(s, vis);
-    if (src.sel.mode == 1) {
-        all = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(all), 63);
-        if ((threadIdx.x & 63u) == 0) ctmp[wave] = all;
-    }
     __syncthreads();
     if (threadIdx.x == 0) {
         partials[blockIdx.x] = (uint64_t)tmp[0].x + tmp[1].x + tmp[2].x + tmp[3].x;
         partials[gridDim.x + blockIdx.x] = (uint64_t)tmp[0].y + tmp[1].y + tmp[2].y + tmp[3].y;
-        if (src.sel.mode == 1)
-            partials[2 * gridDim.x + blockIdx.x] = (uint64_t)ctmp[0] + ctmp[1] + ctmp[2] + ctmp[3];
     }
 }
 
@@ -139,25 +122,27 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 }
 
 // src (may be null): the block sums come from there instead (the fused
-// preprocess's, PreFuse) and are cleared after reading.
+// preprocess's, PreFuse: 2 x nb words) and are cleared after reading.
+// guard (may be null): while *guard == 0 the scan only reports P = 0.
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
                                                                      uint32_t* __restrict__ npairs, uint64_t cap,
-                                                                     uint32_t* __restrict__ hist,
-                                                                     unsigned long long* __restrict__ zero64,
-                                                                     unsigned long long* __restrict__ src) {
-    if (zero64 && threadIdx.x == 0) *zero64 = 0ull;
+                                                                     unsigned long long* __restrict__ src,
+                                                                     const unsigned long long* __restrict__ guard) {
+    if (guard && *guard == 0ull) {
+        if (threadIdx.x == 0) {
+            total[0] = total[1] = 0u;
+            *npairs = 0u;
+        }
+        return;
+    }
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
         seg_sample[0] = 0u;
         seg_sample[1] = 0u;
     }
-    // two-slab mode 1: every reduce block has taken the cut, so the histogram
-    // is cleared here for the next frame's preprocess
-    if (hist)
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(kCutCopies * kCutBuckets); i += kPartThreads) hist[i] = 0u;
     __shared__ uint64_t tmp[kPartThreads / 64];
     constexpr uint32_t CH = kPartThreads * kPartIpt;
     uint64_t carry = 0, vis = 0;
@@ -185,44 +170,12 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         }
         carry += t;
     }
-    uint64_t vt, at = 0;
+    uint64_t vt;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
-    if (hist) {
-        // two-slab frames: the second slab's pairs (all - first) of every
-        // block get offsets after all of the first slab's, so one duplicate
-        // writes both slabs' pairs (partials[2 nb + b], in place)
-        uint64_t run_far = carry;
-        for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
-            const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
-            uint64_t f[kPartIpt], s = 0;
-#pragma unroll
-            for (int k = 0; k < kPartIpt; ++k) {
-                // (the first slab's counts are scanned already: its sums are
-                // the differences of consecutive offsets)
-                const uint64_t a = i0 + k < nb ? partials[2 * nb + i0 + k] : 0u;
-                const uint64_t nr = i0 + k < nb ? (i0 + k + 1 < nb ? partials[i0 + k + 1] : carry) - partials[i0 + k]
-                                                : 0u;
-                f[k] = a - nr;
-                s += f[k];
-            }
-            uint64_t t;
-            uint64_t run = run_far + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
-            __syncthreads();  // every lane has read the block sums it rewrites
-#pragma unroll
-            for (int k = 0; k < kPartIpt; ++k) {
-                if (i0 + k < nb) partials[2 * nb + i0 + k] = run;
-                run += f[k];
-            }
-            run_far += t;
-        }
-        at = run_far;
-    }
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
-        if (hist) total[4] = at;  // the pairs of both slabs
-        // 0: the pair buffers are too small (for both slabs' pairs when split)
-        if (npairs) *npairs = (hist ? at : carry) <= cap ? (uint32_t)carry : 0u;
+        if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
     }
 }
 
@@ -259,7 +212,9 @@ __device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_
     return base + inc - v;
 }
 
-template <bool SPLIT>
+// MODE (CutSel): 0 every pair; 2 the fallback lists of a depth-cut frame
+// (nothing while *npairs == 0, which its guarded scan leaves).
+template <int MODE>
 __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
                                                                      const uint64_t* __restrict__ partials,
                                                                      const uint32_t* __restrict__ order,
@@ -271,22 +226,14 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
-    __shared__ uint32_t stn[SPLIT ? kScanItems + kScanItems / 32 : 1];  // (two-slab frames: first-slab offsets)
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
-    // Two-slab frames (sel mode 1): every item emits, a first-slab item (depth
-    // key below the cut) at the first slab's offsets, the others after all of
-    // them at the second slab's (scan_partials_kernel); only the first slab's
-    // pairs are counted for its sort.
-    constexpr bool split = SPLIT;  // (src.sel.mode == 1)
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
     // issued between stores would wait for them
     // (absent arrays read a stand-in, so no load sits in a branch, where its
     // value would be waited for at once)
     const uint64_t part = partials[blockIdx.x];
-    const uint64_t fpart = split ? partials[2 * gridDim.x + blockIdx.x] : 0u;
-    const uint32_t K = src.sel.mode ? *src.sel.kcut : 0u;
     const uint32_t* dsrc = dkey ? dkey : src.lo;
     const uint32_t* osrc = order ? order : src.lo;
     uint32_t rlo[kDupIpt], rhi[kDupIpt], dk[kDupIpt], ord[kDupIpt];
@@ -300,6 +247,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     }
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
+    const CutSel& sel = src.sel;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid;
@@ -307,35 +255,19 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        const uint32_t c = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
-        st[pad32(i)] = c;
-        if (split) stn[pad32(i)] = dk[k] < K ? c : 0u;
+        st[pad32(i)] = item_pairs<MODE>(src, rlo[k], rhi[k], dk[k]);
     }
     block_lds_sync();
-    uint32_t v[kDupIpt], vn[kDupIpt];
-    uint32_t s = 0, sn = 0;
+    uint32_t v[kDupIpt];
+    uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         v[k] = st[pad32(tid * kDupIpt + k)];
         s += v[k];
-        vn[k] = split ? stn[pad32(tid * kDupIpt + k)] : 0u;
-        sn += vn[k];
     }
     uint32_t t;
     const uint32_t ex = block_dup_exclusive_scan(s, tmp, &t);  // (ends with a barrier)
-    if (split) {
-        // the block's first-slab offsets (from part) and second-slab offsets
-        // (from fpart: every pair of an item before it, minus its first-slab ones)
-        const uint32_t exn = block_dup_exclusive_scan(sn, tmp, &t);
-        uint32_t run = ex, runn = exn;
-#pragma unroll
-        for (int k = 0; k < kDupIpt; ++k) {
-            const bool first = vn[k] == v[k];  // (an item with no pairs takes either)
-            st[pad32(tid * kDupIpt + k)] = first ? (uint32_t)part + runn : (uint32_t)fpart + (run - runn);
-            run += v[k];
-            runn += vn[k];
-        }
-    } else {
+    {
         uint32_t run = (uint32_t)part + ex;
 #pragma unroll
         for (int k = 0; k < kDupIpt; ++k) {
@@ -356,21 +288,21 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         const uint32_t off = st[pad32(i)];
         const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t val = order ? ord[k] : j;
-        if (pc.C && (!split || dk[k] < K)) {  // (the first sort pass counts the first slab only)
+        const uint32_t d_k = dk[k];
+        auto keep = [&](uint32_t bin) { return MODE == 0 || cut_keep(sel, d_k, bin); };
+        if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
-            emit_bin_pairs(
-                r, tiles_x, src.own, key_hi, val, off, keys, vals,
-                [&](uint32_t g, uint32_t bin) {
-                    if (g == next) {
-                        ++t;
-                        next += pc.tile;
-                    }
-                    const uint32_t d = bin & pc.mask;
-                    if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
-                    else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
-                });
+            emit_bin_pairs_if(r, tiles_x, src.own, key_hi, val, off, keys, vals, keep, [&](uint32_t g, uint32_t bin) {
+                if (g == next) {
+                    ++t;
+                    next += pc.tile;
+                }
+                const uint32_t d = bin & pc.mask;
+                if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
+                else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
+            });
         } else {
-            emit_bin_pairs(r, tiles_x, src.own, key_hi, val, off, keys, vals);
+            emit_bin_pairs_if(r, tiles_x, src.own, key_hi, val, off, keys, vals, keep, [](uint32_t, uint32_t) {});
         }
     }
     if (pc.C) {
@@ -539,10 +471,10 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
                                     uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done,
-                                    const SlabSel& sel) {
-    if (sel.mode && (sel.mode != 1 || !sel.dkey || !sel.kcut || !sel.hist))
+                                    const CutSel& sel, uint32_t tiles_x) {
+    if (sel.mode != 0 && (sel.mode != 2 || !sel.dkey || !sel.cut || !tiles_x || !sel.qrec || !sel.guard))
         return hipErrorInvalidValue;
-    const CountSrc src{rect_lo, rect_hi, own, masked, sel};
+    const CountSrc src{rect_lo, rect_hi, own, masked, sel, tiles_x};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
         if (nranges) {
@@ -553,14 +485,13 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
             const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * 4, st);
             if (e != hipSuccess) return e;
         }
+    } else if (sel.mode == 2) {
+        scan_reduce_kernel<2><<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     } else {
-        scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
+        scan_reduce_kernel<0><<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
-    // (an empty mode-1 frame runs no reduce: the cut stays from the last one,
-    // and the duplicate emits nothing either way)
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, sel.mode == 1 ? sel.hist : nullptr,
-                          sel.mode == 1 ? sel.zero64 : nullptr, nullptr);
+                          total, seg_sample, npairs, cap, nullptr, sel.mode == 2 ? sel.guard : nullptr);
     return hipGetLastError();
 }
 
@@ -569,7 +500,7 @@ hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uin
                                       hipEvent_t done) {
     if (!part) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, nullptr, nullptr, part);
+                          total, seg_sample, npairs, cap, part, nullptr);
     return hipGetLastError();
 }
 
@@ -577,13 +508,13 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
-                                 const SlabSel& sel) {
+                                 const CutSel& sel) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
-    if (sel.mode && (sel.mode != 1 || order || !dkey || sel.dkey != dkey || !sel.kcut))
+    if (sel.mode && (sel.mode != 2 || order || !dkey || sel.dkey != dkey || !sel.cut || !sel.qrec))
         return hipErrorInvalidValue;
-    const CountSrc src{rect_lo, rect_hi, own, masked, sel};
+    const CountSrc src{rect_lo, rect_hi, own, masked, sel, tiles_x};
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
@@ -595,12 +526,15 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
             duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
         return hipGetLastError();
     }
-    if (sel.mode == 1)
-        scan_duplicate_kernel<true><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
-                                                                vals, npairs, pc);
-    else
-        scan_duplicate_kernel<false><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
-                                                                 keys, vals, npairs, pc);
+    switch (sel.mode) {
+    case 2:
+        scan_duplicate_kernel<2><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
+                                                             vals, npairs, pc);
+        break;
+    default:
+        scan_duplicate_kernel<0><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
+                                                             vals, npairs, pc);
+    }
     return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 8
+#define GSPLAT_ABI_VERSION 9
 
 typedef enum {
     GS_OK = 0,
@@ -77,12 +77,13 @@ typedef struct gs_options {
                               at a resolution goes depth-first), 1 = depth-first (global depth
                               sort of the splats, then binning), 2 = bin-first (bin lists in
                               arrival order, then a stable per-bin depth sort).  DESIGN.md §1 */
-    int32_t depth_split;   /* bin-first frames (modes tile/live50, no cap, fp32 output): 1 = the lists
-                              are built and composited in two depth slabs, the second slab's pairs
-                              sorted only for the bins the first left open (same image, bit for
-                              bit); 0 = one slab (default: measured faster at 6M
-                              @1080p, 0.79 vs 0.83 ms: two composite passes cost more than the
-                              sorting the second slab skips) */
+    int32_t depth_split;   /* per-bin depth cuts (single-GPU bin-first frames, modes
+                              tile/live50, no cap): 1 = a frame's bin lists hold only the pairs at
+                              or in front of their bin's cut, the depth at which the bin's tiles
+                              saturated in the previous frame on the same buffer set, plus a
+                              margin; a tile those lists leave open finishes from its saved state
+                              with the rest of its bin's pairs (fallback lists).  Same image, bit
+                              for bit, for any camera path; 0 = whole lists */
     int32_t reserved[3];
 } gs_options;
 
@@ -125,10 +126,11 @@ typedef struct gs_stats {
        last frame's composite to read it. */
     int64_t records_fetched;
     /* pairs the frame actually emitted and sorted (= pairs, except in
-       two-slab frames, gs_options.depth_split: the first slab's plus the
-       second slab's in the bins the first left open), the tiles the first
-       slab left open, and the depth key cut (first slab = keys below it).
-       Read with records_fetched. */
+       depth-cut frames, gs_options.depth_split: the front lists' pairs plus
+       the fallback lists'), the 8x8-pixel quadrants the front lists left
+       open (open_tiles), and
+       two_slab = 1 for a depth-cut frame.  Read with records_fetched.
+       depth_cut: unused (0). */
     int64_t pairs_sorted;
     int64_t open_tiles;
     int32_t two_slab;
@@ -198,14 +200,6 @@ gs_status gs_sorted_pairs_host(gs_handle *h, uint32_t *keys, uint32_t *vals, int
  * tmp_keys/tmp_vals: n elements each; result ends in keys/vals. */
 gs_status gs_radix_sort_pairs(uint32_t *keys, uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals,
                               int64_t n, int32_t bits, void *hip_stream);
-/* The same sort keeping only the pairs whose key bits [0, bits) index a
- * nonzero word of `open` (device, 2^bits words; bits 1..16): the two-slab
- * frames' second-slab sort.  Reads keys_in/vals_in (n, not
- * aliasing the other arrays), leaves the *kept pairs, stably sorted, in
- * keys/vals; tmp_*: n elements each.  Synchronous. */
-gs_status gs_radix_sort_pairs_filtered(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys,
-                                       uint32_t *vals, uint32_t *tmp_keys, uint32_t *tmp_vals, int64_t n,
-                                       int32_t bits, const uint32_t *open, int64_t *kept, void *hip_stream);
 
 /* ---- multi-GPU: bin-row ownership across ranks ----- */
 /* No reference counterpart (the reference is single-GPU Metal).

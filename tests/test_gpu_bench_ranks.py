@@ -19,7 +19,8 @@ ROOT = Path(__file__).resolve().parents[1]
 def test_bench_two_rank_rehearsal(built):
     env = dict(os.environ, GS_BENCH_BACKEND="gloo", GS_BENCH_SAME_DEVICE="1")
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--splats", "300000", "--cpu-baseline", "0", "--pmc", "0", "--settle", "2"]
+           "--splats", "300000", "--cpu-baseline", "0", "--pmc", "0", "--settle", "2",
+           "--settled-probe", "4"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -31,3 +32,5 @@ def test_bench_two_rank_rehearsal(built):
     assert d["config"]["parallelism"].startswith("rows:")
     assert d["value"] > 0 and d["scaling"] == "strong"
     assert d["settle"]["frames"] == 2 * 3  # per timed scheme, the same count on every rank
+    # the settled figure is reported beside the value, never as it
+    assert d["settled"]["extra_frames"] == 4 and d["settled"]["ms_per_step"] > 0

@@ -108,11 +108,10 @@ def test_records_fetched_counter(built):
         assert 0 < st["records_fetched"] <= 4 * st["pairs"]
         assert st["records_fetched"] < 4 * st["pairs"]  # dense scene: tiles saturate and stop fetching
         tiles = 4 * st["tiles"]
-        # (two-slab frames: both composites read the ranges, and the open
-        # tiles' pixel states are written and read back, 16 B each way)
-        two = st["two_slab"]
-        assert st["bytes_composite"] == tiles * 8 * (2 if two else 1) + w * h * 16 + st["records_fetched"] * 52 + \
-            st["open_tiles"] * 256 * 32
+        # (depth-cut frames: the open quadrants' pixel states are written
+        # and read back, 16 B each way)
+        assert st["bytes_composite"] == tiles * 8 + w * h * 16 + st["records_fetched"] * 52 + \
+            st["open_tiles"] * 64 * 32
         got[binning] = st["records_fetched"]
     assert got["depth_first"] == got["bin_first"]
 

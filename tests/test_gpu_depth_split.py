@@ -1,16 +1,19 @@
-"""Two-slab frames (gs_options.depth_split = 1): bin-first frames
-built and composited in two depth slabs, the second slab's pairs emitted and
-sorted only for the bins the first slab's composite left open.  The per-pixel
-operation sequence is the one-slab sequence of tile.metal:239-266 (the first
-slab holds every pair below the depth-key cut, so it precedes the rest in S1
-order), so the image must be bit-identical to the one-slab frame and to the
-oracle, whatever the cut.
+"""Depth-cut frames (gs_options.depth_split = 1).
 
-Covered: dense scenes (most bins close in the first slab), sparse ones
-(every bin stays open), the live-50 rule, SH3, tiny / ragged frames, two
-frames in flight over a camera path with growing pair counts, and the cut
-pushed to both extremes (GS_DEPTH_SPLIT_FRAC is read once per process, so
-the extremes run in child processes)."""
+A bin-first frame's lists hold only the pairs whose depth key lies at or
+ahead of their bin's cut (S1 order, tile.metal:239-249), the key at which
+the bin's tiles finished in the set's previous frame, plus a margin.  A tile
+those lists leave open keeps its per-pixel state and finishes with the rest
+of its bin's pairs (the fallback lists).  Whatever the cuts, each pixel sees
+the full list's operation sequence (tile.metal:251-266 / 50layer.metal:
+208-222), so every frame must be bit-identical to the whole-list frame and
+to the oracle.
+
+Covered: static and moving cameras (the cuts then lag the view), camera
+jumps that leave many tiles open, sparse scenes that never saturate, the
+live-50 rule, SH3, BGRA8 output, one and two frames in flight, resolution
+changes, lists over 8192 pairs, and a zero margin (GS_CUT_MARGIN, read once
+per process, so in a child process)."""
 import os
 import subprocess
 import sys
@@ -35,8 +38,8 @@ def _scene(n, seed, sh, aspect, scale=1.0):
 def _pair(sc, **kw):
     from gaussian_splat_amd import InstancedSplatRenderer, Options
     out = []
-    for split in (True, False):
-        r = InstancedSplatRenderer(sc, Options(binning="bin_first", crop=False, depth_split=split, **kw))
+    for cut in (True, False):
+        r = InstancedSplatRenderer(sc, Options(binning="bin_first", crop=False, depth_split=cut, **kw))
         r.initialize(0)
         out.append(r)
     return out
@@ -46,52 +49,109 @@ def _bits(a, b):
     return int(np.count_nonzero(np.asarray(a).view(np.uint32) != np.asarray(b).view(np.uint32)))
 
 
-@pytest.mark.parametrize("n,w,h,mode,sh,scale", [
-    (300000, 640, 360, "tile", 0, 1.0),    # dense: most bins close in the first slab
-    (300000, 640, 360, "live50", 0, 1.0),
-    (120000, 960, 540, "tile", 3, 1.5),
-    (8000, 640, 360, "tile", 0, 0.5),      # sparse: nothing saturates, every bin stays open
-    (40000, 17, 9, "tile", 0, 1.0),        # ragged single-bin frame
-    (5000, 1, 1, "live50", 0, 1.0),
-    (200000, 1920, 1080, "tile", 0, 3.0),  # large splats, long lists (> 8192 per bin)
+def _path(w, h, kind, n):
+    """Camera path: 'still' (one view), 'orbit' (small steps, the cuts lag
+    by a frame), 'jump' (large turns and zooms: stale cuts everywhere)."""
+    from gaussian_splat_amd.api import default_camera
+    views = []
+    for k in range(n):
+        cam = default_camera(w, h)
+        if kind == "orbit":
+            cam.orbit(0.02 * k, 0.005 * k)
+        elif kind == "jump":
+            cam.setDistance((6.0, 2.5, 4.0, 1.8, 5.0, 3.0)[k % 6])
+            cam.orbit(0.9 * k, 0.15 * (k % 3))
+        views.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
+    return views
+
+
+@pytest.mark.parametrize("n,w,h,mode,sh,scale,path", [
+    (300000, 640, 360, "tile", 0, 1.0, "still"),
+    (300000, 640, 360, "tile", 0, 1.0, "orbit"),
+    (300000, 640, 360, "live50", 0, 1.0, "jump"),
+    (120000, 960, 540, "tile", 3, 1.5, "jump"),
+    (8000, 640, 360, "tile", 0, 0.5, "orbit"),      # sparse: nothing saturates, no list is cut
+    (40000, 17, 9, "tile", 0, 1.0, "jump"),         # ragged single-bin frame
+    (5000, 1, 1, "live50", 0, 1.0, "orbit"),
+    (200000, 1920, 1080, "tile", 0, 3.0, "jump"),   # large splats, long lists (> 8192 per bin)
 ])
-def test_two_slab_bitexact(built, n, w, h, mode, sh, scale):
+def test_depth_cuts_bitexact(built, n, w, h, mode, sh, scale, path):
     from oracle import oracle_py as O
     sc = _scene(n, 131 + n % 7, sh, w / h, scale)
-    two, one = _pair(sc, mode=mode, sh_degree=sh)
-    for V, P in orbit_views(w, h, 2):
-        a = two.render_host(V, P, w, h)
-        b = one.render_host(V, P, w, h)
-        assert _bits(a, b) == 0
-        st, so = two.last_stats(), one.last_stats()
+    cut, whole = _pair(sc, mode=mode, sh_degree=sh)
+    opened = 0
+    for k, (V, P) in enumerate(_path(w, h, path, 6)):
+        a = cut.render_host(V, P, w, h)
+        b = whole.render_host(V, P, w, h)
+        assert _bits(a, b) == 0, k
+        st, so = cut.last_stats(), whole.last_stats()
         assert st["two_slab"] == 1 and so["two_slab"] == 0
-        assert st["pairs"] == so["pairs"] and st["pairs_sorted"] <= st["pairs"]
-        assert 0 <= st["open_tiles"] <= 4 * st["tiles"]
-        ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
-        assert _bits(a, ref) == 0
-    print(f"{n} @{w}x{h} {mode}: pairs {st['pairs']} sorted {st['pairs_sorted']} open tiles {st['open_tiles']} "
-          f"cut {st['depth_cut']:#x}")
+        # (a large rect's pairs behind the cut sit in both lists, CutSel)
+        assert st["pairs"] == so["pairs"] and st["pairs_sorted"] <= 2 * st["pairs"]
+        assert 0 <= st["open_tiles"] <= 16 * st["tiles"]  # (8x8 quadrants left open)
+        opened += st["open_tiles"]
+        if k in (0, 5):
+            ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
+            assert _bits(a, ref) == 0, k
+    print(f"{n} @{w}x{h} {mode} {path}: pairs {st['pairs']} sorted {st['pairs_sorted']} open tiles (sum) {opened}")
 
 
-def test_two_slab_dense_scene_saves_pairs(built):
-    """On the bench-like dense scene most bins close in the first slab: the
-    frame sorts well under the one-slab pair count."""
+def test_depth_cuts_still_camera_saves_pairs(built):
+    """The bench-like dense scene under a still camera: from the third frame
+    on, the lists hold a fraction of the pairs and no tile is left open."""
     # the bench scene's coverage per pixel (6M splats @1080p) at a quarter of
     # the pixels: 1.5M splats of twice the size @960x540
     sc = _scene(1_500_000, 5, 0, 16 / 9, scale=2.0)
-    two, one = _pair(sc)
+    cut, whole = _pair(sc)
     V, P = orbit_views(960, 540, 1)[0]
-    assert _bits(two.render_host(V, P, 960, 540), one.render_host(V, P, 960, 540)) == 0
-    st = two.last_stats()
-    assert st["pairs_sorted"] < 0.8 * st["pairs"], st
-    assert st["open_tiles"] < 2 * st["tiles"], st  # fewer than half of the 16x16 tiles stay open
+    ref = whole.render_host(V, P, 960, 540)
+    for k in range(4):
+        assert _bits(cut.render_host(V, P, 960, 540), ref) == 0, k
+    st = cut.last_stats()
+    assert st["pairs_sorted"] < 0.6 * st["pairs"], st
+    assert st["open_tiles"] == 0, st
 
 
-def test_two_slab_pipelined_camera_path(built):
-    """Two frames in flight: the second slab's lists are built on the
-    composite stream while the side stream projects the next frame into the
-    other buffer set (rects, cut and scratch per set).  A camera path whose
-    pair count grows makes the first frames re-queue with larger buffers."""
+def test_depth_cuts_jump_opens_tiles(built):
+    """One frame in flight: each frame uses the previous frame's cuts.  A
+    view that moves the scene nearer after a still stretch leaves tiles open
+    (their saturation lies behind the old cuts); the fallback lists finish
+    them, bit for bit."""
+    from gaussian_splat_amd.api import default_camera
+    W, H = 640, 360
+    sc = _scene(400000, 23, 0, W / H, scale=1.2)
+    cut, whole = _pair(sc)
+    far = default_camera(W, H)
+    far.setDistance(7.0)
+    near = default_camera(W, H)
+    near.setDistance(2.0)
+    near.orbit(0.4, 0.1)
+    opened = 0
+    for cam in (far, far, far, near, near, far, near):
+        V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+        assert _bits(cut.render_host(V, P, W, H), whole.render_host(V, P, W, H)) == 0
+        opened += cut.last_stats()["open_tiles"]
+    assert opened > 0
+
+
+def test_depth_cuts_bgra8_and_resolution_change(built):
+    """BGRA8 output in depth-cut frames (the open tiles' states live in their
+    own buffer), and a resolution change (the cuts start over)."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    sc = _scene(250000, 31, 0, 16 / 9)
+    cut, whole = _pair(sc)
+    for (w, h) in ((640, 360), (640, 360), (800, 450), (800, 450), (640, 360), (640, 360)):
+        for V, P in _path(w, h, "orbit", 2):
+            assert _bits(cut.render_bgra8_host(V, P, w, h), whole.render_bgra8_host(V, P, w, h)) == 0
+            assert _bits(cut.render_host(V, P, w, h), whole.render_host(V, P, w, h)) == 0
+
+
+def test_depth_cuts_pipelined_camera_path(built):
+    """Two frames in flight: a frame's cuts come from the frame before last
+    (its buffer set); its fallback lists are built on the composite stream
+    while the side stream projects the next frame into the other set (rects,
+    open flags, cut tables per set).  A camera path whose pair count grows
+    makes the first frames re-queue with larger buffers."""
     import torch
 
     from gaussian_splat_amd import InstancedSplatRenderer, Options, default_camera
@@ -109,35 +169,36 @@ def test_two_slab_pipelined_camera_path(built):
     r = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False, binning="bin_first", frames_in_flight=2,
                                            depth_split=True))
     r.initialize(0)
-    outs = [r.render(V, P, W, H) for V, P in views for _ in range(2)]
+    outs = [r.render(V, P, W, H).clone() for V, P in views for _ in range(3)]
     torch.cuda.synchronize()
     for k, o in enumerate(outs):
-        assert _bits(o.cpu().numpy(), refs[k // 2]) == 0, k
+        assert _bits(o.cpu().numpy(), refs[k // 3]) == 0, k
     assert r.last_stats()["two_slab"] == 1
 
 
 _CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
-from test_gpu_depth_split import _scene, _pair, _bits
-from conftest import orbit_views
+from test_gpu_depth_split import _scene, _pair, _bits, _path
 sc = _scene(200000, 9, 0, 16 / 9)
-two, one = _pair(sc)
-V, P = orbit_views(640, 360, 1)[0]
-a = two.render_host(V, P, 640, 360); b = one.render_host(V, P, 640, 360)
-st = two.last_stats()
-assert st["two_slab"] == 1 and _bits(a, b) == 0, (st, _bits(a, b))
-print("ok", st["pairs"], st["pairs_sorted"], st["open_tiles"], hex(st["depth_cut"]))
+cut, whole = _pair(sc)
+opened = 0
+for V, P in _path(640, 360, "orbit", 8):
+    a = cut.render_host(V, P, 640, 360); b = whole.render_host(V, P, 640, 360)
+    st = cut.last_stats()
+    assert st["two_slab"] == 1 and _bits(a, b) == 0, (st, _bits(a, b))
+    opened += st["open_tiles"]
+print("ok", st["pairs"], st["pairs_sorted"], opened)
 """
 
 
-@pytest.mark.parametrize("frac", ["0.0", "0.999", "0.6"])
-def test_two_slab_cut_extremes(built, frac):
-    """The cut at the front (the first slab holds the farthest bucket only),
-    at the back (nearly everything in the first slab) and in between: the
-    same image every time."""
-    env = dict(os.environ, GS_DEPTH_SPLIT_FRAC=frac)
+@pytest.mark.parametrize("margin", ["0", "1000"])
+def test_depth_cuts_margin_extremes(built, margin):
+    """No margin (the cuts sit on the last record each tile staged, so a
+    moving camera opens tiles every frame) and a wide one: the same image
+    every time."""
+    env = dict(os.environ, GS_CUT_MARGIN=margin)
     code = _CHILD.format(root=str(ROOT), tests=str(ROOT / "tests"))
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout + p.stderr
-    print(frac, p.stdout.strip())
+    print(margin, p.stdout.strip())

@@ -489,30 +489,6 @@ def test_radix_sort(built, n, bits):
     np.testing.assert_array_equal(vt.cpu().numpy().view(np.uint32), v[order])
 
 
-@pytest.mark.parametrize("n,bits,frac", [(1, 4, 1.0), (5000, 6, 0.5), (123457, 11, 0.3), (2_000_003, 13, 0.7),
-                                         (300000, 11, 0.0), (6144 * 3, 16, 1.0)])
-def test_radix_sort_filtered(built, n, bits, frac):
-    """The second-slab sort (gs_radix_sort_pairs_filtered): pairs whose bin
-    (key bits [0, bits)) is open are kept and stably sorted by bin, the depth
-    bits above riding along; the others are dropped (numpy restatement)."""
-    import torch
-    from gaussian_splat_amd.api import radix_sort_pairs_filtered
-    rng = np.random.default_rng(n * 7 + bits)
-    k = (rng.integers(0, 1 << bits, n, dtype=np.uint64) | (rng.integers(0, 1 << (32 - bits), n, dtype=np.uint64)
-                                                           << np.uint64(bits))).astype(np.uint32)
-    v = rng.integers(0, 1 << 31, n, dtype=np.uint64).astype(np.uint32)
-    open_bins = (rng.random(1 << bits) < frac).astype(np.int32)
-    kept = open_bins[k & ((1 << bits) - 1)] != 0
-    order = np.argsort(k[kept] & ((1 << bits) - 1), kind="stable")
-    ko, vo = radix_sort_pairs_filtered(torch.from_numpy(k.view(np.int32)).cuda(),
-                                       torch.from_numpy(v.view(np.int32)).cuda(), bits,
-                                       torch.from_numpy(open_bins).cuda())
-    torch.cuda.synchronize()
-    assert ko.numel() == int(kept.sum())
-    np.testing.assert_array_equal(ko.cpu().numpy().view(np.uint32), k[kept][order])
-    np.testing.assert_array_equal(vo.cpu().numpy().view(np.uint32), v[kept][order])
-
-
 def test_empty_and_culled(built):
     from gaussian_splat_amd import scene as S
     sc = _scene(5000, 2, 0)

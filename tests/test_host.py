@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol(built):
     for name in sorted(declared):
         assert hasattr(L, name), name
     assert set(_lib.SIGNATURES) == declared
-    assert L.gs_abi_version() == 8
+    assert L.gs_abi_version() == 9
     assert L.gs_exchange_record_bytes() == 48
 
 
