@@ -90,6 +90,27 @@ def test_composite_known_answers(case, mode):
     np.testing.assert_allclose(out, c[mode], rtol=0, atol=2e-7)
 
 
+@pytest.mark.parametrize("case", sorted(KA["composite"]))
+def test_composite_known_answers_aform(case):
+    """The T-form contract against the reference's own A-form
+    (tile.metal:252-263: sa = alpha (1 - A), A += sa, break at A >= 0.99),
+    derived in float64 and float32 (tools/make_golden.py).  Where both forms
+    break after the same record the answers agree to rounding; where the break
+    flips, A reaches 0.99 within 1e-5 at that test (a straddle, the 0.99 edge
+    of tests/pixel_pins.py), and the case is named."""
+    c = KA["composite"][case]
+    out = O.composite_list(np.array(c["frags"], np.float32).reshape(-1, 5), mode="tile", cap=c.get("cap", 0))
+    if not c["straddle"]:
+        assert c["n_tform"] == c["n_aform64"] == c["n_aform32"]
+        np.testing.assert_allclose(out, c["tile_aform64"], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(out, c["tile_aform32"], rtol=0, atol=2.5e-7)
+    else:
+        assert case == "saturate_edge", "an unexpected break flip between the T-form and the A-form"
+        assert abs(c["straddle_A"] - 0.99) < 1e-5
+        # the A-form stops one record earlier; that record's weight is what separates them
+        assert c["n_tform"] == c["n_aform64"] + 1
+
+
 def test_survey_depth_order_finding():
     """descending distance -> the farthest (green) ends on top."""
     out = O.composite_list(np.array(KA["composite"]["survey_rgb"]["frags"], np.float32), "tile")

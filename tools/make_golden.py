@@ -141,6 +141,34 @@ def known_answers() -> dict:
                 break
         return [float(C[0]), float(C[1]), float(C[2]), float(np.float32(1) - T)]
 
+    def tile_rule_aform(fr, dt):
+        # the reference's own form, tile.metal:252-263: sa = alpha (1 - A),
+        # C += c sa, A += sa, break at A >= 0.99 (there in half; here in
+        # float64 and float32).  Returns (rgba, records composited, the A
+        # before each break test).
+        order = sorted(range(len(fr)), key=lambda i: (-float(np.float16(fr[i][0])), i))
+        A = dt(0); C = np.zeros(3, dt); n = 0; hist = []
+        for i in order:
+            d, rr, g, b, al = (dt(v) for v in fr[i])
+            sa = dt(al * (dt(1) - A))
+            C = (C + np.array([rr, g, b], dt) * sa).astype(dt)
+            A = dt(A + sa)
+            n += 1
+            hist.append(float(A))
+            if A >= dt(0.99):
+                break
+        return [float(C[0]), float(C[1]), float(C[2]), float(A)], n, hist
+
+    def tile_count(fr):  # records the T-form contract composites
+        order = sorted(range(len(fr)), key=lambda i: (-float(np.float16(fr[i][0])), i))
+        T = np.float32(1); n = 0
+        for i in order:
+            T = np.float32(T - np.float32(np.float32(fr[i][4]) * T))
+            n += 1
+            if T <= np.float32(0.01):
+                break
+        return n
+
     def live_rule(fr):  # 50layer.metal:197-222
         order = sorted(range(len(fr)), key=lambda i: (-float(np.float16(fr[i][0])), i))
         T = np.float32(1); C = np.zeros(3, np.float32)
@@ -168,6 +196,21 @@ def known_answers() -> dict:
     many = [[1.0 + 0.1 * i, (i % 3 == 0) * 1.0, (i % 3 == 1) * 1.0, (i % 3 == 2) * 1.0, 0.05] for i in range(40)]
     ka["composite"]["cap32"] = {"frags": many, "cap": 32, "tile": tile_rule(many[:32]),
                                 "live50": live_rule(many[:32])}
+    # The tile rule's answers in the reference's A-form,
+    # beside the T-form contract's.  A case whose break
+    # index differs between the forms is a straddle: A lands within 1e-5 of
+    # 0.99 there, and the f32 rounding of either form decides.
+    for k, c in ka["composite"].items():
+        fr = c["frags"][:c["cap"]] if c.get("cap") else c["frags"]
+        a64, n64, h64 = tile_rule_aform(fr, np.float64) if fr else ([0, 0, 0, 0], 0, [])
+        a32, n32, _ = tile_rule_aform(fr, np.float32) if fr else ([0, 0, 0, 0], 0, [])
+        nt = tile_count(fr) if fr else 0
+        c["tile_aform64"], c["tile_aform32"] = a64, a32
+        c["n_tform"], c["n_aform64"], c["n_aform32"] = nt, n64, n32
+        c["straddle"] = bool(nt != n64 or nt != n32)
+        if c["straddle"]:  # the A (float64) at the first break test whose outcome differs
+            j = min(nt, n64, n32) - 1
+            c["straddle_A"] = h64[j]
     ka["half_bits"] = {"1.0": 0x3C00, "0.2": 0x3266, "65504.0": 0x7BFF, "65520.0": 0x7C00, "0.0001": 0x068E,
                        "5.3851647": int(np.float16(5.3851647).view(np.uint16)), "1000.0": 0x63D0}
     return ka
