@@ -274,7 +274,7 @@ def main():
 
     settled = {"frames": 0, "ms": 0.0}
 
-    def timed(step, steps, warmup, settle=None):
+    def timed(step, steps, warmup, settle=None, drain=None):
         # --settle: untimed frames before the warmup (default none, the
         # driver's --warmup governs).  Every rank runs the same count, so
         # collectives stay matched.
@@ -287,6 +287,8 @@ def main():
         settled["ms"] += (time.perf_counter() - t_s) * 1e3
         for _ in range(warmup):
             step()
+        if drain is not None:
+            drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -294,6 +296,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
+        if drain is not None:  # (pipelined row frames: the last frame finishes inside the timed region)
+            drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -304,7 +308,7 @@ def main():
             dt = float(t.item())
         return dt * 1e3 / steps
 
-    def settled_probe(step, steps):
+    def settled_probe(step, steps, drain=None):
         # The value is the driver's protocol (its --warmup only).  The GPU
         # leaves idle clocks over the first ~40 frames (5-frame blocks 0.89 ->
         # 0.78 ms at 1080p, tools/warm_probe.py), so the same K
@@ -314,7 +318,7 @@ def main():
             return None
         for _ in range(args.settled_probe):
             step()
-        return {"extra_frames": args.settled_probe, "ms_per_step": round(timed(step, steps, 0, settle=0), 4),
+        return {"extra_frames": args.settled_probe, "ms_per_step": round(timed(step, steps, 0, settle=0, drain=drain), 4),
                 "note": "the same frames timed again after the value's run and these extra untimed frames"}
 
     schemes = {}
@@ -335,6 +339,7 @@ def main():
         else:
             step = lambda: r.render(view, proj, W, H, out=out)
         rh = r
+        drain = None
         ms = timed(step, args.steps, args.warmup)
         settled_line = settled_probe(step, args.steps)
     else:
@@ -356,13 +361,20 @@ def main():
                 sr = SlabRenderer(be, rank, world)
             else:
                 be = HipShardBackend(scene, rank, world, b, opts, local)
-                sr = ShardedRenderer(be, rank, world)
+                # two frames in flight: frame k's record exchange (its own
+                # communicator) overlaps frame k-1's render and gather
+                pipe = args.frames_in_flight >= 2
+                sr = ShardedRenderer(be, rank, world, pipeline=pipe,
+                                     exchange_group=dist.new_group(backend=backend) if pipe else None)
             stp = (lambda s_=sr: s_.render(view, proj, W, H, gather=True))
-            schemes[sch] = {"ms": timed(stp, args.steps, args.warmup), "handle": be.r, "step": stp}
+            drn = getattr(sr, "flush", None) if getattr(sr, "pipeline", False) else None
+            schemes[sch] = {"ms": timed(stp, args.steps, args.warmup, drain=drn), "handle": be.r, "step": stp,
+                            "drain": drn}
         # the splat-sharded exact scheme is the headline whenever it ran
         head = "rows" if "rows" in schemes else order[0]
         ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
-        settled_line = settled_probe(step, args.steps)
+        drain = schemes[head]["drain"]
+        settled_line = settled_probe(step, args.steps, drain=drain)
     value = N / (ms * 1e-3) / 1e6
 
     s0 = rh.last_stats()
@@ -400,6 +412,8 @@ def main():
             stats.append(rh.last_stats())
         st = stage_summary(stats)
         rh.set_stage_timing(timing)
+    if drain is not None:  # (pipelined row frames: every rank finishes the frame in flight)
+        drain()
 
     line = None
     if rank == 0:
@@ -419,7 +433,8 @@ def main():
             "config": {"workload": args.label, "global_splats": N, "width": W, "height": H, "sh_degree": args.sh,
                        "parallelism": ((f"rows: {world} ranks, splat-index shards of one global scene, 32-px bin-row "
                                         f"ownership, all_to_all of projected records + band gather ({backend}, world "
-                                        f"{world})")
+                                        f"{world}" + ("; 2 frames in flight: a frame's exchange under the previous "
+                                                      "frame's render" if drain is not None else "") + ")")
                                        if head == "rows" else
                                        (f"bands: {world} ranks, the scene replicated on every rank, each renders its "
                                         f"32-px bin rows, band gather ({backend}, world {world})")

@@ -120,57 +120,73 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
     }
 }
 
-// Cell-exclusion mask (gs_device.h): which 8x8 pixel cells of the rect's
-// first 4x4 the q <= 2 ln 100 ellipse provably misses.  In pixel offsets
+// Cell-exclusion masks (gs_device.h): which cells of the rect's first 4x4
+// the q <= 2 ln 100 ellipse provably misses.  In pixel offsets
 // X = px + 0.5 - cx, Y = cy - (py + 0.5) the record gives u = X ax + Y ay,
 // v = X bx + Y by, so q = aX^2 + 2bXY + cY^2 with a = ax^2 + bx^2,
-// b = ax ay + bx by, c = ay^2 + by^2, det = ac - b^2.  For each 8-px row
-// band [Ya, Yb] the ellipse's X extent is closed form: X(Y) =
+// b = ax ay + bx by, c = ay^2 + by^2, det = ac - b^2.  For each row band of
+// pixel centres [Ya, Yb] the ellipse's X extent is closed form: X(Y) =
 // (-bY +- sqrt(Qa - det Y^2)) / a, extremal at the band ends or at the
 // ellipse's own x-extreme points Y = -+b sqrt(Q/(c det)).  Q and the X range
 // carry a margin, so a cell is excluded only when no pixel centre of it can
 // be covered (the composite then skips a record that would add exact zeros).
-template <int SHIFT>  // cell size 1 << SHIFT px: 3 = the composite's 8x8 cells, 5 = 32x32 bins
-__device__ __forceinline__ uint32_t cell_exclusion_mask(float cx, float cy, float ax, float ay, float bx, float by,
-                                                        uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
-    constexpr uint32_t CS = 1u << SHIFT;
-    const uint32_t cx0 = x0 >> SHIFT, cy0 = y0 >> SHIFT, cx1 = x1 >> SHIFT, cy1 = y1 >> SHIFT;
-    if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
-    if (cx1 == cx0 && cy1 == cy0) return 0u;  // one cell: the rect itself decides
-    const float a = ax * ax + bx * bx, b = ax * ay + bx * by, c = ay * ay + by * by;
+// The ellipse terms are shared by the 8x8-cell and 32x32-bin masks; a band's
+// X range becomes the row's candidate cells [ql, qh] in integers.
+struct EllipseX {
+    float b, ia, det, Qa, ymax, xs, ys, pad;
+    bool ok;
+};
+__device__ __forceinline__ EllipseX ellipse_x(float ax, float ay, float bx, float by) {
+    EllipseX e;
+    const float a = ax * ax + bx * bx, c = ay * ay + by * by;
+    e.b = ax * ay + bx * by;
     // det = ac - b^2 = (ax by - ay bx)^2: the record's axes are orthogonal, so
     // the cross product does not cancel (ac - b^2 would, for thin ellipses)
     const float cr = ax * by - ay * bx;
-    const float det = cr * cr;
-    if (!(det > 0.0f) || !(a > 0.0f) || !(c > 0.0f) || !(det < 3.0e38f)) return 0u;  // degenerate: no claim
+    e.det = cr * cr;
+    e.ok = e.det > 0.0f && a > 0.0f && c > 0.0f && e.det < 3.0e38f;  // degenerate: no claim
     // hardware approximations (v_rcp_f32, v_sqrt_f32: ~1 ulp) are well inside
     // the 0.2 % margin on Q and the padding on X
     const float Q = kQMax * 1.002f + 1e-3f;
-    const float ia = __builtin_amdgcn_rcpf(a), idet = __builtin_amdgcn_rcpf(det);
-    const float ymax = __builtin_amdgcn_sqrtf(Q * a * idet);          // |Y| reach of the ellipse
-    const float xs = __builtin_amdgcn_sqrtf(Q * c * idet);            // X of the x-extreme points
-    const float ys = b * xs * __builtin_amdgcn_rcpf(c);               // max-X point at Y = -ys, min-X at +ys
+    e.Qa = Q * a;
+    e.ia = __builtin_amdgcn_rcpf(a);
+    const float idet = __builtin_amdgcn_rcpf(e.det);
+    e.ymax = __builtin_amdgcn_sqrtf(e.Qa * idet);               // |Y| reach of the ellipse
+    e.xs = __builtin_amdgcn_sqrtf(Q * c * idet);                // X of the x-extreme points
+    e.ys = e.b * e.xs * __builtin_amdgcn_rcpf(c);               // max-X point at Y = -ys, min-X at +ys
+    e.pad = 0.01f + 1e-3f * fabsf(e.xs);
+    return e;
+}
+template <int SHIFT>  // cell size 1 << SHIFT px: 3 = the composite's 8x8 cells, 5 = 32x32 bins
+__device__ __forceinline__ uint32_t cell_exclusion_mask(const EllipseX& e, float cx, float cy, uint32_t x0, uint32_t y0,
+                                                        uint32_t x1, uint32_t y1) {
+    constexpr uint32_t CS = 1u << SHIFT;
+    constexpr float ICS = 1.0f / (float)CS;
+    const uint32_t cx0 = x0 >> SHIFT, cy0 = y0 >> SHIFT, cx1 = x1 >> SHIFT, cy1 = y1 >> SHIFT;
+    if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
+    if (cx1 == cx0 && cy1 == cy0) return 0u;  // one cell: the rect itself decides
+    if (!e.ok) return 0u;
+    const uint32_t all = (1u << (cx1 - cx0 + 1u)) - 1u;  // the rect's cells in a row
+    const float fcx0 = (float)cx0;
     uint32_t excl = 0;
     for (uint32_t r = 0; r <= cy1 - cy0; ++r) {
         const float pyA = (float)((cy0 + r) * CS);  // band's pixel rows pyA .. pyA+CS-1
         float yl = cy - (pyA + ((float)CS - 0.5f)), yh = cy - (pyA + 0.5f);
-        yl = fmaxf(yl, -ymax);
-        yh = fminf(yh, ymax);
-        float xmin = 1e30f, xmax = -1e30f;  // (empty unless the band meets the ellipse)
+        yl = fmaxf(yl, -e.ymax);
+        yh = fminf(yh, e.ymax);
+        uint32_t keep = 0u;  // (none unless the band meets the ellipse)
         if (yl <= yh) {
-            auto root = [&](float y) { return __builtin_amdgcn_sqrtf(fmaxf(Q * a - det * y * y, 0.0f)); };
-            auto xhi = [&](float y) { return (-b * y + root(y)) * ia; };
-            auto xlo = [&](float y) { return (-b * y - root(y)) * ia; };
-            xmax = (-ys >= yl && -ys <= yh) ? xs : fmaxf(xhi(yl), xhi(yh));
-            xmin = (ys >= yl && ys <= yh) ? -xs : fminf(xlo(yl), xlo(yh));
-            const float pad = 0.01f + 1e-3f * fabsf(xs);
-            xmax += pad;
-            xmin -= pad;
+            auto root = [&](float y) { return __builtin_amdgcn_sqrtf(fmaxf(e.Qa - e.det * y * y, 0.0f)); };
+            const float rl = root(yl), rh = root(yh);
+            const float xmax = ((-e.ys >= yl && -e.ys <= yh) ? e.xs : fmaxf(-e.b * yl + rl, -e.b * yh + rh) * e.ia) + e.pad;
+            const float xmin = ((e.ys >= yl && e.ys <= yh) ? -e.xs : fminf(-e.b * yl - rl, -e.b * yh - rh) * e.ia) - e.pad;
+            // cell q (pixel centres X = (cx0+q) CS + 0.5 - cx .. + CS - 1) is a
+            // candidate iff its first centre <= xmax and its last >= xmin
+            const float qh = fminf(fmaxf(floorf((xmax + cx - 0.5f) * ICS) - fcx0, -1.0f), 4.0f);
+            const float ql = fminf(fmaxf(ceilf((xmin + cx + 0.5f) * ICS - 1.0f) - fcx0, 0.0f), 5.0f);
+            keep = ((1u << ((uint32_t)(int)qh + 1u)) - 1u) & ~((1u << (uint32_t)(int)ql) - 1u);
         }
-        for (uint32_t q = 0; q <= cx1 - cx0; ++q) {
-            const float px0 = (float)((cx0 + q) * CS) + 0.5f - cx;  // cell's X range
-            if (px0 + (float)(CS - 1u) < xmin || px0 > xmax) excl |= 1u << (r * 4u + q);
-        }
+        excl |= (all & ~keep) << (r * 4u);
     }
     return excl;
 }
@@ -344,11 +360,12 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
 #ifdef GS_AB_NO_MASKS  // A/B build: masks off (cost of the masks in this kernel)
                     const uint32_t excl = 0u, bexcl = 0u;
 #else
-                    const uint32_t excl =
-                        U.cell_mask ? cell_exclusion_mask<3>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1) : 0u;
-                    const uint32_t bexcl =
-                        U.cell_mask ? cell_exclusion_mask<kBinShift>(cx, cy, ra.z, ra.w, rb.x, rb.y, x0, y0, x1, y1)
-                                    : 0u;
+                    uint32_t excl = 0u, bexcl = 0u;
+                    if (U.cell_mask) {
+                        const EllipseX ex = ellipse_x(ra.z, ra.w, rb.x, rb.y);
+                        excl = cell_exclusion_mask<3>(ex, cx, cy, x0, y0, x1, y1);
+                        bexcl = cell_exclusion_mask<kBinShift>(ex, cx, cy, x0, y0, x1, y1);
+                    }
 #endif
                     o[0] = ra;
                     o[1] = rb;

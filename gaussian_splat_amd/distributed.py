@@ -13,6 +13,12 @@ straddle an ownership boundary.  Per frame:
                         owned bin rows (a compact band buffer)
   4. gather             bands -> rank 0, scattered back into the frame
 
+Pipelined (`ShardedRenderer(pipeline=True)`, two frames in flight): a call
+projects frame k and starts its record exchange (asynchronous, on its own
+process group), then renders and gathers frame k-1, whose records arrived
+while frame k was projected; `flush()` finishes the last frame.  The link
+transfer of one frame overlaps the other frame's compute.
+
 Records arrive in source-rank order = global splat-index order, so each
 owned bin sees exactly the single-GPU list order: the assembled frame is
 bit-identical to a 1-GPU render (tests/test_gpu_parity.py,
@@ -173,17 +179,26 @@ class HipShardBackend:
                   "gs_shard_set_rows")
         self.world, self.rank, self.device = world, rank, torch.device(f"cuda:{device}")
         self.xbytes = int(lib().gs_exchange_record_bytes())
-        self.send = torch.empty(max(1, shard.n * world * self.xbytes), dtype=torch.uint8, device=self.device)
+        self._send = [torch.empty(max(1, shard.n * world * self.xbytes), dtype=torch.uint8, device=self.device)]
 
-    def project(self, view, proj, width, height):
+    @property
+    def send(self):
+        return self._send[0]
+
+    def project(self, view, proj, width, height, slot: int = 0):
+        """Project and pack into send buffer `slot` (0/1: a pipelined frame's
+        exchange may still be reading the other)."""
         import torch
 
+        while len(self._send) <= slot:
+            self._send.append(torch.empty_like(self._send[0]))
+        buf = self._send[slot]
         counts = (C.c_int64 * self.world)()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         check(lib().gs_shard_project(self.r._h, _mat16(view), _mat16(proj), width, height,
-                                     C.c_void_p(self.send.data_ptr()), self.send.numel(), counts,
+                                     C.c_void_p(buf.data_ptr()), buf.numel(), counts,
                                      C.c_void_p(stream)), "gs_shard_project")
-        return self.send, [int(c) for c in counts]
+        return buf, [int(c) for c in counts]
 
     def empty(self, nbytes):
         import torch
@@ -319,8 +334,23 @@ def _host_staged(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-def exchange(send, counts, xbytes, world, group=None):
-    """all_to_all of counts then of records (bytes); returns (recv, nrec)."""
+class PendingExchange:
+    """A record all_to_all in flight (exchange_start); wait() -> (recv, nrec)."""
+
+    def __init__(self, work, recv, total, dev):
+        self.work, self.recv, self.total, self.dev = work, recv, total, dev
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()  # (RCCL: the current stream waits for the exchange)
+            self.work = None
+        recv = self.recv if self.recv.device == self.dev else self.recv.to(self.dev)
+        return recv, self.total
+
+
+def exchange_start(send, counts, xbytes, world, group=None) -> PendingExchange:
+    """all_to_all of counts (the host sizes the receive buffer), then the
+    records' all_to_all started asynchronously."""
     import torch
     import torch.distributed as dist
 
@@ -334,28 +364,61 @@ def exchange(send, counts, xbytes, world, group=None):
     ssz = sum(counts) * xbytes
     recv = torch.empty(max(1, total * xbytes), dtype=torch.uint8, device=cdev)
     src = send[:ssz] if cdev == dev else send[:ssz].cpu()
-    dist.all_to_all_single(recv[: total * xbytes], src, [c * xbytes for c in rcounts],
-                           [c * xbytes for c in counts], group=group)
-    return (recv if cdev == dev else recv.to(dev)), total
+    work = dist.all_to_all_single(recv[: total * xbytes], src, [c * xbytes for c in rcounts],
+                                  [c * xbytes for c in counts], group=group, async_op=True)
+    return PendingExchange(work, recv, total, dev)
+
+
+def exchange(send, counts, xbytes, world, group=None):
+    """all_to_all of counts then of records (bytes); returns (recv, nrec)."""
+    return exchange_start(send, counts, xbytes, world, group).wait()
 
 
 class ShardedRenderer:
-    """One rank of a multi-GPU frame (torch.distributed must be initialised)."""
+    """One rank of a multi-GPU frame (torch.distributed must be initialised).
 
-    def __init__(self, backend, rank: int, world: int, group=None):
+    pipeline=True: two frames in flight.  render() projects this frame and
+    starts its record exchange on `exchange_group` (its own communicator, so
+    it runs beside the gather), then renders and gathers the PREVIOUS frame
+    and returns it (None on the first call); flush() finishes the frame still
+    in flight.  Every rank must make the same calls."""
+
+    def __init__(self, backend, rank: int, world: int, group=None, pipeline: bool = False, exchange_group=None):
         self.b, self.rank, self.world, self.group = backend, rank, world, group
+        self.pipeline = pipeline
+        self.xgroup = exchange_group if exchange_group is not None else group
+        self._pending = None
+        self._slot = 0
 
-    def render(self, view, proj, width, height, gather: bool = True):
-        """Returns the full frame on rank 0 (None elsewhere) when gather=True,
-        else this rank's band buffer."""
-        send, counts = self.b.project(view, proj, width, height)
-        recv, nrec = exchange(send, counts, self.b.xbytes, self.world, self.group)
+    def _finish(self, pend, width, height, gather):
+        recv, nrec = pend.wait()
         band = self.b.render(recv, nrec, width, height)
         if not gather:
             return band
         if self.world == 1:
             return assemble([band], width, height, 1)
         return gather_frame(band, width, height, self.world, self.rank, getattr(self.b, "owner", None), self.group)
+
+    def render(self, view, proj, width, height, gather: bool = True):
+        """Returns the full frame on rank 0 (None elsewhere) when gather=True,
+        else this rank's band buffer (pipelined: the previous frame's)."""
+        if not self.pipeline:
+            send, counts = self.b.project(view, proj, width, height)
+            return self._finish(exchange_start(send, counts, self.b.xbytes, self.world, self.group),
+                                width, height, gather)
+        send, counts = self.b.project(view, proj, width, height, slot=self._slot)
+        self._slot ^= 1
+        nxt = (exchange_start(send, counts, self.b.xbytes, self.world, self.xgroup), width, height, gather)
+        out = self._finish(*self._pending) if self._pending is not None else None
+        self._pending = nxt
+        return out
+
+    def flush(self):
+        """The frame still in flight (pipelined), or None."""
+        if self._pending is None:
+            return None
+        p, self._pending = self._pending, None
+        return self._finish(*p)
 
 
 def _all_reduce_sum(t, group):

@@ -28,7 +28,7 @@ class OracleShardBackend:
         self.shard, self.rank, self.world, self.base = shard, rank, world, index_base
         self.sh, self.mode, self.cap = sh_degree, mode, cap
 
-    def project(self, view, proj, width, height):
+    def project(self, view, proj, width, height, slot=0):
         import torch
 
         from gaussian_splat_amd.distributed import row_owner

@@ -66,6 +66,66 @@ def test_gloo_sharded_frame_bitexact(world, sh, mode, cap):
     assert same, f"sharded frame differs from single-process oracle (L-inf {linf})"
 
 
+def _pipe_worker(rank, world, port, n, w, h, q):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import torch.distributed as dist
+    from cpu_shard_backend import OracleShardBackend
+    from gaussian_splat_amd import scene as S
+    from gaussian_splat_amd.api import default_camera
+    from gaussian_splat_amd.distributed import ShardedRenderer, shard_bounds
+
+    os.environ["OMP_NUM_THREADS"] = "2"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sc = S.synthetic_scene(n, seed=23, sh_degree=0, aspect=w / h)
+        cam = default_camera(w, h)
+        views = []
+        for _ in range(3):
+            views.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
+            cam.orbit(0.4, 0.05)
+        b, e = shard_bounds(n, world, rank)
+        xg = dist.new_group(backend="gloo")  # the exchange's own communicator
+        sr = ShardedRenderer(OracleShardBackend(sc.subset(slice(b, e)), rank, world, b), rank, world,
+                             pipeline=True, exchange_group=xg)
+        outs = [sr.render(V, P, w, h) for V, P in views] + [sr.flush(), sr.flush()]
+        if rank == 0:
+            from oracle import oracle_py as O
+            ok = outs[0] is None and outs[4] is None  # one frame of latency; nothing left after the flush
+            worst = 0.0
+            for k, (V, P) in enumerate(views):
+                ref, _ = O.render(sc, V, P, w, h)
+                got = outs[k + 1].numpy()
+                ok = ok and got.shape == ref.shape and bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
+                worst = max(worst, float(np.abs(got - ref).max()) if got.shape == ref.shape else -1.0)
+            q.put((ok, worst))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_pipelined_rows_bitexact(world):
+    """Pipelined row frames (two in flight, the exchange on its own group):
+    call k returns frame k-1, flush() the last; each equals the oracle frame
+    of its own view bit for bit."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, 20000, 256, 192, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    same, linf = res
+    assert same, f"pipelined sharded frames differ from the oracle (L-inf {linf})"
+
+
 def _band_worker(rank, world, port, n, w, h, sh, mode, q):
     import sys
     from pathlib import Path
