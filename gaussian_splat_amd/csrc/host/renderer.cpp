@@ -151,17 +151,19 @@ struct gs_handle {
     int set = 0;
     bool last_pipe = false;  // the last frame ran pipelined (a switch into pipelining waits for the caller's stream)
     DevBuf alt_rec, alt_dkey, alt_keys, alt_vals, alt_tkeys, alt_tvals, alt_ranges, alt_thr, alt_rlo, alt_rhi,
-        alt_qrec;
+        alt_qrec, alt_fkeys, alt_fvals;
     // Depth cuts (gs_options.depth_split).  cutbuf, per buffer
     // set, two per-bin cut tables: a frame's front lists keep the pairs at or
     // ahead of the cuts its set's previous frame (two frames back) left in
     // one; its composite writes the quadrant records (qrec: cut positions and
     // open flags, one set each, swapped) and launch_cut_finalize turns them
-    // into the other table; then the roles swap.  cstate: the open quadrants'
-    // pixel states; the fallback lists' scan sums, pair count, sort scratch
-    // (composite stream only) and totals (per set, for gs_last_stats); kept:
-    // the front lists' pair count per set.
-    DevBuf qrec, cutbuf, cstate, fpart, fnpairs, scratch2, tot2, kept;
+    // into the other table; then the roles swap.  fkeys/fvals (per set): the
+    // front lists, sorted out of keys/vals, which keep every pair of the frame
+    // for the fallback lists (its bins with an open quadrant, behind their
+    // cuts: fbtab, fbn, sorted with scratch2; composite stream only).
+    // cstate: the open quadrants' pixel states.  kept: per set, the front
+    // lists' pairs [set] and the fallback lists' [2 + set] (gs_last_stats).
+    DevBuf qrec, cutbuf, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
     uint32_t cut_bins = 0;       // bins per table in cutbuf
     int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
     int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
@@ -187,6 +189,8 @@ struct gs_handle {
         std::swap(rlo, alt_rlo);
         std::swap(rhi, alt_rhi);
         std::swap(qrec, alt_qrec);
+        std::swap(fkeys, alt_fkeys);
+        std::swap(fvals, alt_fvals);
         set ^= 1;
     }
     int64_t index_base = 0;
@@ -196,8 +200,8 @@ struct gs_handle {
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &alt_rlo,
-                          &alt_rhi, &alt_qrec, &seg_sample, &npairs, &fetch, &qrec, &cutbuf, &cstate, &fpart,
-                          &fnpairs, &scratch2, &tot2, &kept, &ppart})
+                          &alt_rhi, &alt_qrec, &alt_fkeys, &alt_fvals, &seg_sample, &npairs, &fetch, &qrec, &cutbuf,
+                          &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -375,7 +379,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
         GS_HIP(h->seg_sample.reserve(16));
         GS_HIP(hipMemset(h->seg_sample.ptr, 0, 16));
     }
-    GS_HIP(h->npairs.reserve(4));
+    GS_HIP(h->npairs.reserve(8));  // (per buffer set: a set's depth-cut fallback reads its own)
     GS_HIP(h->fetch.reserve(32));  // per buffer set: [2 set] records fetched, [2 set + 1] open tiles (depth cuts)
     if (!h->totals_ev) GS_HIP(hipEventCreateWithFlags(&h->totals_ev, hipEventDisableTiming));
     if (h->opt.stage_timing && !h->events) {
@@ -489,13 +493,20 @@ int list_key_bits(const gs::FrameUniforms& U) { return std::max(bits_for((uint32
 // Pair capacity of the current buffer set: at least `want` (0 on failure).
 uint32_t reserve_pairs(gs_handle* h, uint64_t want) {
     const size_t p = (size_t)std::max<uint64_t>(want, 1) * 4;
+    // (depth-cut frames: the front lists in their own pair buffers)
+    const bool cut = h->cut_pending;
+    auto smallest = [&]() {
+        size_t m = std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes});
+        return cut ? std::min({m, h->fkeys.bytes, h->fvals.bytes}) : m;
+    };
     // growing frees the set's buffers: its last composite must be done
-    if (p > std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) &&
-        hipEventSynchronize(h->set_free[h->set]) != hipSuccess)
-        return 0;
+    if (p > smallest() && hipEventSynchronize(h->set_free[h->set]) != hipSuccess) return 0;
     for (DevBuf* b : {&h->keys, &h->vals, &h->tkeys, &h->tvals})
         if (b->reserve(p) != hipSuccess) return 0;
-    const size_t c = std::min({h->keys.bytes, h->vals.bytes, h->tkeys.bytes, h->tvals.bytes}) / 4;
+    if (cut)
+        for (DevBuf* b : {&h->fkeys, &h->fvals})
+            if (b->reserve(p) != hipSuccess) return 0;
+    const size_t c = smallest() / 4;
     const uint32_t cap = (uint32_t)std::min<size_t>(c, UINT32_MAX - 1);
     if (h->sort_scratch.reserve(gs::radix_sort_scratch_words(cap) * 4) != hipSuccess) return 0;
     return cap;
@@ -577,10 +588,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     }
     uint32_t cap = lp.cap;
     gs::PassCounts pc = lp.pc;
-    const bool cut_frame = h->cut_pending && h->cut_in && !order && own.dev.owner == nullptr && carry_dkey;
+    uint32_t* const np = h->npairs.as<uint32_t>() + h->set;  // P on the device (this set's)
+    const bool cut_frame = h->cut_pending && h->cut_in && own.dev.owner == nullptr && carry_dkey;
     gs::SortFilter flt;  // front lists: the pairs at or ahead of their bin's cut
     if (cut_frame) {
-        GS_HIP(h->kept.reserve(8));
+        GS_HIP(h->kept.reserve(16));
         flt.cut = h->cut_in;
         flt.bmask = (1u << bits) - 1u;
         flt.dshift = bits;
@@ -590,13 +602,13 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
                                               h->partials.as<uint64_t>(), h->dev_total,
-                                              h->seg_sample.as<uint32_t>() + 2 * h->set, h->npairs.as<uint32_t>(), cap,
+                                              h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
                                               st, h->totals_ev));
         h->ppart_dirty = false;
     } else {
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                             h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set,
-                                            h->ranges.as<uint2>(), T, h->npairs.as<uint32_t>(), cap, pc.C,
+                                            h->ranges.as<uint2>(), T, np, cap, pc.C,
                                             pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, h->totals_ev));
     }
     if (timed) mark(h, 3, st);
@@ -608,21 +620,27 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                                 h->npairs.as<uint32_t>(), st, h->offsets.as<uint32_t>(), pc);
+                                                 np, st, h->offsets.as<uint32_t>(), pc);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
-        return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
-                                     h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap,
-                                     bits, h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>(),
-                                     h->npairs.as<uint32_t>(), pc.C != nullptr, flt);
+        // (depth-cut frames: sorted into fkeys/fvals, so keys/vals keep every
+        // pair for the fallback lists)
+        return gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
+                                     cut_frame ? h->fkeys.as<uint32_t>() : h->keys.as<uint32_t>(),
+                                     cut_frame ? h->fvals.as<uint32_t>() : h->vals.as<uint32_t>(),
+                                     h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap, bits,
+                                     h->sort_scratch.as<uint32_t>(), &in_tmp, st, h->ranges.as<uint2>(), np,
+                                     pc.C != nullptr, flt);
     };
     auto lists_done = [&]() -> gs_status {
-        uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
-        uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
+        uint32_t* fk = cut_frame ? h->fkeys.as<uint32_t>() : h->keys.as<uint32_t>();
+        uint32_t* fv = cut_frame ? h->fvals.as<uint32_t>() : h->vals.as<uint32_t>();
+        uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : fk;
+        uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : fv;
         h->last_keys = sk;
         h->last_vals = sv;
-        h->last_tmp_keys = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
-        h->last_tmp_vals = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+        h->last_tmp_keys = in_tmp ? fk : h->tkeys.as<uint32_t>();
+        h->last_tmp_vals = in_tmp ? fv : h->tvals.as<uint32_t>();
         h->last_key_bits = bits;
         h->pair_cap = cap;
         if (timed) mark(h, 5, st);
@@ -647,7 +665,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         GS_HIP(hipStreamSynchronize(st));
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
-        GS_HIP(hipMemcpy(h->npairs.ptr, &p32, 4, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
         pc = cut_frame ? gs::PassCounts{} : pass_counts(h, m, order == nullptr, plan, cap, P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         if (tail) {  // (the no-op frame's composite counted into these)
@@ -672,43 +690,51 @@ hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
 }
 
 // Depth-cut frames, after the front lists' composite on sc:
-// the fallback lists of the tiles it left open (their bins' pairs behind the
-// cut, dkey > cut[bin]) are emitted, sorted by bin, put in depth order per
-// bin and composited from the saved states.  Nothing waits for the host:
-// every kernel here returns at once when the open tile count is zero, the
-// usual case.  The front lists' buffers are free by then (same stream).
-gs_status cut_fallback(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, hipStream_t sc) {
-    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y), m = (uint32_t)h->n;
+// the next cuts of this set (from the quadrant records), and the fallback
+// lists of the quadrants it left open: the frame's pairs (keys/vals, every
+// pair, still there) of the bins with an open quadrant that lie behind the
+// cut, picked by the first pass of their own bin sort (SortFilter `behind`,
+// against the table cut_finalize writes), put in depth order per bin and
+// composited from the saved states.  Nothing waits for the host: with no
+// quadrant open, cut_finalize leaves a pair count of 0 and every kernel here
+// returns at once (the usual case).  The front lists' buffers are free by
+// then (same stream).
+gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, const uint32_t* dkey,
+                   hipStream_t sc) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    gs::CutFallback fb;
+    if (h->cut_in) {
+        GS_HIP(reserve_after(h->fbtab, (size_t)T * 4, sc));
+        GS_HIP(reserve_after(h->fbn, 4, sc));
+        fb.cut_in = h->cut_in;
+        fb.open = open_counter(h);
+        fb.npairs = h->npairs.as<uint32_t>() + h->set;
+        fb.table = h->fbtab.as<uint32_t>();
+        fb.n = h->fbn.as<uint32_t>();
+        fb.kept = h->kept.as<uint32_t>() + 2 + h->set;
+        fb.ranges = h->ranges.as<uint2>();
+    }
+    GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, cut_margin(), sc, fb));
+    if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
     const int bits = h->last_key_bits;
     const uint32_t cap = h->pair_cap;
-    const uint32_t nb = (m + gs::kScanItems - 1) / gs::kScanItems;
-    GS_HIP(reserve_after(h->fpart, ((size_t)nb + 1) * 16, sc));
-    GS_HIP(reserve_after(h->fnpairs, 4, sc));
     GS_HIP(reserve_after(h->scratch2, gs::radix_sort_scratch_words(cap) * 4, sc));
-    GS_HIP(h->tot2.reserve(2 * 64));
-    gs::CutSel fs;
-    fs.mode = 2;
-    fs.dkey = h->dkey.as<uint32_t>();
-    fs.cut = h->cut_in;
-    fs.qrec = h->qrec.as<const uint32_t>();  // (any of a bin's 16 quadrants open)
-    fs.guard = open_counter(h);
-    uint64_t* tot = h->tot2.as<uint64_t>() + 8 * h->set;  // (read by gs_last_stats)
-    uint32_t* np = h->fnpairs.as<uint32_t>();
-    GS_HIP(gs::launch_tile_count_totals(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), m, gs::RowOwnership{nullptr, 0},
-                                        U.cell_mask != 0, h->fpart.as<uint64_t>(), tot, nullptr, h->ranges.as<uint2>(),
-                                        T, np, cap, nullptr, 0, sc, nullptr, fs, (uint32_t)U.tiles_x));
-    GS_HIP(gs::launch_scan_duplicate(nullptr, h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), h->fpart.as<uint64_t>(), m,
-                                     (uint32_t)U.tiles_x, gs::RowOwnership{nullptr, 0}, U.cell_mask != 0,
-                                     h->dkey.as<uint32_t>(), bits, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), np,
-                                     sc, nullptr, gs::PassCounts{}, fs));
+    gs::SortFilter flt;
+    flt.cut = fb.table;
+    flt.bmask = (1u << bits) - 1u;
+    flt.dshift = bits;
+    flt.kept = fb.kept;
+    flt.behind = 1;
     bool in_tmp = false;
-    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), h->keys.as<uint32_t>(),
-                                 h->vals.as<uint32_t>(), h->tkeys.as<uint32_t>(), h->tvals.as<uint32_t>(), cap, bits,
-                                 h->scratch2.as<uint32_t>(), &in_tmp, sc, h->ranges.as<uint2>(), np, false));
-    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : h->keys.as<uint32_t>();
-    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : h->vals.as<uint32_t>();
-    uint32_t* tk = in_tmp ? h->keys.as<uint32_t>() : h->tkeys.as<uint32_t>();
-    uint32_t* tv = in_tmp ? h->vals.as<uint32_t>() : h->tvals.as<uint32_t>();
+    uint32_t* fk = h->fkeys.as<uint32_t>();
+    uint32_t* fv = h->fvals.as<uint32_t>();
+    GS_HIP(gs::launch_radix_sort(h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), fk, fv, h->tkeys.as<uint32_t>(),
+                                 h->tvals.as<uint32_t>(), cap, bits, h->scratch2.as<uint32_t>(), &in_tmp, sc,
+                                 h->ranges.as<uint2>(), fb.n, false, flt));
+    uint32_t* sk = in_tmp ? h->tkeys.as<uint32_t>() : fk;
+    uint32_t* sv = in_tmp ? h->tvals.as<uint32_t>() : fv;
+    uint32_t* tk = in_tmp ? fk : h->tkeys.as<uint32_t>();
+    uint32_t* tv = in_tmp ? fv : h->tvals.as<uint32_t>();
     GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), T, sk, sv, tk, tv, bits, nullptr, sc, nullptr,
                                      open_counter(h)));
     ca.vals = sv;
@@ -764,8 +790,8 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* vals = nullptr;
     uint64_t P = 0;
     const bool mlab = h->opt.mode == GS_MODE_MLAB;
-    // depth cuts: decided with the fused scan (render_frame); only a bin-first
-    // frame of local splats can carry them
+    // depth cuts: decided before the preprocess (render_frame); only a frame
+    // of local splats can carry them
     const bool cut_ok = h->cut_pending && !slab_t && !compact;
     h->cut_frame = false;
     if (mlab && (ca.cap > 0 || slab_t))
@@ -837,14 +863,9 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
                 h->slab_ca = c;
                 h->slab_lists = true;
             }
-            // the next cuts of this set, then the fallback lists, only if some
-            // list was cut (null cuts: every pair is in the front lists, no
-            // quadrant can be left open)
-            if (cutf)
-                GS_HIP(gs::launch_cut_finalize(c.qrec, sv, dkey, h->cut_out, (uint32_t)(U.tiles_x * U.tiles_y),
-                                               cut_margin(), sc));
-            if (cutf && h->cut_in) {
-                gs_status fs_ = cut_fallback(h, U, c, sc);
+            // the next cuts of this set, then the fallback lists
+            if (cutf) {
+                gs_status fs_ = cut_tail(h, U, c, dkey, sc);
                 if (fs_ != GS_OK) return fs_;
             }
             mark(h, 7, sc);
@@ -883,6 +904,40 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* slo = in_tmp ? vtmp[1] : vout[1];
     const uint32_t* shi = in_tmp ? vtmp[2] : vout[2];
     mark(h, 2, st);
+    // Depth cuts in depth order: the pair keys carry the sorted
+    // depth keys above the bin ids, so the bin sort's first pass filters at
+    // the cuts exactly as in bin-first frames; the composite, the next cuts
+    // and the fallback lists are queued behind the lists (ListTail).
+    const bool cutf = cut_ok && (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) && ca.cap == 0 &&
+                      list_key_bits(U) + gs::kDepthBits <= 32;
+    h->cut_frame = cutf;
+    if (cutf) {
+        const uint32_t* sdk = in_tmp ? h->dtk.as<uint32_t>() : h->dsk.as<uint32_t>();  // (dkeys in depth order)
+        ca.fetched = fetch_counter(h);
+        ca.pass = 1;
+        ca.qrec = h->qrec.as<uint32_t>();
+        ca.open_q_count = open_counter(h);
+        ca.state = h->cstate.as<float4>();
+        ca.cut_in = h->cut_in;
+        const ListTail tail = [&](const uint32_t* sv) -> gs_status {
+            gs::CompositeArgs c = ca;
+            c.vals = sv;
+            c.ranges = h->ranges.as<uint2>();
+            mark(h, 6, st);
+            GS_HIP(handoff());
+            GS_HIP(gs::launch_composite(c, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
+            gs_status fs_ = cut_tail(h, U, c, dkey, sc);
+            if (fs_ != GS_OK) return fs_;
+            mark(h, 7, sc);
+            return GS_OK;
+        };
+        gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P, sdk, &tail);
+        if (s != GS_OK) return s;
+        h->cut_phase[h->set] ^= 1;  // this frame's cuts are read by its set's next frame
+        h->cut_valid[h->set] = true;
+        h->stats.pairs = (int64_t)P;
+        return GS_OK;
+    }
     // 2. bin lists in depth order
     gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P);
     if (s != GS_OK) return s;
@@ -1274,7 +1329,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     if (!band && h->world == 1 && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
         const bool bf = bin_first_order(h, U, (uint32_t)h->n);
         h->order_pick = bf ? 1 : 0;
-        cut_frame = bf && cut_on;
+        cut_frame = cut_on && list_key_bits(U) + gs::kDepthBits <= 32;  // (the depth key rides above the bin id)
         if (cut_frame) {
             // two tables per set (cutbuf), the per-tile open flags of the set,
             // the open tiles' pixel states (composite stream)
@@ -1374,19 +1429,17 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
                 const int64_t P = s.pairs, P1 = (int64_t)k1;
                 s.pairs_sorted = P1;
                 s.bytes_sort = P * 12 + P1 * 8 + P1 * 20 * (int64_t)(s.sort_passes - 1);
-                s.bytes_depth_sort = P1 * 12;
+                if (h->bin_first_frame) s.bytes_depth_sort = P1 * 12;  // (depth-first: the global depth sort, unchanged)
             }
             unsigned long long open = 0;
-            uint64_t P2 = 0;
+            uint32_t P2 = 0;
             GS_HIP(hipMemcpy(&open, h->fetch.as<unsigned long long>() + 2 * h->stats_set + 1, 8,
                              hipMemcpyDeviceToHost));
-            if (open) GS_HIP(hipMemcpy(&P2, h->tot2.as<uint64_t>() + 8 * h->stats_set, 8, hipMemcpyDeviceToHost));
+            if (open) GS_HIP(hipMemcpy(&P2, h->kept.as<uint32_t>() + 2 + h->stats_set, 4, hipMemcpyDeviceToHost));
             s.open_tiles = (int64_t)open;
             s.pairs_sorted += (int64_t)P2;
-            if (open) {
-                s.bytes_scan += s.splats * 12;
-                s.bytes_duplicate += s.splats * 12 + (int64_t)P2 * 8;
-                s.bytes_sort += (int64_t)P2 * 20 * (int64_t)s.sort_passes;
+            if (open) {  // the fallback sort's first pass reads every pair again
+                s.bytes_sort += s.pairs * 12 + (int64_t)P2 * 8 + (int64_t)P2 * 20 * (int64_t)(s.sort_passes - 1);
                 s.bytes_depth_sort += (int64_t)P2 * 12;
                 s.bytes_composite += (int64_t)open * 64 * 32;  // (8x8 quadrants)
             }

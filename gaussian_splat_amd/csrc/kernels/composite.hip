@@ -509,26 +509,39 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
 __global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __restrict__ qrec,
                                                            const uint32_t* __restrict__ vals,
                                                            const uint32_t* __restrict__ dkey, uint32_t* __restrict__ cut,
-                                                           uint32_t nbins, uint32_t margin) {
+                                                           uint32_t nbins, uint32_t margin, const CutFallback fb) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    const bool any_open = fb.cut_in && *fb.open != 0ull;
+    if (fb.cut_in && b == 0) {
+        *fb.n = any_open ? *fb.npairs : 0u;
+        *fb.kept = 0u;
+    }
     if (b >= nbins) return;
-    uint32_t c = 0u;
-    const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);  // (the bin's 16 positions)
-    uint32_t p = 0u;
+    const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);  // (the bin's 16 positions, 16 flags)
+    uint32_t p = 0u, open = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint4 v = q[i];
         p = max(p, max(max(v.x, v.y), max(v.z, v.w)));
+        const uint4 f = q[4 + i];
+        open |= f.x | f.y | f.z | f.w;
     }
+    uint32_t c = 0u;
     if (p == 0xFFFFFFFFu) c = 0xFFFFu;
     else if (p > 0u) c = min(dkey[vals[p - 1u]] + margin, 0xFFFFu);
     cut[b] = c;
+    if (fb.cut_in) {
+        fb.table[b] = open ? fb.cut_in[b] : 0xFFFFFFFFu;
+        if (any_open) fb.ranges[b] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
 }
 
 hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
-                               uint32_t nbins, uint32_t margin, hipStream_t st) {
+                               uint32_t nbins, uint32_t margin, hipStream_t st, const CutFallback& fb) {
     if (nbins == 0) return hipSuccess;
-    cut_finalize_kernel<<<(nbins + 255) / 256, 256, 0, st>>>(qrec, vals, dkey, cut_out, nbins, margin);
+    if (fb.cut_in && (!fb.open || !fb.npairs || !fb.table || !fb.n || !fb.kept || !fb.ranges))
+        return hipErrorInvalidValue;
+    cut_finalize_kernel<<<(nbins + 255) / 256, 256, 0, st>>>(qrec, vals, dkey, cut_out, nbins, margin, fb);
     return hipGetLastError();
 }
 

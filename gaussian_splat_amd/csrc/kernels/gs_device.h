@@ -200,46 +200,11 @@ __device__ __forceinline__ uint32_t rect_tile_count(uint32_t lo, uint32_t hi, co
 // frame's bin lists (the front lists) hold the pairs whose depth key lies at
 // or ahead of their bin's cut in S1 order, dkey <= cut[bin]: every pair is
 // emitted, and the bin sort's first pass drops the others (SortFilter).  The
-// fallback for the tiles those lists leave open emits the other pairs of the
-// bins with an open tile: CutSel mode 2, dkey > cut[bin] and open[bin] != 0
-// (the 16 quadrant flags of the bin's four tiles); every fallback kernel
-// returns at once when *guard (the frame's open quadrant count) is 0.  S1
-// composites ascending dkey, so each bin's front list precedes all its other
-// pairs.  mode 0: every pair.
+// fallback lists for the quadrants those lists leave open are the same
+// frame's pairs of the bins with an open quadrant behind the cut, picked by
+// the first pass of their own bin sort.  S1 composites ascending dkey, so each
+// bin's front list precedes all its other pairs.
 constexpr uint32_t kQrecWords = 32;  // per bin: 16 quadrant cut positions, 16 open flags (CompositeArgs)
-struct CutSel {
-    int mode = 0;
-    const uint32_t* dkey = nullptr;  // per item (index order)
-    const uint32_t* cut = nullptr;   // per bin
-    const uint32_t* qrec = nullptr;  // per bin kQrecWords: open flags in words [16, 32)
-    const unsigned long long* guard = nullptr;
-};
-__device__ __forceinline__ bool cut_keep(const CutSel& s, uint32_t dk, uint32_t bin) {
-    if (dk <= s.cut[bin]) return false;
-    const uint4* f = reinterpret_cast<const uint4*>(s.qrec + (size_t)bin * kQrecWords + 16u);
-    uint32_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint4 o = f[i];
-        any |= o.x | o.y | o.z | o.w;
-    }
-    return any != 0u;
-}
-
-// (splat, bin) pairs of the rect in owned bin rows, minus the excluded bins,
-// for which keep(bin) holds.
-template <typename Keep>
-__device__ __forceinline__ uint32_t rect_count_if(const BinRect& r, uint32_t tiles_x, const RowOwnership& own,
-                                                  Keep&& keep) {
-    if (r.empty) return 0u;
-    uint32_t n = 0;
-    for (uint32_t by = r.by0; by <= r.by1; ++by) {
-        if (!owns_bin_row(by, own)) continue;
-        for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx)
-            if (!bin_excluded(r, by, bx) && keep(by * tiles_x + bx)) ++n;
-    }
-    return n;
-}
 
 // The (bin, splat) pairs of one splat, from pair offset `off` on: one per bin
 // of its rect in an owned bin row, minus the bins its ellipse provably misses

@@ -51,13 +51,10 @@ constexpr int kScanItems = 4096;  // per block
 // host re-queues them with larger buffers).  Then launch_scan_duplicate.
 // zero[0..nzero) is cleared on the way (the first sort pass's digit counts,
 // PassCounts).
-// sel (mode 0 or 2): which pairs are counted (CutSel); mode 2
-// also makes both kernels return at once while *sel.guard == 0 (then P = 0).
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr,
-                                    const CutSel& sel = CutSel{}, uint32_t tiles_x = 0);
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr);
 // (done: recorded by the totals kernel's own dispatch packet, not a separate
 // marker packet, which would leave a ~6 us bubble in the stream.)
 // The scan half alone, after a preprocess with PreFuse: the block sums in
@@ -79,19 +76,17 @@ constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts i
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
 // when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
 // for each bin of its rect whose row this rank owns, minus the excluded bins,
-// at its pair offset.  dkey (index order only, may be null): key = dkey[j] <<
-// bin_bits | bin, the depth key riding above the bin id for the per-bin sort.
+// at its pair offset.  dkey (may be null): key = dkey[j] << bin_bits | bin,
+// the depth key riding above the bin id (index order: for the per-bin sort;
+// depth order, dkey in that order: for a depth-cut frame's sort filter).
 // Index order runs one fused kernel; depth order (order set) a down-sweep
 // into offsets (n words of scratch) and a one-splat-per-lane duplicate.
 // Nothing is written when *npairs == 0 (see launch_tile_count_totals).
-// sel (index order only): which pairs are emitted (CutSel mode 0 or 2; the
-// counts must be the ones the scan was given).
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
-                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
-                                 const CutSel& sel = CutSel{});
+                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{});
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -142,17 +137,21 @@ uint32_t radix_sort_tile_items();
 // n_dev (optional): the item count is read on the device from *n_dev (<= n;
 // n sizes the grids and the scratch), so the sort can be queued before the
 // host knows it.
-// Filter (the bin sort of a depth-cut frame): only items whose
+// Filter (the bin sorts of a depth-cut frame): only items whose
 // depth key (key >> dshift) lies at or ahead of their bin's cut (<=
-// cut[key & bmask]) are counted and sorted; the first pass drops the others
-// and stores the number kept in *kept (the later passes read it, as n_dev);
-// the result holds the kept items.
+// cut[key & bmask]; behind it, > cut[...], with `behind`: the fallback lists)
+// are counted and sorted; the first pass drops the others and stores the
+// number kept in *kept (the later passes read it, as n_dev); the result holds
+// the kept items.
 struct SortFilter {
     const uint32_t* cut = nullptr;  // null: every item
     uint32_t bmask = 0;
     int dshift = 0;
     uint32_t* kept = nullptr;
-    __device__ __forceinline__ bool keep(uint32_t key) const { return (key >> dshift) <= cut[key & bmask]; }
+    uint32_t behind = 0;
+    __device__ __forceinline__ bool keep(uint32_t key) const {
+        return ((key >> dshift) <= cut[key & bmask]) != (behind != 0u);
+    }
 };
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,
                              uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t n, int bits, uint32_t* scratch,
@@ -224,8 +223,23 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
 // cut positions (CompositeArgs::qrec): ~0 -> 0xFFFF (every pair), 0 -> 0,
 // else the depth key of the list record before it plus `margin`, at most
 // 0xFFFF.  vals and dkey: the composited lists and depth keys.
+// With fb.cut_in (the frame's lists were cut), the same kernel prepares the
+// fallback lists' sort: fb.table[bin] = cut_in[bin] for a bin with an open
+// quadrant (its pairs behind the cut are sorted again), else ~0 (none);
+// *fb.n = *fb.npairs when a quadrant is open, else 0, and *fb.kept = 0 (so
+// every fallback kernel returns at once when none is); the bin ranges are
+// cleared for the fallback sort when one is open.
+struct CutFallback {
+    const uint32_t* cut_in = nullptr;  // null: no fallback (the lists were whole)
+    const unsigned long long* open = nullptr;
+    const uint32_t* npairs = nullptr;
+    uint32_t* table = nullptr;
+    uint32_t* n = nullptr;
+    uint32_t* kept = nullptr;
+    uint2* ranges = nullptr;
+};
 hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
-                               uint32_t nbins, uint32_t margin, hipStream_t st);
+                               uint32_t nbins, uint32_t margin, hipStream_t st, const CutFallback& fb);
 // Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).

@@ -25,52 +25,32 @@ struct CountSrc {
     const uint32_t* lo;
     const uint32_t* hi;
     RowOwnership own;
-    bool masked;       // rect words carry the bin-exclusion mask
-    CutSel sel;        // which pairs (depth cuts, gs_device.h; mode 0: every pair)
-    uint32_t tiles_x;  // (bin ids of the CutSel tables)
+    bool masked;  // rect words carry the bin-exclusion mask
 };
 
-// Pairs of an item's rect under the selection (dk: its depth key).
-template <int MODE>
-__device__ __forceinline__ uint32_t item_pairs(const CountSrc& src, uint32_t lo, uint32_t hi, uint32_t dk) {
-    if constexpr (MODE == 0) {
-        return rect_tile_count(lo, hi, src.own, src.masked);
-    } else {
-        const CutSel& sel = src.sel;
-        return rect_count_if(bin_rect(lo, hi, src.masked), src.tiles_x, src.own,
-                             [&](uint32_t bin) { return cut_keep(sel, dk, bin); });
-    }
-}
-
 // Per block: pair count -> partials[b], contributing splats -> partials[nb + b].
-// MODE 2 (the depth-cut fallback): nothing while *guard == 0.
-template <int MODE>
 __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t n,
                                                           uint64_t* __restrict__ partials,
                                                           uint2* __restrict__ fill, uint32_t nfill,
                                                           uint32_t* __restrict__ zero, uint32_t nzero) {
-    if constexpr (MODE == 2)
-        if (*src.sel.guard == 0ull) return;
     __shared__ uint2 tmp[4];
     const uint32_t base = blockIdx.x * kScanItems;
     // every rect loaded before the first use (clamped, branch-free): one
     // memory round trip instead of one per item (a conditional load is waited
     // for inside its branch)
-    uint32_t lo[kScanIpt], hi[kScanIpt], dk[kScanIpt];
-    const uint32_t* dsrc = MODE ? src.sel.dkey : src.lo;
+    uint32_t lo[kScanIpt], hi[kScanIpt];
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const uint32_t i = min(base + k * 256 + threadIdx.x, n - 1u);
         lo[k] = src.lo[i];
         hi[k] = src.hi[i];
-        dk[k] = dsrc[i];
     }
     // 32-bit sums: a block's pairs are at most 4096 splats x 16384 bins (4096^2 frames)
     uint32_t s = 0, vis = 0;
 #pragma unroll
     for (int k = 0; k < kScanIpt; ++k) {
         const bool in = base + k * 256 + threadIdx.x < n;
-        const uint32_t c = in ? item_pairs<MODE>(src, lo[k], hi[k], dk[k]) : 0u;
+        const uint32_t c = in ? rect_tile_count(lo[k], hi[k], src.own, src.masked) : 0u;
         s += c;
         vis += c > 0;
     }
@@ -123,20 +103,11 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 
 // src (may be null): the block sums come from there instead (the fused
 // preprocess's, PreFuse: 2 x nb words) and are cleared after reading.
-// guard (may be null): while *guard == 0 the scan only reports P = 0.
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
                                                                      uint32_t* __restrict__ npairs, uint64_t cap,
-                                                                     unsigned long long* __restrict__ src,
-                                                                     const unsigned long long* __restrict__ guard) {
-    if (guard && *guard == 0ull) {
-        if (threadIdx.x == 0) {
-            total[0] = total[1] = 0u;
-            *npairs = 0u;
-        }
-        return;
-    }
+                                                                     unsigned long long* __restrict__ src) {
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
@@ -212,9 +183,6 @@ __device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_
     return base + inc - v;
 }
 
-// MODE (CutSel): 0 every pair; 2 the fallback lists of a depth-cut frame
-// (nothing while *npairs == 0, which its guarded scan leaves).
-template <int MODE>
 __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
                                                                      const uint64_t* __restrict__ partials,
                                                                      const uint32_t* __restrict__ order,
@@ -247,7 +215,6 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     }
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
-    const CutSel& sel = src.sel;
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid;
@@ -255,7 +222,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        st[pad32(i)] = item_pairs<MODE>(src, rlo[k], rhi[k], dk[k]);
+        st[pad32(i)] = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
     }
     block_lds_sync();
     uint32_t v[kDupIpt];
@@ -288,8 +255,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         const uint32_t off = st[pad32(i)];
         const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t val = order ? ord[k] : j;
-        const uint32_t d_k = dk[k];
-        auto keep = [&](uint32_t bin) { return MODE == 0 || cut_keep(sel, d_k, bin); };
+        auto keep = [](uint32_t) { return true; };
         if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
             emit_bin_pairs_if(r, tiles_x, src.own, key_hi, val, off, keys, vals, keep, [&](uint32_t g, uint32_t bin) {
@@ -361,15 +327,19 @@ __global__ __launch_bounds__(256) void scan_down_kernel(CountSrc src, uint32_t n
     }
 }
 
+// dks (optional, depth-cut frames): the items' depth keys in the same order,
+// carried above the bin id (key = dkey << bin_bits | bin) for the first sort
+// pass's cut filter.
 __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n, const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ offsets, uint32_t tiles_x,
                                                         uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                        const uint32_t* __restrict__ npairs) {
+                                                        const uint32_t* __restrict__ npairs,
+                                                        const uint32_t* __restrict__ dks, int bin_bits) {
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
     if (j >= n || *npairs == 0u) return;
     const BinRect r = bin_rect(src.lo[j], src.hi[j], src.masked);
     if (r.empty) return;  // culled
-    emit_bin_pairs(r, tiles_x, src.own, 0u, order ? order[j] : j, offsets[j], keys, vals);
+    emit_bin_pairs(r, tiles_x, src.own, dks ? dks[j] << bin_bits : 0u, order ? order[j] : j, offsets[j], keys, vals);
 }
 
 // a / b for the small quotients of the emission (a < 2^32, b < 2^16): float
@@ -406,7 +376,8 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
                                                              const uint32_t* __restrict__ order,
                                                              const uint32_t* __restrict__ offsets, uint32_t tiles_x,
                                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                             const uint32_t* __restrict__ npairs) {
+                                                             const uint32_t* __restrict__ npairs,
+                                                             const uint32_t* __restrict__ dks, int bin_bits) {
     __shared__ uint32_t mk[4][64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t w0 = blockIdx.x * 256u + wave * 64u;
@@ -415,6 +386,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     uint32_t lo = src.lo[jc], hi = src.hi[jc];
     const uint32_t off = offsets[jc];
     const uint32_t val = order ? order[jc] : jc;
+    const uint32_t khi = dks ? dks[jc] << bin_bits : 0u;  // (depth-cut frames: the depth key above the bin id)
     if (j >= n) {
         lo = kEmptyRectLo;
         hi = 0u;
@@ -449,6 +421,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
         const uint32_t o_pa = (uint32_t)__shfl((int)pa, ol, 64);
         const uint32_t o_pb = (uint32_t)__shfl((int)pb, ol, 64);
         const uint32_t o_val = (uint32_t)__shfl((int)val, ol, 64);
+        const uint32_t o_khi = dks ? (uint32_t)__shfl((int)khi, ol, 64) : 0u;
         const uint32_t q = q0 + lane;
         if (q < T) {
             const uint32_t li = q - o_start, oinc = o_pb >> 16, ocols = o_pb & 0xFFFFu;
@@ -461,7 +434,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
                 dy = udiv_est(li, ocols);
                 dx = li - dy * ocols;
             }
-            keys[off0 + q] = ((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx;
+            keys[off0 + q] = o_khi | (((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx);
             vals[off0 + q] = o_val;
         }
     }
@@ -470,11 +443,8 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done,
-                                    const CutSel& sel, uint32_t tiles_x) {
-    if (sel.mode != 0 && (sel.mode != 2 || !sel.dkey || !sel.cut || !tiles_x || !sel.qrec || !sel.guard))
-        return hipErrorInvalidValue;
-    const CountSrc src{rect_lo, rect_hi, own, masked, sel, tiles_x};
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done) {
+    const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
         if (nranges) {
@@ -485,13 +455,11 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
             const hipError_t e = hipMemsetAsync(zero, 0, (size_t)nzero * 4, st);
             if (e != hipSuccess) return e;
         }
-    } else if (sel.mode == 2) {
-        scan_reduce_kernel<2><<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     } else {
-        scan_reduce_kernel<0><<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
+        scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, nullptr, sel.mode == 2 ? sel.guard : nullptr);
+                          total, seg_sample, npairs, cap, nullptr);
     return hipGetLastError();
 }
 
@@ -500,41 +468,34 @@ hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uin
                                       hipEvent_t done) {
     if (!part) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, part, nullptr);
+                          total, seg_sample, npairs, cap, part);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
-                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
-                                 const CutSel& sel) {
+                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
-    if (dkey && (order || bin_bits + kDepthBits > 32)) return hipErrorInvalidValue;
-    if (sel.mode && (sel.mode != 2 || order || !dkey || sel.dkey != dkey || !sel.cut || !sel.qrec))
-        return hipErrorInvalidValue;
-    const CountSrc src{rect_lo, rect_hi, own, masked, sel, tiles_x};
+    // (order: dkey holds the items' depth keys in that order)
+    if (dkey && bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
+    const CountSrc src{rect_lo, rect_hi, own, masked};
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
 #ifndef GS_AB_DUP_LANE
         if (!own.owner)
-            duplicate_coop_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
+            duplicate_coop_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs,
+                                                                   dkey, bin_bits);
         else
 #endif
-            duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs);
+            duplicate_kernel<<<(n + 255) / 256, 256, 0, st>>>(src, n, order, offsets, tiles_x, keys, vals, npairs, dkey,
+                                                              bin_bits);
         return hipGetLastError();
     }
-    switch (sel.mode) {
-    case 2:
-        scan_duplicate_kernel<2><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
-                                                             vals, npairs, pc);
-        break;
-    default:
-        scan_duplicate_kernel<0><<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys,
-                                                             vals, npairs, pc);
-    }
+    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
+                                                      npairs, pc);
     return hipGetLastError();
 }
 

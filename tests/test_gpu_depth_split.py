@@ -1,6 +1,6 @@
 """Depth-cut frames (gs_options.depth_split = 1).
 
-A bin-first frame's lists hold only the pairs whose depth key lies at or
+A frame's lists (bin-first or depth-first binning) hold only the pairs whose depth key lies at or
 ahead of their bin's cut (S1 order, tile.metal:239-249), the key at which
 the bin's tiles finished in the set's previous frame, plus a margin.  A tile
 those lists leave open keeps its per-pixel state and finishes with the rest
@@ -35,11 +35,11 @@ def _scene(n, seed, sh, aspect, scale=1.0):
     return sc
 
 
-def _pair(sc, **kw):
+def _pair(sc, binning="bin_first", **kw):
     from gaussian_splat_amd import InstancedSplatRenderer, Options
     out = []
     for cut in (True, False):
-        r = InstancedSplatRenderer(sc, Options(binning="bin_first", crop=False, depth_split=cut, **kw))
+        r = InstancedSplatRenderer(sc, Options(binning=binning, crop=False, depth_split=cut, **kw))
         r.initialize(0)
         out.append(r)
     return out
@@ -65,20 +65,26 @@ def _path(w, h, kind, n):
     return views
 
 
-@pytest.mark.parametrize("n,w,h,mode,sh,scale,path", [
-    (300000, 640, 360, "tile", 0, 1.0, "still"),
-    (300000, 640, 360, "tile", 0, 1.0, "orbit"),
-    (300000, 640, 360, "live50", 0, 1.0, "jump"),
-    (120000, 960, 540, "tile", 3, 1.5, "jump"),
-    (8000, 640, 360, "tile", 0, 0.5, "orbit"),      # sparse: nothing saturates, no list is cut
-    (40000, 17, 9, "tile", 0, 1.0, "jump"),         # ragged single-bin frame
-    (5000, 1, 1, "live50", 0, 1.0, "orbit"),
-    (200000, 1920, 1080, "tile", 0, 3.0, "jump"),   # large splats, long lists (> 8192 per bin)
+@pytest.mark.parametrize("n,w,h,mode,sh,scale,path,binning", [
+    (300000, 640, 360, "tile", 0, 1.0, "still", "bin_first"),
+    (300000, 640, 360, "tile", 0, 1.0, "orbit", "bin_first"),
+    (300000, 640, 360, "live50", 0, 1.0, "jump", "bin_first"),
+    (120000, 960, 540, "tile", 3, 1.5, "jump", "bin_first"),
+    (8000, 640, 360, "tile", 0, 0.5, "orbit", "bin_first"),      # sparse: nothing saturates, no list is cut
+    (40000, 17, 9, "tile", 0, 1.0, "jump", "bin_first"),         # ragged single-bin frame
+    (5000, 1, 1, "live50", 0, 1.0, "orbit", "bin_first"),
+    (200000, 1920, 1080, "tile", 0, 3.0, "jump", "bin_first"),   # large splats, long lists (> 8192 per bin)
+    # depth-first binning (4K and 50M frames): the pair keys carry the sorted depth keys
+    (300000, 640, 360, "tile", 0, 1.0, "orbit", "depth_first"),
+    (300000, 640, 360, "live50", 0, 1.0, "jump", "depth_first"),
+    (120000, 960, 540, "tile", 3, 1.5, "jump", "depth_first"),
+    (40000, 17, 9, "tile", 0, 1.0, "jump", "depth_first"),
+    (200000, 1920, 1080, "tile", 0, 3.0, "jump", "depth_first"),
 ])
-def test_depth_cuts_bitexact(built, n, w, h, mode, sh, scale, path):
+def test_depth_cuts_bitexact(built, n, w, h, mode, sh, scale, path, binning):
     from oracle import oracle_py as O
     sc = _scene(n, 131 + n % 7, sh, w / h, scale)
-    cut, whole = _pair(sc, mode=mode, sh_degree=sh)
+    cut, whole = _pair(sc, binning=binning, mode=mode, sh_degree=sh)
     opened = 0
     for k, (V, P) in enumerate(_path(w, h, path, 6)):
         a = cut.render_host(V, P, w, h)
@@ -86,23 +92,25 @@ def test_depth_cuts_bitexact(built, n, w, h, mode, sh, scale, path):
         assert _bits(a, b) == 0, k
         st, so = cut.last_stats(), whole.last_stats()
         assert st["two_slab"] == 1 and so["two_slab"] == 0
-        # (a large rect's pairs behind the cut sit in both lists, CutSel)
-        assert st["pairs"] == so["pairs"] and st["pairs_sorted"] <= 2 * st["pairs"]
+        # (front lists: dkey <= cut; fallback lists: a subset of the rest)
+        assert st["pairs"] == so["pairs"] and st["pairs_sorted"] <= st["pairs"]
         assert 0 <= st["open_tiles"] <= 16 * st["tiles"]  # (8x8 quadrants left open)
         opened += st["open_tiles"]
         if k in (0, 5):
             ref, _ = O.render(sc, V, P, w, h, sh_degree=sh, mode=mode)
             assert _bits(a, ref) == 0, k
-    print(f"{n} @{w}x{h} {mode} {path}: pairs {st['pairs']} sorted {st['pairs_sorted']} open tiles (sum) {opened}")
+    print(f"{n} @{w}x{h} {mode} {path} {binning}: pairs {st['pairs']} sorted {st['pairs_sorted']} "
+          f"open tiles (sum) {opened}")
 
 
-def test_depth_cuts_still_camera_saves_pairs(built):
+@pytest.mark.parametrize("binning", ["bin_first", "depth_first"])
+def test_depth_cuts_still_camera_saves_pairs(built, binning):
     """The bench-like dense scene under a still camera: from the third frame
     on, the lists hold a fraction of the pairs and no tile is left open."""
     # the bench scene's coverage per pixel (6M splats @1080p) at a quarter of
     # the pixels: 1.5M splats of twice the size @960x540
     sc = _scene(1_500_000, 5, 0, 16 / 9, scale=2.0)
-    cut, whole = _pair(sc)
+    cut, whole = _pair(sc, binning=binning)
     V, P = orbit_views(960, 540, 1)[0]
     ref = whole.render_host(V, P, 960, 540)
     for k in range(4):
@@ -112,7 +120,8 @@ def test_depth_cuts_still_camera_saves_pairs(built):
     assert st["open_tiles"] == 0, st
 
 
-def test_depth_cuts_jump_opens_tiles(built):
+@pytest.mark.parametrize("binning", ["bin_first", "depth_first"])
+def test_depth_cuts_jump_opens_tiles(built, binning):
     """One frame in flight: each frame uses the previous frame's cuts.  A
     view that moves the scene nearer after a still stretch leaves tiles open
     (their saturation lies behind the old cuts); the fallback lists finish
@@ -120,7 +129,7 @@ def test_depth_cuts_jump_opens_tiles(built):
     from gaussian_splat_amd.api import default_camera
     W, H = 640, 360
     sc = _scene(400000, 23, 0, W / H, scale=1.2)
-    cut, whole = _pair(sc)
+    cut, whole = _pair(sc, binning=binning)
     far = default_camera(W, H)
     far.setDistance(7.0)
     near = default_camera(W, H)
@@ -146,7 +155,8 @@ def test_depth_cuts_bgra8_and_resolution_change(built):
             assert _bits(cut.render_host(V, P, w, h), whole.render_host(V, P, w, h)) == 0
 
 
-def test_depth_cuts_pipelined_camera_path(built):
+@pytest.mark.parametrize("binning", ["bin_first", "depth_first"])
+def test_depth_cuts_pipelined_camera_path(built, binning):
     """Two frames in flight: a frame's cuts come from the frame before last
     (its buffer set); its fallback lists are built on the composite stream
     while the side stream projects the next frame into the other set (rects,
@@ -166,7 +176,7 @@ def test_depth_cuts_pipelined_camera_path(built):
     ref = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False, binning="bin_first", depth_split=False))
     ref.initialize(0)
     refs = [ref.render_host(V, P, W, H) for V, P in views]
-    r = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False, binning="bin_first", frames_in_flight=2,
+    r = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False, binning=binning, frames_in_flight=2,
                                            depth_split=True))
     r.initialize(0)
     outs = [r.render(V, P, W, H).clone() for V, P in views for _ in range(3)]
