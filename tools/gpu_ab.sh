@@ -1,11 +1,7 @@
 #!/bin/bash
 # A/B on the GPU box: bench each ab/<name>.so in VARIANTS (default: all), ROUNDS times interleaved;
-# optional TRACE variants run tools/composite_trace.py.  Every GPU step has its own time limit.
+# optional PARITY variants run the parity tests first.  Every GPU step has its own time limit.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for v in ${TRACE}; do
-  GSPLAT_LIB=$PWD/ab/$v.so timeout -k 10 300 python tools/composite_trace.py > gpurun_out/trace_$v.txt 2>&1; rc=$?
-  echo "== trace $v rc=$rc"; grep -v amdgpu.ids gpurun_out/trace_$v.txt; [ $rc -eq 0 ] || exit $rc
-done
 for v in ${PARITY}; do
   GSPLAT_LIB=$PWD/ab/$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -q -m gpu \
     -k "${AB_TESTS:-1080p or config1 or cap_parity or virtual_slabs or anisotropic or config2 or config3}" --timeout 200 --timeout-method thread \
