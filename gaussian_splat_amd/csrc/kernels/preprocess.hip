@@ -157,12 +157,15 @@ __device__ __forceinline__ EllipseX ellipse_x(float ax, float ay, float bx, floa
     e.pad = 0.01f + 1e-3f * fabsf(e.xs);
     return e;
 }
-template <int SHIFT>  // cell size 1 << SHIFT px: 3 = the composite's 8x8 cells, 5 = 32x32 bins
+// The exclusion mask of the rect's first 4x4 cells of 1 << shift px (3: the
+// composite's 8x8 cells, 5: 32x32 bins); 0 (no claim) for a rect of one cell
+// or wider than 4 cells.  shift is per lane: one loop serves the lanes that
+// need cells and those that need bins.
 __device__ __forceinline__ uint32_t cell_exclusion_mask(const EllipseX& e, float cx, float cy, uint32_t x0, uint32_t y0,
-                                                        uint32_t x1, uint32_t y1) {
-    constexpr uint32_t CS = 1u << SHIFT;
-    constexpr float ICS = 1.0f / (float)CS;
-    const uint32_t cx0 = x0 >> SHIFT, cy0 = y0 >> SHIFT, cx1 = x1 >> SHIFT, cy1 = y1 >> SHIFT;
+                                                        uint32_t x1, uint32_t y1, uint32_t shift) {
+    const uint32_t CS = 1u << shift;
+    const float fcs = (float)CS, ICS = shift == 3u ? 0.125f : 0.03125f;
+    const uint32_t cx0 = x0 >> shift, cy0 = y0 >> shift, cx1 = x1 >> shift, cy1 = y1 >> shift;
     if (cx1 - cx0 >= 4u || cy1 - cy0 >= 4u) return 0u;
     if (cx1 == cx0 && cy1 == cy0) return 0u;  // one cell: the rect itself decides
     if (!e.ok) return 0u;
@@ -171,7 +174,7 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(const EllipseX& e, float
     uint32_t excl = 0;
     for (uint32_t r = 0; r <= cy1 - cy0; ++r) {
         const float pyA = (float)((cy0 + r) * CS);  // band's pixel rows pyA .. pyA+CS-1
-        float yl = cy - (pyA + ((float)CS - 0.5f)), yh = cy - (pyA + 0.5f);
+        float yl = cy - (pyA + (fcs - 0.5f)), yh = cy - (pyA + 0.5f);
         yl = fmaxf(yl, -e.ymax);
         yh = fminf(yh, e.ymax);
         uint32_t keep = 0u;  // (none unless the band meets the ellipse)
@@ -189,6 +192,32 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(const EllipseX& e, float
         excl |= (all & ~keep) << (r * 4u);
     }
     return excl;
+}
+
+// The bin-exclusion mask of a rect within 4x4 8-px cells (so within 2x2
+// bins) from its cell mask: a bin is excluded when every cell of the rect in
+// it is.  Bit br*4 + bq: bin (bx0 + bq, by0 + br), bx0 = x0 >> 5.
+__device__ __forceinline__ uint32_t bins_from_cells(uint32_t cexcl, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    const uint32_t cx0 = x0 >> 3, cy0 = y0 >> 3, cx1 = x1 >> 3, cy1 = y1 >> 3;
+    const uint32_t ncol = cx1 - cx0 + 1u, nrow = cy1 - cy0 + 1u;
+    // cells of the rect in bin column 0 / row 0: those before the next 4-cell boundary
+    const uint32_t split_x = min(4u - (cx0 & 3u), ncol), split_y = min(4u - (cy0 & 3u), nrow);
+    const uint32_t col0 = (1u << split_x) - 1u, col1 = ((1u << ncol) - 1u) & ~col0;
+    uint32_t row0 = 0u, row1 = 0u;  // the rect's cell bits (4 per cell row) of bin row 0 / 1
+#pragma unroll
+    for (uint32_t r = 0; r < 4u; ++r) {
+        const uint32_t m = r < nrow ? 0xFu << (4u * r) : 0u;
+        if (r < split_y) row0 |= m;
+        else row1 |= m;
+    }
+    uint32_t b = 0u;
+    const uint32_t inc = ~cexcl;  // (cells not excluded)
+    auto colm = [](uint32_t c) { return c | c << 4 | c << 8 | c << 12; };
+    if ((inc & row0 & colm(col0)) == 0u) b |= 1u;
+    if (col1 && (inc & row0 & colm(col1)) == 0u) b |= 2u;
+    if (row1 && (inc & row1 & colm(col0)) == 0u) b |= 16u;
+    if (col1 && row1 && (inc & row1 & colm(col1)) == 0u) b |= 32u;
+    return b;
 }
 
 #ifndef GS_PRE_WAVES  // A/B knob: min waves per SIMD (caps the VGPRs)
@@ -362,9 +391,13 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
 #else
                     uint32_t excl = 0u, bexcl = 0u;
                     if (U.cell_mask) {
+                        // a rect within 4x4 cells: its cell mask, and the bin
+                        // mask from it; a wider one: no cell claim, its bin mask
                         const EllipseX ex = ellipse_x(ra.z, ra.w, rb.x, rb.y);
-                        excl = cell_exclusion_mask<3>(ex, cx, cy, x0, y0, x1, y1);
-                        bexcl = cell_exclusion_mask<kBinShift>(ex, cx, cy, x0, y0, x1, y1);
+                        const bool small = (x1 >> 3) - (x0 >> 3) < 4u && (y1 >> 3) - (y0 >> 3) < 4u;
+                        const uint32_t m = cell_exclusion_mask(ex, cx, cy, x0, y0, x1, y1, small ? 3u : 5u);
+                        excl = small ? m : 0u;
+                        bexcl = small ? bins_from_cells(m, x0, y0, x1, y1) : m;
                     }
 #endif
                     o[0] = ra;
