@@ -282,50 +282,34 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
             float S00 = dot3(M00, M01, M02, M00, M01, M02);
             float S01 = dot3(M00, M01, M02, M10, M11, M12);
             float S02 = dot3(M00, M01, M02, M20, M21, M22);
-            float S10 = dot3(M10, M11, M12, M00, M01, M02);
             float S11 = dot3(M10, M11, M12, M10, M11, M12);
             float S12 = dot3(M10, M11, M12, M20, M21, M22);
-            float S20 = dot3(M20, M21, M22, M00, M01, M02);
-            float S21 = dot3(M20, M21, M22, M10, M11, M12);
             float S22 = dot3(M20, M21, M22, M20, M21, M22);
-            // K3: Sigma_view = (W Sigma) W^T, W(r,c) = V[c*4+r] (tile.metal:109-115)
-            float W00 = V[0], W01 = V[4], W02 = V[8];
-            float W10 = V[1], W11 = V[5], W12 = V[9];
-            float W20 = V[2], W21 = V[6], W22 = V[10];
-            float T00 = dot3(W00, W01, W02, S00, S10, S20);
-            float T01 = dot3(W00, W01, W02, S01, S11, S21);
-            float T02 = dot3(W00, W01, W02, S02, S12, S22);
-            float T10 = dot3(W10, W11, W12, S00, S10, S20);
-            float T11 = dot3(W10, W11, W12, S01, S11, S21);
-            float T12 = dot3(W10, W11, W12, S02, S12, S22);
-            float T20 = dot3(W20, W21, W22, S00, S10, S20);
-            float T21 = dot3(W20, W21, W22, S01, S11, S21);
-            float T22 = dot3(W20, W21, W22, S02, S12, S22);
-            float V00 = dot3(T00, T01, T02, W00, W01, W02);
-            float V01 = dot3(T00, T01, T02, W10, W11, W12);
-            float V02 = dot3(T00, T01, T02, W20, W21, W22);
-            float V10 = dot3(T10, T11, T12, W00, W01, W02);
-            float V11 = dot3(T10, T11, T12, W10, W11, W12);
-            float V12 = dot3(T10, T11, T12, W20, W21, W22);
-            float V20 = dot3(T20, T21, T22, W00, W01, W02);
-            float V21 = dot3(T20, T21, T22, W10, W11, W12);
-            float V22 = dot3(T20, T21, T22, W20, W21, W22);
-            // Jacobian, reference sign convention (tile.metal:117-123)
+            // K3 + Jacobian (tile.metal:109-127): cov = J (W Sigma W^T) J^T,
+            // evaluated as A Sigma A^T with A = J W (2x3; the contract's order,
+            // Sigma symmetric, J's zero entries skipped).
+            // W(r,c) = V[c*4+r]; J with the reference's z-column sign (:117-123).
             float fx = U.P[0] * ((float)U.width * 0.5f);
             float fy = U.P[5] * ((float)U.height * 0.5f);
             float iz = 1.0f / zf;
             float iz2 = iz * iz;
-            float J00 = fx * iz, J01 = 0.0f, J02 = ((-fx) * vx) * iz2;
-            float J10 = 0.0f, J11 = fy * iz, J12 = ((-fy) * vy) * iz2;
-            float SJ00 = dot3(V00, V01, V02, J00, J01, J02);
-            float SJ01 = dot3(V10, V11, V12, J00, J01, J02);
-            float SJ02 = dot3(V20, V21, V22, J00, J01, J02);
-            float SJ10 = dot3(V00, V01, V02, J10, J11, J12);
-            float SJ11 = dot3(V10, V11, V12, J10, J11, J12);
-            float SJ12 = dot3(V20, V21, V22, J10, J11, J12);
-            float ca = dot3(J00, J01, J02, SJ00, SJ01, SJ02);
-            float cb = dot3(J00, J01, J02, SJ10, SJ11, SJ12);
-            float cc = dot3(J10, J11, J12, SJ10, SJ11, SJ12);
+            float J00 = fx * iz, J02 = ((-fx) * vx) * iz2;
+            float J11 = fy * iz, J12 = ((-fy) * vy) * iz2;
+            float A00 = __builtin_fmaf(J02, V[2], J00 * V[0]);
+            float A01 = __builtin_fmaf(J02, V[6], J00 * V[4]);
+            float A02 = __builtin_fmaf(J02, V[10], J00 * V[8]);
+            float A10 = __builtin_fmaf(J12, V[2], J11 * V[1]);
+            float A11 = __builtin_fmaf(J12, V[6], J11 * V[5]);
+            float A12 = __builtin_fmaf(J12, V[10], J11 * V[9]);
+            float B00 = dot3(A00, A01, A02, S00, S01, S02);
+            float B01 = dot3(A00, A01, A02, S01, S11, S12);
+            float B02 = dot3(A00, A01, A02, S02, S12, S22);
+            float B10 = dot3(A10, A11, A12, S00, S01, S02);
+            float B11 = dot3(A10, A11, A12, S01, S11, S12);
+            float B12 = dot3(A10, A11, A12, S02, S12, S22);
+            float ca = dot3(B00, B01, B02, A00, A01, A02);
+            float cb = dot3(B00, B01, B02, A10, A11, A12);
+            float cc = dot3(B10, B11, B12, A10, A11, A12);
             ca = ca + 1e-4f;  // tile.metal:129-131
             cc = cc + 1e-4f;
             // K4 eigenSym2x2 (tile.metal:62-83) and radii (:136-140)

@@ -502,33 +502,29 @@ void ora_project(const ora_scene *s, int64_t i, const float V[16], const float P
     float S[3][3];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) S[r][c] = dot3f(M[r][0], M[r][1], M[r][2], M[c][0], M[c][1], M[c][2]);
+    /* (S is symmetric bit for bit: dot3f's products commute) */
 
-    /* K3: Sigma_view = (W Sigma) W^T, W(i,j) = V[col j][row i] (tile.metal:109-115). */
-    float Wm[3][3];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) Wm[r][c] = V[c * 4 + r];
-    float T[3][3];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) T[r][c] = dot3f(Wm[r][0], Wm[r][1], Wm[r][2], S[0][c], S[1][c], S[2][c]);
-    float Sv[3][3];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) Sv[r][c] = dot3f(T[r][0], T[r][1], T[r][2], Wm[c][0], Wm[c][1], Wm[c][2]);
-
-    /* Jacobian with the reference's z-column sign (tile.metal:117-123). */
+    /* K3 + Jacobian (tile.metal:109-127): cov2d = J (W Sigma W^T) J^T,
+     * evaluated as A Sigma A^T with A = J W, W(i,j) =
+     * V[col j][row i], J with the reference's z-column sign (:117-123) and
+     * its zero entries skipped. */
     float fx = P[0] * ((float)W * 0.5f);
     float fy = P[5] * ((float)H * 0.5f);
     float iz = 1.0f / zf;
     float iz2 = iz * iz;
-    float J0[3] = {fx * iz, 0.0f, ((-fx) * vx) * iz2};
-    float J1[3] = {0.0f, fy * iz, ((-fy) * vy) * iz2};
-    float SJ0[3], SJ1[3];
-    for (int r = 0; r < 3; ++r) {
-        SJ0[r] = dot3f(Sv[r][0], Sv[r][1], Sv[r][2], J0[0], J0[1], J0[2]);
-        SJ1[r] = dot3f(Sv[r][0], Sv[r][1], Sv[r][2], J1[0], J1[1], J1[2]);
+    float J00 = fx * iz, J02 = ((-fx) * vx) * iz2;
+    float J11 = fy * iz, J12 = ((-fy) * vy) * iz2;
+    float A[2][3];
+    for (int c = 0; c < 3; ++c) {
+        A[0][c] = fmaf(J02, V[c * 4 + 2], J00 * V[c * 4 + 0]);
+        A[1][c] = fmaf(J12, V[c * 4 + 2], J11 * V[c * 4 + 1]);
     }
-    float a = dot3f(J0[0], J0[1], J0[2], SJ0[0], SJ0[1], SJ0[2]);
-    float b = dot3f(J0[0], J0[1], J0[2], SJ1[0], SJ1[1], SJ1[2]);
-    float c = dot3f(J1[0], J1[1], J1[2], SJ1[0], SJ1[1], SJ1[2]);
+    float B[2][3];
+    for (int r = 0; r < 2; ++r)
+        for (int c = 0; c < 3; ++c) B[r][c] = dot3f(A[r][0], A[r][1], A[r][2], S[0][c], S[1][c], S[2][c]);
+    float a = dot3f(B[0][0], B[0][1], B[0][2], A[0][0], A[0][1], A[0][2]);
+    float b = dot3f(B[0][0], B[0][1], B[0][2], A[1][0], A[1][1], A[1][2]);
+    float c = dot3f(B[1][0], B[1][1], B[1][2], A[1][0], A[1][1], A[1][2]);
     a = a + 1e-4f; /* tile.metal:129-131 */
     c = c + 1e-4f;
 
