@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round-2 artifacts: GPU tests, driver-default bench, profiled unpipelined bench + rocprofv3 kernel
-# stats of the same command, PMC summary, other BASELINE configs, heavy-tail scene, 2-rank rehearsal.
-# Every GPU step has its own time limit; the script stops at the first failure.
+# Round artifacts: GPU tests, driver-default bench, profiled unpipelined bench + rocprofv3 kernel
+# stats of the same command, PMC summary, other BASELINE configs, heavy-tail scene, orbiting camera,
+# 2-rank rehearsal, pipelined kernel timeline, virtual-rank row probes (config 4 and 5).
+# Every GPU step has its own time limit; the script stops at the first failure.  STEPS selects.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-O=gpurun_out/art; rm -rf $O; mkdir -p $O
+O=gpurun_out/art; mkdir -p $O
 step() { name=$1; shift; echo "== $name"; "$@"; rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-for s in ${STEPS:-tests bench prof pmc configs heavy ranks}; do case $s in
+for s in ${STEPS:-tests bench prof pmc configs heavy orbit ranks timeline}; do case $s in
 tests) step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
        tail -1 $O/pytest_gpu.log ;;
 bench) step bench bash -c "timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err"; cat $O/bench_default.json ;;
@@ -23,6 +24,15 @@ configs) for c in 1m 4k 50m; do
          python -c "import json;d=json.load(open('$O/bench_$c.json'));print('$c', d['ms_per_step'], d['value'], d['config']['binning'], d['roofline']['kernels']['composite']['ms'])"; done ;;
 heavy) step heavy bash -c "timeout -k 10 600 python bench.py --profile heavy --steps 50 --cpu-baseline 0 > $O/bench_heavy.json 2> $O/bench_heavy.err"
        python -c "import json;d=json.load(open('$O/bench_heavy.json'));print('heavy', d['ms_per_step'], d['value'], d['config']['pairs'])" ;;
+orbit) for p in uniform heavy; do
+         step orbit_$p bash -c "timeout -k 10 600 python bench.py --camera orbit --profile $p --steps 50 --cpu-baseline 0 --pmc 0 > $O/bench_orbit_$p.json 2> $O/bench_orbit_$p.err"
+         python -c "import json;d=json.load(open('$O/bench_orbit_$p.json'));c=d['config'];print('orbit $p', d['ms_per_step'], c['pairs'], c['pairs_sorted'], c['open_tiles'])"; done ;;
+timeline) step timeline bash -c "timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pmc 0 --no-stage-timing > $O/tl.log 2>&1"
+       python tools/trace_timeline.py $(find $O/tl -name "*kernel_trace.csv" | head -1) 3 > $O/timeline_fif2.txt; head -30 $O/timeline_fif2.txt ;;
+rows50m) step rows50m bash -c "timeout -k 10 900 python tools/rows_probe.py --splats 50000000 --width 3840 --height 2160 --sh 0 --frames 10 > $O/rows_probe_virtual_ranks_50m.json 2> $O/rows_probe_50m.err"
+       tail -5 $O/rows_probe_50m.err ;;
+rows4k) step rows4k bash -c "timeout -k 10 600 python tools/rows_probe.py --splats 6000000 --width 3840 --height 2160 --sh 3 > $O/rows_probe_virtual_ranks_4k.json 2> $O/rows_probe_4k.err"
+       tail -5 $O/rows_probe_4k.err ;;
 ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
        cat $O/rehearsal_2rank_gloo.json ;;
 esac; done

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-x}
 rm -rf gpurun_out/prof_$TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-  python bench.py --steps 10 --warmup 3 --cpu-baseline 0 --traffic 0 "$@" > gpurun_out/prof_$TAG.log 2>&1
+  python bench.py --steps 10 --warmup 3 --cpu-baseline 0 --pmc 0 "$@" > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/prof_$TAG.log; exit $rc; }
 f=$(find gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
 python - "$f" <<'PY'
