@@ -1507,7 +1507,7 @@ gs_status gs_project_host(gs_handle* h, const float* view, const float* proj, in
 
 gs_status gs_sorted_pairs_host(gs_handle* h, uint32_t* keys, uint32_t* vals, int64_t cap, int64_t* count) {
     if (!h || !count) return fail(GS_ERR_INVALID_ARG, "null argument");
-    if (h->cut_frame)
+    if (h->cut_lists)  // (a depth-cut frame without cuts yet has whole lists)
         return fail(GS_ERR_UNSUPPORTED, "the last frame's lists were cut at per-bin depths (depth_split = 0 keeps them whole)");
     int64_t P = h->stats.pairs;
     *count = P;
