@@ -194,6 +194,18 @@ __device__ __forceinline__ uint32_t cell_exclusion_mask(const EllipseX& e, float
     return excl;
 }
 
+// A bin mask that excludes every bin of the rect keeps its first one (see
+// bins_from_cells).
+__device__ __forceinline__ uint32_t keep_one_bin(uint32_t b, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    const uint32_t cols = (x1 >> 5) - (x0 >> 5) + 1u, rows = (y1 >> 5) - (y0 >> 5) + 1u;
+    if (cols > 4u || rows > 4u) return b;
+    const uint32_t row = (1u << cols) - 1u;
+    uint32_t all = 0u;
+#pragma unroll
+    for (uint32_t r = 0; r < 4u; ++r) all |= r < rows ? row << (4u * r) : 0u;
+    return b == all ? b & ~1u : b;
+}
+
 // The bin-exclusion mask of a rect within 4x4 8-px cells (so within 2x2
 // bins) from its cell mask: a bin is excluded when every cell of the rect in
 // it is.  Bit br*4 + bq: bin (bx0 + bq, by0 + br), bx0 = x0 >> 5.
@@ -217,6 +229,11 @@ __device__ __forceinline__ uint32_t bins_from_cells(uint32_t cexcl, uint32_t x0,
     if (col1 && (inc & row0 & colm(col1)) == 0u) b |= 2u;
     if (row1 && (inc & row1 & colm(col0)) == 0u) b |= 16u;
     if (col1 && row1 && (inc & row1 & colm(col1)) == 0u) b |= 32u;
+    // a splat whose ellipse reaches no pixel centre of its rect keeps its
+    // first bin: every non-empty rect emits a pair (gs_stats.visible counts
+    // the oracle's visible splats; the pair adds exact zeros)
+    const uint32_t allb = (col1 ? 3u : 1u) * (row1 ? 17u : 1u);
+    if (b == allb) b &= ~1u;
     return b;
 }
 
@@ -381,7 +398,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
                         const bool small = (x1 >> 3) - (x0 >> 3) < 4u && (y1 >> 3) - (y0 >> 3) < 4u;
                         const uint32_t m = cell_exclusion_mask(ex, cx, cy, x0, y0, x1, y1, small ? 3u : 5u);
                         excl = small ? m : 0u;
-                        bexcl = small ? bins_from_cells(m, x0, y0, x1, y1) : m;
+                        bexcl = small ? bins_from_cells(m, x0, y0, x1, y1) : keep_one_bin(m, x0, y0, x1, y1);
                     }
 #endif
                     o[0] = ra;
