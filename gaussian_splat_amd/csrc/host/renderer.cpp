@@ -597,7 +597,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         flt.bmask = (1u << bits) - 1u;
         flt.dshift = bits;
         flt.kept = h->kept.as<uint32_t>() + h->set;
-        if (pc.C) pc.cut = h->cut_in;  // (the duplicate counts the kept pairs' digits)
+        pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
     }
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
@@ -666,8 +666,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
-        pc = pass_counts(h, m, order == nullptr, plan, cap, P);
-        if (cut_frame && pc.C) pc.cut = h->cut_in;
+        pc = cut_frame ? gs::PassCounts{} : pass_counts(h, m, order == nullptr, plan, cap, P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         if (tail) {  // (the no-op frame's composite counted into these)
             GS_HIP(hipStreamSynchronize(st));
@@ -1361,6 +1360,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             fuse.nb = nb;
             fuse.fill = h->ranges.as<uint2>();
             fuse.nfill = T;
+            if (h->cut_in) h->fused_prep.pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
             fuse.zero = h->fused_prep.pc.C;
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
             h->fused_prep.ok = true;

@@ -68,12 +68,9 @@ hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uin
 // `ntiles` columns, tiles of `tile` pairs, digit = bin & mask: the index-order
 // duplicate adds them up as it writes (C zeroed before), so the sort skips
 // that pass's count kernel (launch_radix_sort first_counted).  C null: off.
-// cut (depth-cut frames, SortFilter): only the pairs at or ahead of their
-// bin's cut are counted, as the filtered first pass keeps them.
 struct PassCounts {
     uint32_t* C = nullptr;
     uint32_t tile = 0, mask = 0, ntiles = 0;
-    const uint32_t* cut = nullptr;
 };
 constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts in LDS (the rest: global atomics)
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j

@@ -419,7 +419,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
                                   const uint32_t* n_dev, bool first_counted, const SortFilter& flt = SortFilter{}) {
-    if (flt.cut && (NV != 1 || !flt.kept)) return hipErrorInvalidValue;
+    if (flt.cut && (NV != 1 || first_counted || !flt.kept)) return hipErrorInvalidValue;
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -447,9 +447,8 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         hipError_t e = hipSuccess;
         if constexpr (NV == 1) {
             if (filt) {
-                if (!first_counted)  // (or counted by the producer with the same filter, PassCounts::cut)
-                    rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p],
-                                                                            C, tiles, n_dev, flt);
+                rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                        tiles, n_dev, flt);
                 rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
                 e = launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
                                           tiles, rg, rmask, n_dev, flt);

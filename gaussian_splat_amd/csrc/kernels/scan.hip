@@ -79,11 +79,8 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
 // One 1024-lane workgroup: each lane scans kPartIpt consecutive block sums in
 // registers, one block-wide scan joins them (a single pass for nb <= 4096;
 // larger grids loop).
-#ifndef GS_PART_THREADS  // A/B knob (a narrow workgroup finds a CU beside a co-running composite sooner)
-#define GS_PART_THREADS 1024
-#endif
-constexpr int kPartThreads = GS_PART_THREADS;
-constexpr int kPartIpt = 4096 / kPartThreads;
+constexpr int kPartThreads = 1024;
+constexpr int kPartIpt = 4;
 
 template <typename T>
 __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
@@ -261,13 +258,11 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         auto keep = [](uint32_t) { return true; };
         if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
-            const uint32_t dkk = dk[k];
             emit_bin_pairs_if(r, tiles_x, src.own, key_hi, val, off, keys, vals, keep, [&](uint32_t g, uint32_t bin) {
                 if (g == next) {
                     ++t;
                     next += pc.tile;
                 }
-                if (pc.cut && dkk > pc.cut[bin]) return;  // (a depth-cut frame's first pass keeps the front pairs)
                 const uint32_t d = bin & pc.mask;
                 if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
                 else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
