@@ -226,24 +226,18 @@ __device__ void sort_list_global(uint32_t s, uint32_t m, uint32_t* keys, uint32_
     }
 }
 
-#ifndef GS_SEG_SPLIT  // A/B knob: two size classes (launch_bin_depth_sort)
-#define GS_SEG_SPLIT 0
-#endif
 #ifndef GS_SEG_MINW  // min waves per SIMD (launch bounds: caps the VGPRs)
 #define GS_SEG_MINW 6
 #endif
 
-// skip_le: lists of at most this many pairs are left to another launch (a
-// smaller size class); SMALL: lists longer than NT * IPT are left alone.
-template <int NT, int IPT, int MINW = 1, bool SMALL = false>
+template <int NT, int IPT, int MINW = 1>
 __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* __restrict__ ranges,
                                                                   uint32_t* __restrict__ keys,
                                                                   uint32_t* __restrict__ vals,
                                                                   uint32_t* __restrict__ tmp_keys,
                                                                   uint32_t* __restrict__ tmp_vals, int bin_bits,
                                                                   uint32_t* __restrict__ sample,
-                                                                  const unsigned long long* __restrict__ guard,
-                                                                  uint32_t skip_le) {
+                                                                  const unsigned long long* __restrict__ guard) {
     static_assert((uint32_t)NT * IPT <= (1u << kSegPosBits), "position field");
     __shared__ SegRankLds<NT> L;
     __shared__ uint32_t stage[NT * IPT];
@@ -254,10 +248,10 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
         if (blockIdx.x == 0) atomicOr(&sample[1], kSegSampleValid);
         if (m > (uint32_t)NT * IPT) atomicAdd(&sample[0], m);
     }
-    if (m < 2u || m <= skip_le) return;  // nothing to order (or another launch's)
+    if (m < 2u) return;  // nothing to order
     const uint32_t s = rg.x;
     if (m > (uint32_t)NT * IPT) {  // a hot bin: chunked LSD over global memory
-        if constexpr (!SMALL) sort_list_global<NT, 8>(s, m, keys, vals, tmp_keys, tmp_vals, bin_bits, L, stage);
+        sort_list_global<NT, 8>(s, m, keys, vals, tmp_keys, tmp_vals, bin_bits, L, stage);
         return;
     }
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -325,15 +319,8 @@ hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* 
     if (bin_bits < 0 || bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     // one workgroup per bin
     static_assert(GS_SEG_NT * GS_SEG_IPT == kSegLdsMax, "gs_kernels.h");
-#if GS_SEG_SPLIT  // A/B: lists of <= 2048 pairs in a 256 x 8 size class first (fewer registers, more workgroups per CU)
-    hipExtLaunchKernelGGL((bin_depth_sort_kernel<256, 8, 8, true>), dim3(nbins), dim3(256), 0, st, nullptr, nullptr, 0,
-                          ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, nullptr, guard, 0u);
-    const uint32_t skip = 2048u;
-#else
-    const uint32_t skip = 0u;
-#endif
     hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>), dim3(nbins), dim3(GS_SEG_NT), 0,
-                          st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample, guard, skip);
+                          st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample, guard);
     return hipGetLastError();
 }
 
