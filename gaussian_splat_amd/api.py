@@ -56,7 +56,7 @@ class Options:
     binning: str = "default"
     # bin-first frames in two depth slabs, the second only where the first left pixels open
     # (True) or in one (False, the default: measured faster); the same image
-    depth_split: bool = False
+    depth_split: bool = True  # per-bin depth cuts (gs_options.depth_split): same image, fewer pairs sorted
 
     def to_c(self) -> GsOptions:
         o = GsOptions()

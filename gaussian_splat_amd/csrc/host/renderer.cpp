@@ -1044,6 +1044,7 @@ void gs_default_options(gs_options* o) {
     o->crop_radius = 5.0f;
     o->stage_timing = 0;
     o->frames_in_flight = 1;
+    o->depth_split = 1;  // per-bin depth cuts: same image, fewer pairs sorted
 }
 
 gs_status gs_create_from_soa(const gs_scene_soa* scene, const gs_options* opt, gs_handle** out) {

@@ -77,13 +77,14 @@ typedef struct gs_options {
                               at a resolution goes depth-first), 1 = depth-first (global depth
                               sort of the splats, then binning), 2 = bin-first (bin lists in
                               arrival order, then a stable per-bin depth sort).  DESIGN.md §1 */
-    int32_t depth_split;   /* per-bin depth cuts (single-GPU bin-first frames, modes
-                              tile/live50, no cap): 1 = a frame's bin lists hold only the pairs at
-                              or in front of their bin's cut, the depth at which the bin's tiles
-                              saturated in the previous frame on the same buffer set, plus a
-                              margin; a tile those lists leave open finishes from its saved state
-                              with the rest of its bin's pairs (fallback lists).  Same image, bit
-                              for bit, for any camera path; 0 = whole lists */
+    int32_t depth_split;   /* per-bin depth cuts (single-GPU frames, modes
+                              tile/live50, no cap): 1 (gs_default_options) = a frame's bin lists
+                              hold only the pairs at or in front of their bin's cut, the depth at
+                              which the bin's tiles saturated in the previous frame on the same
+                              buffer set, plus a margin; a tile those lists leave open finishes
+                              from its saved state with the rest of its bin's pairs (fallback
+                              lists).  Same image, bit for bit, for any camera path; 0 = whole
+                              lists */
     int32_t reserved[3];
 } gs_options;
 
