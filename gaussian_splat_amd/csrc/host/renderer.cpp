@@ -716,6 +716,9 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     }
     GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, cut_margin(), sc, fb));
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
+#ifdef GS_AB_NO_FALLBACK  // timing ablation build only: exact only while no quadrant is left open
+    return GS_OK;
+#endif
     const int bits = h->last_key_bits;
     const uint32_t cap = h->pair_cap;
     GS_HIP(reserve_after(h->scratch2, gs::radix_sort_scratch_words(cap) * 4, sc));
