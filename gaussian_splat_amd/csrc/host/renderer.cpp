@@ -728,6 +728,10 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     flt.dshift = bits;
     flt.kept = fb.kept;
     flt.behind = 1;
+    // (usually no quadrant is open and the sort's input is empty: a fixed
+    // grid that loops over the tiles then costs a few workgroups, not one
+    // per tile of the frame's pairs)
+    flt.stride_grid = 512;
     bool in_tmp = false;
     uint32_t* fk = h->fkeys.as<uint32_t>();
     uint32_t* fv = h->fvals.as<uint32_t>();

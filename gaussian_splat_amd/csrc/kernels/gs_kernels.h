@@ -149,6 +149,7 @@ struct SortFilter {
     int dshift = 0;
     uint32_t* kept = nullptr;
     uint32_t behind = 0;
+    uint32_t stride_grid = 0;  // > 0: every pass on at most this many workgroups, looping over the tiles
     __device__ __forceinline__ bool keep(uint32_t key) const {
         return ((key >> dshift) <= cut[key & bmask]) != (behind != 0u);
     }

@@ -82,7 +82,7 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
 // FILT (the first pass of a depth-cut frame's bin sort, SortFilter): only
 // the items at or ahead of their bin's cut are counted and sorted.  Compiled
 // in only where it is used, so the other kernels keep their registers.
-template <int NV, bool FILT>
+template <int NV, bool FILT, bool STRIDE = false>
 __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                         uint32_t mask, uint32_t* __restrict__ C, uint32_t ntiles,
                                                         const uint32_t* __restrict__ n_dev, const SortFilter flt) {
@@ -91,9 +91,10 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
     if (n == 0u) return;    // (nothing to sort: the scan and the pass return at once)
     __shared__ uint32_t h[kRsWaves][kSortBins];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t t0 = blockIdx.x * TILE;
+    const uint32_t t0 = tile * TILE;
     constexpr int K = TILE / kRsThreads;
     if (t0 >= n) {  // (n read on the device: tiles past it count zeros)
     } else {
@@ -114,7 +115,10 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
         uint32_t c = 0;
 #pragma unroll
         for (int w = 0; w < kRsWaves; ++w) c += h[w][tid];
-        C[(size_t)tid * ntiles + blockIdx.x] = c;
+        C[(size_t)tid * ntiles + tile] = c;
+    }
+    if constexpr (!STRIDE) break;
+    __syncthreads();  // (the next tile clears h)
     }
 }
 
@@ -173,7 +177,9 @@ __global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __re
 // the caller fills the array with 0xFF first (empty = {~0, ~0} = [~0, 0)).
 // Bits above rmask ride along unsorted (the bin-first binning carries each
 // pair's depth key there, bin_depth_sort.hip).
-template <int NV, int BITS, bool FILT>
+// STRIDE: a fixed grid loops over the tiles (the depth-cut fallback lists'
+// sort, whose input is usually empty: a small grid then costs little).
+template <int NV, int BITS, bool FILT, bool STRIDE = false>
 __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t tile = blockIdx.x;
+    for (uint32_t tile = blockIdx.x; tile * TILE < n; tile += gridDim.x) {
     for (uint32_t i = tid; i < kRsWaves * ND; i += kRsThreads) (&wh[0][0])[i] = 0;
     // Keys and all value arrays are loaded up front so their latency hides
     // behind the ranking.  Barriers here order LDS only: they never wait for
@@ -367,6 +373,9 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
             if (j < cnt) io.vout[a][gdst[k]] = stage[j];
         }
     }
+    if constexpr (!STRIDE) break;
+    __syncthreads();  // (the next tile reuses the LDS arrays)
+    }
 }
 
 SortPlan make_sort_plan(int bits, bool narrow_first) {
@@ -397,18 +406,19 @@ size_t radix_sort_scratch_words(uint32_t n) {
     return (size_t)(tiles ? tiles : 1) * kSortBins + kSortBins;
 }
 
-// rts_pass_kernel for a digit width (the ballot match unrolled per width)
-template <int NV, bool FILT, typename... A>
+// rts_pass_kernel for a digit width (the ballot match unrolled per width);
+// STRIDE: `tiles` workgroups loop over all the tiles
+template <int NV, bool FILT, bool STRIDE = false, typename... A>
 static hipError_t launch_pass(int width, uint32_t tiles, hipStream_t st, A... args) {
     switch (width) {
-    case 1: rts_pass_kernel<NV, 1, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 2: rts_pass_kernel<NV, 2, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 3: rts_pass_kernel<NV, 3, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 4: rts_pass_kernel<NV, 4, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 5: rts_pass_kernel<NV, 5, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 6: rts_pass_kernel<NV, 6, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 7: rts_pass_kernel<NV, 7, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 8: rts_pass_kernel<NV, 8, FILT><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 1: rts_pass_kernel<NV, 1, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 2: rts_pass_kernel<NV, 2, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 3: rts_pass_kernel<NV, 3, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 4: rts_pass_kernel<NV, 4, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 5: rts_pass_kernel<NV, 5, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 6: rts_pass_kernel<NV, 6, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 7: rts_pass_kernel<NV, 7, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 8: rts_pass_kernel<NV, 8, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -446,6 +456,26 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
         const bool filt = p == 0 && flt.cut != nullptr;
         hipError_t e = hipSuccess;
         if constexpr (NV == 1) {
+            if (flt.cut && flt.stride_grid) {  // (every pass on a fixed grid looping over the tiles)
+                const uint32_t g = tiles < flt.stride_grid ? tiles : flt.stride_grid;
+                if (filt)
+                    rts_count_kernel<NV, true, true><<<g, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                             tiles, n_dev, flt);
+                else
+                    rts_count_kernel<NV, false, true><<<g, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p],
+                                                                              C, tiles, n_dev, SortFilter{});
+                rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
+                e = filt ? launch_pass<NV, true, true>(plan.width[p], g, st, io, n, plan.shift[p], plan.mask[p], C,
+                                                       totals, tiles, rg, rmask, n_dev, flt)
+                         : launch_pass<NV, false, true>(plan.width[p], g, st, io, n, plan.shift[p], plan.mask[p], C,
+                                                        totals, tiles, rg, rmask, n_dev, SortFilter{});
+                if (e != hipSuccess) return e;
+                if (filt) n_dev = flt.kept;
+                io.kin = io.kout;
+                for (int a = 0; a < NV; ++a) io.vin[a] = io.vout[a];
+                to_final = !to_final;
+                continue;
+            }
             if (filt) {
                 rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
                                                                         tiles, n_dev, flt);

@@ -65,15 +65,20 @@ def comp_res():
 def test_bin_sort_pass_budget(sort_res, bits):
     # one value array: the bin sort's passes (and the depth-cut frames'
     # filtered first pass)
-    r = _one(sort_res, rf"rts_pass_kernelILi1ELi{bits}ELb0EEEv")
+    r = _one(sort_res, rf"rts_pass_kernelILi1ELi{bits}ELb0ELb0EEEv")
     assert r["VGPRs Spill"] == 0 and r["ScratchSize"] == 0
     assert r["VGPRs"] <= 80 and r["Occupancy"] >= 6, r
 
 
 def test_filtered_sort_pass_budget(sort_res):
-    r = _one(sort_res, r"rts_pass_kernelILi1ELi6ELb1EEEv")
+    # the front lists' filtered pass
+    r = _one(sort_res, r"rts_pass_kernelILi1ELi6ELb1ELb0EEEv")
     assert r["VGPRs Spill"] == 0 and r["ScratchSize"] == 0
     assert r["VGPRs"] <= 80 and r["Occupancy"] >= 6, r
+    # the fallback lists' (a fixed grid looping over the tiles; usually empty input, so only
+    # spills are ruled out)
+    r = _one(sort_res, r"rts_pass_kernelILi1ELi6ELb1ELb1EEEv")
+    assert r["VGPRs Spill"] == 0 and r["ScratchSize"] == 0, r
 
 
 def test_projection_budget(pre_res):
