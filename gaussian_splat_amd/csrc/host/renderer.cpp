@@ -122,6 +122,7 @@ struct gs_handle {
         uint64_t frame_pairs = 0;       // P of the last scanned frame
         uint64_t sample_pairs = 0;      // P of the last bin-first frame (the sample's frame)
         double long_share = 0.0;        // share of its pairs in lists longer than kSegLdsMax
+        uint64_t wmax = 0, wmax_pairs = 0;  // a bin-first frame's wave-max emission work and its P
     } order;
     gs_stats stats{};
     // Bin-first single-GPU frames: the preprocess sums each scan block's
@@ -319,21 +320,29 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 }
 
 // Binning order of a frame (gs_options.binning).  Both orders
-// build the same lists; the default picks the cheaper one with a cost model
-// measured on MI355X (bench config and the 4K scale runs):
-//   depth-first: global depth sort, ~25 ps per splat (2 passes over N);
-//   bin-first:   per-bin depth sort, ~6 ps per pair in lists that fit LDS,
-//                ~20 ps per pair in longer lists, ~4.9 ns per bin
-// (6M splats: 1080p 85 vs 150 us -> bin-first; 4K 176 vs 150 us and
-// 50M @ 4K 3.7 vs 1.2 ms -> depth-first).
-// P (scaled by the item count: multi-GPU frames receive a varying number of
-// records) and the long-list share come from the previous frames at the same
-// resolution; with no history the frame goes depth-first.
+// build the same lists; the default picks the cheaper chain with a cost model
+// measured on MI355X (1080p uniform / heavy-tailed,
+// 4K, 50M @ 4K, with and without depth cuts):
+//   depth-first: global depth sort ~20 ps per splat, depth-order duplicate
+//                (wave-cooperative) ~4.5 ps per pair;
+//   bin-first:   index-order duplicate ~80 ps per unit of wave-max work W
+//                (the sum over waves of 64 splats of the largest pair count:
+//                the duplicate emits a wave's splats in lockstep, so a few
+//                huge splats dominate a heavy-tailed scene), plus the per-bin
+//                depth sort of the pairs that reach it, ~6 ps per pair in
+//                lists that fit LDS, ~20 ps in longer ones, ~4.9 ns per bin.
+// With depth cuts the per-bin sort sees the front lists only (about 0.3 P,
+// lists that fit LDS).  W comes from the last bin-first frame (the fused
+// preprocess measures it, PreFuse), scaled with P; before any, 0.07 P (the
+// uniform scenes' measured ratio).  P (scaled by the item count: multi-GPU
+// frames receive a varying number of records) and the long-list share come
+// from the previous frames at the same resolution; with no history the frame
+// goes depth-first.
 // Bin-first needs the depth key to fit above the bin id in a 32-bit pair key.
 // GS_BINNING=depth|bin overrides the option (A/B timing).
 // nrows: the bin rows this frame composites (multi-GPU ranks own a band of
 // them; the per-bin sort's fixed cost is paid for those only; -1: all).
-bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nrows = -1) {
+bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nrows = -1, bool cuts = false) {
     static const char* env = std::getenv("GS_BINNING");
     int b = h->opt.binning;
     if (env && std::strcmp(env, "depth") == 0) b = GS_BINNING_DEPTH_FIRST;
@@ -351,10 +360,13 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int n
     const double P = known ? (double)o.frame_pairs * (double)m / (double)o.n : 0.0;  // pairs scale with items
     o.n = (int64_t)m;  // items of this frame (the scan that follows reads its P)
     if (!known) return false;
-    const double f = o.long_share;
+    const double W = o.wmax_pairs > 0 ? (double)o.wmax * P / (double)o.wmax_pairs : 0.07 * P;
+    const double Ps = cuts ? 0.3 * P : P;             // pairs through the per-bin sort
+    const double f = cuts ? 0.0 : o.long_share;      // (front lists fit LDS)
     const double bins = nrows >= 0 ? (double)nrows * U.tiles_x : (double)T;
-    const double bin_ps = 6.0 * P * (1.0 - f) + 20.0 * P * f + 4900.0 * bins;
-    return bin_ps < 25.0 * (double)m;
+    const double bin_ps = 80.0 * W + 6.0 * Ps * (1.0 - f) + 20.0 * Ps * f + 4900.0 * bins;
+    const double depth_ps = 20.0 * (double)m + 4.5 * P;
+    return bin_ps < depth_ps;
 }
 
 gs_status check_ready(gs_handle* h) {
@@ -654,6 +666,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
     const uint64_t P = h->host_total[0], P_all = P;
     h->stats.visible = (int64_t)h->host_total[1];
+    if (fused && P_all > 0) {  // the duplicate's wave-max work (PreFuse), for the binning-order model
+        h->order.wmax = h->host_total[4];
+        h->order.wmax_pairs = P_all;
+    }
     h->stats.pairs = (int64_t)P_all;
     // the last per-bin depth sort's share of pairs in lists too long for LDS
     if ((h->host_total[3] & gs::kSegSampleValid) && h->order.sample_pairs)
@@ -1336,7 +1352,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     h->cut_pending = false;
     h->cut_in = h->cut_out = nullptr;
     if (!band && h->world == 1 && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
-        const bool bf = bin_first_order(h, U, (uint32_t)h->n);
+        const bool bf = bin_first_order(h, U, (uint32_t)h->n, -1, cut_on);
         h->order_pick = bf ? 1 : 0;
         cut_frame = cut_on && list_key_bits(U) + gs::kDepthBits <= 32;  // (the depth key rides above the bin id)
         if (cut_frame) {
@@ -1359,10 +1375,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         if (bf) {
             if ((s = prepare_lists(h, (uint32_t)h->n, true, U, &h->fused_prep)) != GS_OK) return s;
             const uint32_t nb = (uint32_t)((h->n + gs::kScanItems - 1) / gs::kScanItems);
-            GS_HIP(h->ppart.reserve((size_t)nb * 16));
-            if (h->ppart_words != (size_t)nb * 2 || h->ppart_dirty) {
-                GS_HIP(hipMemsetAsync(h->ppart.ptr, 0, (size_t)nb * 16, sp));  // (then kept clear by the scan)
-                h->ppart_words = (size_t)nb * 2;
+            GS_HIP(h->ppart.reserve((size_t)nb * 24));
+            if (h->ppart_words != (size_t)nb * 3 || h->ppart_dirty) {
+                GS_HIP(hipMemsetAsync(h->ppart.ptr, 0, (size_t)nb * 24, sp));  // (then kept clear by the scan)
+                h->ppart_words = (size_t)nb * 3;
             }
             fuse.part = h->ppart.as<unsigned long long>();
             fuse.nb = nb;

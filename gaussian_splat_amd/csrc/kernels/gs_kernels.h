@@ -20,10 +20,14 @@ namespace gs {
 // Bin-first single-GPU frames: the preprocess also does the
 // reduce half of the scan.  Every workgroup adds its splats' pair counts and
 // visible count into part[b] / part[nb + b] of its scan block b (kScanItems
-// splats; integer atomics, so the sums are exact), and the grid fills the
+// splats; integer atomics, so the sums are exact), and into part[2 nb + b]
+// the sum over its waves of the largest per-splat pair count (the
+// duplicate's wave-serial emission work in index order, for the binning-order
+// model: gs_handle OrderModel::wmax), and the grid fills the
 // frame's empty bin ranges and zeroes the first sort pass's digit counts
-// (what scan_reduce_kernel does otherwise).  part starts at zero and is
-// consumed and cleared again by launch_scan_partials_fused.
+// (what scan_reduce_kernel does otherwise).  part (3 nb words) starts at zero
+// and is consumed and cleared again by launch_scan_partials_fused, which
+// reports the wave-max sum in total[4].
 struct PreFuse {
     unsigned long long* part = nullptr;  // null: off
     uint32_t nb = 0;                     // scan blocks

@@ -422,11 +422,12 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
     if constexpr (EPI == 1) {
         // the scan's reduce half: this workgroup's pairs and visible splats
         // into its scan block's sums (the counts scan_duplicate recomputes)
-        __shared__ uint2 wsum[4];
+        __shared__ uint3 wsum[4];
         const uint32_t c = rect_tile_count(rlo, rhi, RowOwnership{nullptr, 0u}, U.cell_mask != 0);
         const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c), 63);
         const uint32_t wv = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c > 0u ? 1u : 0u), 63);
-        if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = make_uint2(ws, wv);
+        const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c), 63);  // (largest count)
+        if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = make_uint3(ws, wv, wm);
         // the frame's empty bin ranges and zeroed digit counts
         const uint32_t g = blockIdx.x * 256u + threadIdx.x;
         for (uint32_t z = g; z < fuse.nfill; z += gridDim.x * 256u) fuse.fill[z] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
@@ -436,8 +437,10 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
             const uint32_t b = blockIdx.x / (uint32_t)(kScanItems / 256);
             const uint32_t ps = wsum[0].x + wsum[1].x + wsum[2].x + wsum[3].x;
             const uint32_t pv = wsum[0].y + wsum[1].y + wsum[2].y + wsum[3].y;
+            const uint32_t pm = wsum[0].z + wsum[1].z + wsum[2].z + wsum[3].z;
             if (ps) atomicAdd(&fuse.part[b], (unsigned long long)ps);
             if (pv) atomicAdd(&fuse.part[fuse.nb + b], (unsigned long long)pv);
+            if (pm) atomicAdd(&fuse.part[2u * fuse.nb + b], (unsigned long long)pm);
         }
     }
 }

@@ -102,7 +102,8 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 }
 
 // src (may be null): the block sums come from there instead (the fused
-// preprocess's, PreFuse: 2 x nb words) and are cleared after reading.
+// preprocess's, PreFuse: 3 x nb words) and are cleared after reading; the
+// third row's sum (the duplicate's wave-max work) goes to total[4].
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
     }
     __shared__ uint64_t tmp[kPartThreads / 64];
     constexpr uint32_t CH = kPartThreads * kPartIpt;
-    uint64_t carry = 0, vis = 0;
+    uint64_t carry = 0, vis = 0, wmax = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
         const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
         uint64_t v[kPartIpt], s = 0;
@@ -125,7 +126,8 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
             if (src) {
                 v[k] = i0 + k < nb ? (uint64_t)src[i0 + k] : 0u;
                 vis += i0 + k < nb ? (uint64_t)src[nb + i0 + k] : 0u;
-                if (i0 + k < nb) src[i0 + k] = src[nb + i0 + k] = 0ull;  // (read by this lane only)
+                wmax += i0 + k < nb ? (uint64_t)src[2u * nb + i0 + k] : 0u;
+                if (i0 + k < nb) src[i0 + k] = src[nb + i0 + k] = src[2u * nb + i0 + k] = 0ull;  // (read by this lane only)
             } else {
                 v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
                 vis += i0 + k < nb ? partials[nb + i0 + k] : 0u;
@@ -141,11 +143,13 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         }
         carry += t;
     }
-    uint64_t vt;
+    uint64_t vt, wt = 0;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
+    if (src) block1024_exclusive_scan<uint64_t>(wmax, tmp, &wt);
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
+        total[4] = wt;
         if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
     }
 }
