@@ -323,9 +323,9 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 // build the same lists; the default picks the cheaper chain with a cost model
 // measured on MI355X (1080p uniform / heavy-tailed,
 // 4K, 50M @ 4K, with and without depth cuts):
-//   depth-first: global depth sort ~20 ps per splat, depth-order duplicate
-//                (wave-cooperative) ~4.5 ps per pair;
-//   bin-first:   index-order duplicate ~80 ps per unit of wave-max work W
+//   depth-first: global depth sort ~21 ps per splat, depth-order duplicate
+//                (wave-cooperative) ~4.7 ps per pair;
+//   bin-first:   index-order duplicate ~75 ps per unit of wave-max work W
 //                (the sum over waves of 64 splats of the largest pair count:
 //                the duplicate emits a wave's splats in lockstep, so a few
 //                huge splats dominate a heavy-tailed scene), plus the per-bin
@@ -364,8 +364,8 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int n
     const double Ps = cuts ? 0.3 * P : P;             // pairs through the per-bin sort
     const double f = cuts ? 0.0 : o.long_share;      // (front lists fit LDS)
     const double bins = nrows >= 0 ? (double)nrows * U.tiles_x : (double)T;
-    const double bin_ps = 80.0 * W + 6.0 * Ps * (1.0 - f) + 20.0 * Ps * f + 4900.0 * bins;
-    const double depth_ps = 20.0 * (double)m + 4.5 * P;
+    const double bin_ps = 75.0 * W + 6.0 * Ps * (1.0 - f) + 20.0 * Ps * f + 4900.0 * bins;
+    const double depth_ps = 21.0 * (double)m + 4.7 * P;
     return bin_ps < depth_ps;
 }
 
