@@ -164,6 +164,9 @@ def cpu_baseline(scene, view, proj, w, h, sh, threads, seconds, max_frames=50):
 
 
 KERNEL_NAME = {"preprocess": "preprocess_kernel", "composite": "composite_kernel"}
+# (depth-cut frames: the composite's pass 2 over the fallback lists is a separate, usually empty
+# launch; the dispatch-packet events and the PMC means are the front lists' pass)
+KERNEL_EXCLUDE = {"composite": ", 2>"}
 
 
 def pmc_passes(args):
@@ -200,7 +203,10 @@ def pmc_passes(args):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
                         for k, kn in KERNEL_NAME.items():
-                            if kn in row.get("Kernel_Name", "") and row.get("Counter_Name") in grp:
+                            name = row.get("Kernel_Name", "")
+                            if k in KERNEL_EXCLUDE and KERNEL_EXCLUDE[k] in name:
+                                continue
+                            if kn in name and row.get("Counter_Name") in grp:
                                 vals[(k, row["Counter_Name"])].append(float(row["Counter_Value"]))
             for (k, c), v in vals.items():
                 if v:
