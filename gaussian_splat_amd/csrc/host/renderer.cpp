@@ -490,6 +490,7 @@ gs_status frame_ownership(gs_handle* h, int tiles_y, hipStream_t st, Ownership* 
             GS_HIP(hipMemcpyAsync(h->rows_dev.ptr, rows.data(), rows.size() * 2, hipMemcpyHostToDevice, st));
         GS_HIP(hipStreamSynchronize(st));  // the host vectors are the staging copies
         h->owner_host = std::move(o);
+        h->cut_valid[0] = h->cut_valid[1] = false;  // (cuts of other bins)
         h->rows_host = std::move(rows);
     }
     out->dev = gs::RowOwnership{h->owner_dev.as<uint8_t>(), (uint32_t)h->rank};
@@ -601,7 +602,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     uint32_t cap = lp.cap;
     gs::PassCounts pc = lp.pc;
     uint32_t* const np = h->npairs.as<uint32_t>() + h->set;  // P on the device (this set's)
-    const bool cut_frame = h->cut_pending && h->cut_in && own.dev.owner == nullptr && carry_dkey;
+    const bool cut_frame = h->cut_pending && h->cut_in && carry_dkey;
     gs::SortFilter flt;  // front lists: the pairs at or ahead of their bin's cut
     if (cut_frame) {
         GS_HIP(h->kept.reserve(16));
@@ -705,6 +706,49 @@ hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
     return e != hipSuccess ? e : b.reserve(bytes);
 }
 
+// Depth cuts apply to this frame's composite rule and size:
+// tile / live50 rules, no fragment cap, the depth key above the bin id.
+bool cut_rule(const gs_handle* h, const gs::FrameUniforms& U) {
+    return h->opt.cap == 0 && (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) &&
+           list_key_bits(U) + gs::kDepthBits <= 32;
+}
+
+// Depth-cut state of the frame being enqueued on the current set
+// (h->cut_pending, cut_in, cut_out): the set's two cut tables (cutbuf), the
+// quadrant records, the open tiles' pixel states.  A set's tables hold cuts
+// only from a depth-cut frame at this frame size, composite rule and bin-row
+// ownership (frame_ownership drops them); any other frame on the set
+// invalidates them.  st, sp: the streams that may still use the buffers.
+gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, hipStream_t st, hipStream_t sp) {
+    const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
+    if (h->cut_w != U.width || h->cut_h != U.height || h->cut_mode != h->opt.mode) {
+        h->cut_valid[0] = h->cut_valid[1] = false;
+        h->cut_w = U.width;
+        h->cut_h = U.height;
+        h->cut_mode = h->opt.mode;
+    }
+    h->cut_pending = false;
+    h->cut_in = h->cut_out = nullptr;
+    if (!cut_frame) {
+        h->cut_valid[h->set] = false;
+        return GS_OK;
+    }
+    if (h->cut_bins < T) {
+        GS_HIP(hipStreamSynchronize(st));
+        GS_HIP(hipStreamSynchronize(sp));
+        GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
+        h->cut_bins = T;
+        h->cut_valid[0] = h->cut_valid[1] = false;
+    }
+    GS_HIP(h->qrec.reserve((size_t)T * gs::kQrecWords * 4));
+    GS_HIP(reserve_after(h->cstate, (size_t)U.width * U.height * 16, st));
+    h->cut_in = h->cut_valid[h->set] ? h->cut_table(h->set, 0) : nullptr;
+    h->cut_out = h->cut_table(h->set, 1);
+    h->cut_valid[h->set] = false;  // (true again once this frame's composite is queued)
+    h->cut_pending = true;
+    return GS_OK;
+}
+
 // Depth-cut frames, after the front lists' composite on sc:
 // the next cuts of this set (from the quadrant records), and the fallback
 // lists of the quadrants it left open: the frame's pairs (keys/vals, every
@@ -716,7 +760,7 @@ hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
 // returns at once (the usual case).  The front lists' buffers are free by
 // then (same stream).
 gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, const uint32_t* dkey,
-                   hipStream_t sc) {
+                   const gs::RowOwnership& own, hipStream_t sc) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     gs::CutFallback fb;
     if (h->cut_in) {
@@ -730,7 +774,8 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
         fb.kept = h->kept.as<uint32_t>() + 2 + h->set;
         fb.ranges = h->ranges.as<uint2>();
     }
-    GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, cut_margin(), sc, fb));
+    GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, (uint32_t)U.tiles_x, own, cut_margin(), sc,
+                                   fb));
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
 #ifdef GS_AB_NO_FALLBACK  // timing ablation build only: exact only while no quadrant is left open
     return GS_OK;
@@ -813,9 +858,8 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     const uint32_t* vals = nullptr;
     uint64_t P = 0;
     const bool mlab = h->opt.mode == GS_MODE_MLAB;
-    // depth cuts: decided before the preprocess (render_frame); only a frame
-    // of local splats can carry them
-    const bool cut_ok = h->cut_pending && !slab_t && !compact;
+    // depth cuts: decided before the lists (render_frame, render_received)
+    const bool cut_ok = h->cut_pending && !slab_t;
     h->cut_frame = false;
     if (mlab && (ca.cap > 0 || slab_t))
         return fail(GS_ERR_UNSUPPORTED, "MLAB mode has no fragment cap and no depth slabs");
@@ -889,7 +933,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             }
             // the next cuts of this set, then the fallback lists
             if (cutf) {
-                gs_status fs_ = cut_tail(h, U, c, dkey, sc);
+                gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc);
                 if (fs_ != GS_OK) return fs_;
             }
             mark(h, 7, sc);
@@ -950,7 +994,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 6, st);
             GS_HIP(handoff());
             GS_HIP(gs::launch_composite(c, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
-            gs_status fs_ = cut_tail(h, U, c, dkey, sc);
+            gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc);
             if (fs_ != GS_OK) return fs_;
             mark(h, 7, sc);
             return GS_OK;
@@ -1338,40 +1382,13 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     gs::PreFuse fuse;
     h->fused_prep = gs_handle::ListPrep{};
     h->order_pick = -1;
-    // A set's cut tables hold cuts only from a depth-cut frame at this frame
-    // size and composite rule; any other frame on the set invalidates them.
-    const bool cut_on = depth_cuts_on(h) && !band && h->world == 1 && h->opt.cap == 0 &&
-                        (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50);
-    if (h->cut_w != W || h->cut_h != H || h->cut_mode != h->opt.mode) {
-        h->cut_valid[0] = h->cut_valid[1] = false;
-        h->cut_w = W;
-        h->cut_h = H;
-        h->cut_mode = h->opt.mode;
-    }
+    const bool cut_on = depth_cuts_on(h) && !band && h->world == 1 && cut_rule(h, U);
     bool cut_frame = false;
-    h->cut_pending = false;
-    h->cut_in = h->cut_out = nullptr;
     if (!band && h->world == 1 && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
         const bool bf = bin_first_order(h, U, (uint32_t)h->n, -1, cut_on);
         h->order_pick = bf ? 1 : 0;
-        cut_frame = cut_on && list_key_bits(U) + gs::kDepthBits <= 32;  // (the depth key rides above the bin id)
-        if (cut_frame) {
-            // two tables per set (cutbuf), the per-tile open flags of the set,
-            // the open tiles' pixel states (composite stream)
-            if (h->cut_bins < T) {
-                GS_HIP(hipStreamSynchronize(st));
-                GS_HIP(hipStreamSynchronize(sp));
-                GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
-                h->cut_bins = T;
-                h->cut_valid[0] = h->cut_valid[1] = false;
-            }
-            GS_HIP(h->qrec.reserve((size_t)T * gs::kQrecWords * 4));
-            GS_HIP(reserve_after(h->cstate, (size_t)W * H * 16, st));
-            h->cut_in = h->cut_valid[h->set] ? h->cut_table(h->set, 0) : nullptr;
-            h->cut_out = h->cut_table(h->set, 1);
-            h->cut_valid[h->set] = false;  // (true again once this frame's composite is queued)
-            h->cut_pending = true;
-        }
+        cut_frame = cut_on;
+        if ((s = setup_cuts(h, U, cut_frame, st, sp)) != GS_OK) return s;
         if (bf) {
             if ((s = prepare_lists(h, (uint32_t)h->n, true, U, &h->fused_prep)) != GS_OK) return s;
             const uint32_t nb = (uint32_t)((h->n + gs::kScanItems - 1) / gs::kScanItems);
@@ -1391,7 +1408,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             h->ppart_dirty = true;  // (until its scan is queued)
         }
     }
-    if (!cut_frame) h->cut_valid[h->set] = false;
+    if (!cut_frame && (s = setup_cuts(h, U, false, st, sp)) != GS_OK) return s;
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
                                  kernel_event(h, 1), fetch_counter(h), fuse));
@@ -1677,10 +1694,17 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     GS_HIP(h->rrlo.reserve(mm * 4));
     GS_HIP(h->rrhi.reserve(mm * 4));
     float4* rv = static_cast<float4*>(recv);
-    h->order_pick = -1;  // (decided in bin_sort_composite for received records)
     h->fused_prep.ok = false;
+    // depth cuts of the owned bins: the cuts and the quadrant
+    // records are indexed by global bin, the pixel states by global pixel;
+    // the binning order is picked for them
+    Ownership own;
+    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+    const bool cut_on = !slab_t && m > 0 && depth_cuts_on(h) && cut_rule(h, U);
+    if ((s = setup_cuts(h, U, cut_on, st, st)) != GS_OK) return s;
+    h->order_pick = h->opt.mode == GS_MODE_MLAB ? -1 : bin_first_order(h, U, (uint32_t)m, own.nrows, cut_on) ? 1 : 0;
     mark(h, 8, st);
-    GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
+    GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, U.cell_mask != 0, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                   h->rrhi.as<uint32_t>(), st));
     if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
                                 h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, slab_t ? 0 : 1,

@@ -486,8 +486,8 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
-    if (a.pass) {  // depth-cut frames: tile / live50 rules, no cap, no depth slabs, whole frame
-        if (cap || a.slab || a.rows || a.compact || (!a.out && !a.out_bgra8) || !a.qrec || !a.state ||
+    if (a.pass) {  // depth-cut frames: tile / live50 rules, no cap, no depth slabs (owned rows allowed)
+        if (cap || a.slab || (!a.out && !a.out_bgra8) || !a.qrec || !a.state ||
             (mode != 0 && mode != 1) || a.pass > 2 || (a.pass == 1 && !a.open_q_count))
             return hipErrorInvalidValue;
         if (a.pass == 1)
@@ -509,7 +509,8 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
 __global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __restrict__ qrec,
                                                            const uint32_t* __restrict__ vals,
                                                            const uint32_t* __restrict__ dkey, uint32_t* __restrict__ cut,
-                                                           uint32_t nbins, uint32_t margin, const CutFallback fb) {
+                                                           uint32_t nbins, uint32_t tiles_x, const RowOwnership own,
+                                                           uint32_t margin, const CutFallback fb) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     const bool any_open = fb.cut_in && *fb.open != 0ull;
     if (fb.cut_in && b == 0) {
@@ -517,6 +518,14 @@ __global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __res
         *fb.kept = 0u;
     }
     if (b >= nbins) return;
+    if (!owns_bin_row(b / tiles_x, own)) {  // (another rank's bin: no record, no pairs)
+        cut[b] = 0u;
+        if (fb.cut_in) {
+            fb.table[b] = 0xFFFFFFFFu;
+            if (any_open) fb.ranges[b] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        }
+        return;
+    }
     const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);  // (the bin's 16 positions, 16 flags)
     uint32_t p = 0u, open = 0u;
 #pragma unroll
@@ -537,11 +546,14 @@ __global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __res
 }
 
 hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
-                               uint32_t nbins, uint32_t margin, hipStream_t st, const CutFallback& fb) {
+                               uint32_t nbins, uint32_t tiles_x, const RowOwnership& own, uint32_t margin,
+                               hipStream_t st, const CutFallback& fb) {
     if (nbins == 0) return hipSuccess;
+    if (tiles_x == 0) return hipErrorInvalidValue;
     if (fb.cut_in && (!fb.open || !fb.npairs || !fb.table || !fb.n || !fb.kept || !fb.ranges))
         return hipErrorInvalidValue;
-    cut_finalize_kernel<<<(nbins + 255) / 256, 256, 0, st>>>(qrec, vals, dkey, cut_out, nbins, margin, fb);
+    cut_finalize_kernel<<<(nbins + 255) / 256, 256, 0, st>>>(qrec, vals, dkey, cut_out, nbins, tiles_x, own, margin,
+                                                             fb);
     return hipGetLastError();
 }
 

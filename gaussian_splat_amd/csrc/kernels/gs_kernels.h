@@ -233,7 +233,9 @@ hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hi
 // quadrant (its pairs behind the cut are sorted again), else ~0 (none);
 // *fb.n = *fb.npairs when a quadrant is open, else 0, and *fb.kept = 0 (so
 // every fallback kernel returns at once when none is); the bin ranges are
-// cleared for the fallback sort when one is open.
+// cleared for the fallback sort when one is open.  Bins in rows another
+// rank owns (own.owner, rows of tiles_x bins) get cut 0 and no fallback:
+// their quadrant records were never written by this rank's composite.
 struct CutFallback {
     const uint32_t* cut_in = nullptr;  // null: no fallback (the lists were whole)
     const unsigned long long* open = nullptr;
@@ -244,7 +246,8 @@ struct CutFallback {
     uint2* ranges = nullptr;
 };
 hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
-                               uint32_t nbins, uint32_t margin, hipStream_t st, const CutFallback& fb);
+                               uint32_t nbins, uint32_t tiles_x, const RowOwnership& own, uint32_t margin,
+                               hipStream_t st, const CutFallback& fb);
 // Per-pixel cap thresholds from INDEX-ordered bin lists (a.vals / a.ranges):
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).
@@ -282,8 +285,9 @@ hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32
 hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
                              int world, const uint32_t* counts, const uint32_t* dest_total,
                              uint32_t nblocks, float4* send, hipStream_t st);
-// Unpack dkey and packed rect of every received exchange record.
-hipError_t launch_recv_unpack(float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+// Unpack dkey and packed rect of every received exchange record; masked
+// frames (FrameUniforms::cell_mask) get their exclusion masks recomputed.
+hipError_t launch_recv_unpack(float4* recv, uint32_t m, bool masked, uint32_t* dkey, uint32_t* rect_lo,
                               uint32_t* rect_hi, hipStream_t st);
 // dst[i] += src[i] for n4 float4s.
 hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStream_t st);

@@ -11,14 +11,16 @@
 #include <algorithm>
 
 #include "gs_kernels.h"
+#include "gs_masks.h"
 #include "gs_wave.h"
 
 namespace gs {
 
 // 48-B exchange record = the 48-B record with its rect words repacked as
 // x (12 bits) | y (12 bits) << 12 | 8 bits of the 15-bit depth key << 24
-// (low byte in the lo word, high 7 bits in the hi word).  Frames up to
-// kXMaxDim x kXMaxDim (4K UHD included).
+// (low byte in the lo word, high 7 bits in the hi word); the exclusion masks
+// are dropped and recomputed by the receiver (recv_unpack_kernel).  Frames
+// up to kXMaxDim x kXMaxDim (4K UHD included).
 __device__ __forceinline__ uint32_t xrect_pack(uint32_t xy, uint32_t key8) {
     return (xy & 0xFFFu) | (((xy >> 16) & 0xFFFu) << 12) | (key8 << 24);
 }
@@ -100,14 +102,38 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
                                                          uint32_t nblocks, float4* __restrict__ send) {
     __shared__ uint32_t wc[kShWaves][kMaxWorld];   // per-wave counts -> per-wave offsets
     __shared__ uint32_t base_d[kMaxWorld];         // this block's start in destination d
+    __shared__ float4 stg[kShWaves][3 * 64];       // per wave: one destination's run of a round
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t base = blockIdx.x * kShardItems + wave * kShWaveItems;
-    uint32_t cnt = 0;
+    // Every round's records are loaded up front, before the block's offsets
+    // (one memory round trip per wave, not one per round and destination).
+    // The stores go through a per-wave LDS stage: a destination's run of a
+    // round (its records are consecutive in the send buffer) is written by
+    // consecutive lanes, 16 B each, so every store instruction covers whole
+    // cache lines (lane-per-record stores at a 48-B stride left each
+    // instruction a third of every line it touched).
+    float4 r0[kShIpt], r1[kShIpt], r2[kShIpt];
+    uint32_t mk[kShIpt];
+#pragma unroll
     for (int k = 0; k < kShIpt; ++k) {
-        uint32_t i = base + k * 64 + lane;
-        uint32_t m = i < n ? dest_mask[i] : 0u;
+        const uint32_t i = base + k * 64 + lane;
+        mk[k] = i < n ? dest_mask[i] : 0u;
+        r0[k] = r1[k] = r2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mk[k]) {
+            const float4* src = rec + kRecFloat4 * (size_t)i;
+            r0[k] = src[0];
+            r1[k] = src[1];
+            const float4 c = src[2];
+            const uint32_t dk = dkey[i];
+            r2[k] = make_float4(c.x, c.y, __uint_as_float(xrect_pack(__float_as_uint(c.z), dk & 0xFFu)),
+                                __uint_as_float(xrect_pack(__float_as_uint(c.w), dk >> 8)));
+        }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kShIpt; ++k) {
         for (int d = 0; d < world; ++d) {
-            uint64_t b = __ballot((m >> d) & 1u);
+            uint64_t b = __ballot((mk[k] >> d) & 1u);
             if (lane == (uint32_t)d) cnt += (uint32_t)__popcll(b);
         }
     }
@@ -125,33 +151,41 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
         base_d[d] = pre + counts[(size_t)d * nblocks + blockIdx.x];
     }
     __syncthreads();
+    // lane d < world keeps this wave's next slot in destination d
+    uint32_t next = lane < (uint32_t)world ? base_d[lane] + wc[wave][lane] : 0u;
+    float4* const stage = stg[wave];
+#pragma unroll
     for (int k = 0; k < kShIpt; ++k) {
-        uint32_t i = base + k * 64 + lane;
-        uint32_t m = i < n ? dest_mask[i] : 0u;
+        const uint32_t m = mk[k];
         for (int d = 0; d < world; ++d) {
-            bool bit = (m >> d) & 1u;
-            uint64_t b = __ballot(bit);
+            const bool bit = (m >> d) & 1u;
+            const uint64_t b = __ballot(bit);
             if (b == 0) continue;
-            uint32_t run = wc[wave][d];
+            const uint32_t c3 = 3u * (uint32_t)__popcll(b);
             if (bit) {
-                uint32_t pos = base_d[d] + run + mbcnt(b);
-                const float4* src = rec + kRecFloat4 * (size_t)i;
-                float4* dst = send + (size_t)kXRecFloat4 * pos;
-                const float4 c = src[2];
-                const uint32_t lo = __float_as_uint(c.z), hi = __float_as_uint(c.w), dk = dkey[i];
-                dst[0] = src[0];
-                dst[1] = src[1];
-                dst[2] = make_float4(c.x, c.y, __uint_as_float(xrect_pack(lo, dk & 0xFFu)),
-                                     __uint_as_float(xrect_pack(hi, dk >> 8)));
+                const uint32_t j = 3u * mbcnt(b);
+                stage[j] = r0[k];
+                stage[j + 1] = r1[k];
+                stage[j + 2] = r2[k];
             }
-            if (lane == 0) wc[wave][d] = run + (uint32_t)__popcll(b);
+            wave_lds_sync();
+            const uint32_t pos = __shfl(next, d, 64);
+            float4* dst = send + (size_t)kXRecFloat4 * pos;
+            for (uint32_t q = lane; q < c3; q += 64) dst[q] = stage[q];
+            wave_lds_sync();  // (the stage is refilled by the next run)
+            if (lane == (uint32_t)d) next += c3 / 3u;
         }
     }
 }
 
 // Decode the received records in place: the packed rect words become the
 // standard (x | y << 16) ones, so the composite reads them like local records.
-__global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ recv, uint32_t m,
+// In masked frames (FrameUniforms::cell_mask) the exclusion masks the 48-B
+// exchange record has no room for are computed again from the record's own
+// centre, axes and rect (gs_masks.h, the preprocess's function of the same
+// fields): the cell mask into the record, the bin mask into the binning rect,
+// so a rank emits the pairs and culls the cells of the single-GPU frame.
+__global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ recv, uint32_t m, bool masked,
                                                           uint32_t* __restrict__ dkey, uint32_t* __restrict__ rect_lo,
                                                           uint32_t* __restrict__ rect_hi) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -161,10 +195,15 @@ __global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ r
     const uint32_t plo = __float_as_uint(c.z), phi = __float_as_uint(c.w);
     const uint32_t lo = xrect_unpack(plo), hi = xrect_unpack(phi);
     dkey[i] = (plo >> 24) | ((phi >> 24) << 8);
-    rect_lo[i] = lo;
-    rect_hi[i] = hi;
-    c.z = __uint_as_float(lo);
-    c.w = __uint_as_float(hi);
+    RectMasks rm{0u, 0u};
+    if (masked) {
+        const float4 a = r[0], b = r[1];
+        rm = rect_masks(a.x, a.y, a.z, a.w, b.x, b.y, lo & 0xFFFFu, lo >> 16, hi & 0xFFFFu, hi >> 16);
+    }
+    rect_lo[i] = rect_with_mask(lo, rm.bin & 0xFu, (rm.bin >> 4) & 0xFu);
+    rect_hi[i] = rect_with_mask(hi, (rm.bin >> 8) & 0xFu, rm.bin >> 12);
+    c.z = __uint_as_float(rect_with_mask(lo, rm.cell & 0xFu, (rm.cell >> 4) & 0xFu));
+    c.w = __uint_as_float(rect_with_mask(hi, (rm.cell >> 8) & 0xFu, rm.cell >> 12));
     r[2] = c;
 }
 
@@ -238,10 +277,10 @@ hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_recv_unpack(float4* recv, uint32_t m, uint32_t* dkey, uint32_t* rect_lo,
+hipError_t launch_recv_unpack(float4* recv, uint32_t m, bool masked, uint32_t* dkey, uint32_t* rect_lo,
                               uint32_t* rect_hi, hipStream_t st) {
     if (m == 0) return hipSuccess;
-    recv_unpack_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, dkey, rect_lo, rect_hi);
+    recv_unpack_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, masked, dkey, rect_lo, rect_hi);
     return hipGetLastError();
 }
 

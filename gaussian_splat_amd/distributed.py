@@ -516,29 +516,52 @@ def render_virtual_slabs(scene: Scene, world: int, view, proj, width: int, heigh
     return frame.cpu().numpy()
 
 
+class VirtualShards:
+    """All `world` ranks of the row scheme in one process on one GPU, the
+    exchange by slicing: the same kernels and record protocol as the
+    multi-process path, frame after frame (so a rank's depth cuts carry over,
+    DESIGN.md §6).  `options` as for InstancedSplatRenderer (crop off)."""
+
+    def __init__(self, scene: Scene, world: int, options: Options, device: int = 0, owner=None):
+        self.world, self.owner = world, owner
+        self.backends = []
+        for r in range(world):
+            b, e = shard_bounds(scene.n, world, r)
+            self.backends.append(HipShardBackend(scene.subset(slice(b, e)), r, world, b, options, device, owner))
+
+    def set_rows(self, owner):
+        """A new bin-row owner table on every rank (gs_shard_set_rows)."""
+        o = np.ascontiguousarray(owner, np.uint8)
+        for be in self.backends:
+            be.owner = o
+            check(lib().gs_shard_set_rows(be.r._h, o.ctypes.data, len(o)), "gs_shard_set_rows")
+        self.owner = o
+
+    def render(self, view, proj, width: int, height: int):
+        """The assembled frame (device tensor, height x width x 4)."""
+        import torch
+
+        sends = [be.project(view, proj, width, height) for be in self.backends]
+        xb = self.backends[0].xbytes
+        bands = []
+        for dst, be in enumerate(self.backends):
+            parts = []
+            for src in range(self.world):
+                buf, counts = sends[src]
+                off = sum(counts[:dst]) * xb
+                parts.append(buf[off: off + counts[dst] * xb])
+            recv = torch.cat(parts) if parts else be.empty(0)
+            nrec = recv.numel() // xb
+            bands.append(be.render(recv if recv.numel() else be.empty(xb), nrec, width, height))
+        return assemble(bands, width, height, self.world, self.owner)
+
+
 def render_virtual_shards(scene: Scene, world: int, view, proj, width: int, height: int, sh_degree: int = 0,
                           mode: str = "tile", device: int = 0, cap: int = 0, owner=None) -> np.ndarray:
-    """All `world` ranks in one process on one GPU, exchange by slicing —
-    the same kernels and record protocol as the multi-process path."""
+    """One frame of VirtualShards (new ranks, so no depth cuts carried)."""
     import torch
 
-    opts = Options(mode=mode, sh_degree=sh_degree, crop=False, cap=cap)
-    backends = []
-    for r in range(world):
-        b, e = shard_bounds(scene.n, world, r)
-        backends.append(HipShardBackend(scene.subset(slice(b, e)), r, world, b, opts, device, owner))
-    sends = [be.project(view, proj, width, height) for be in backends]
-    xb = backends[0].xbytes
-    bands = []
-    for dst in range(world):
-        parts = []
-        for src in range(world):
-            buf, counts = sends[src]
-            off = sum(counts[:dst]) * xb
-            parts.append(buf[off: off + counts[dst] * xb])
-        recv = torch.cat(parts) if parts else backends[dst].empty(0)
-        nrec = recv.numel() // xb
-        bands.append(backends[dst].render(recv if recv.numel() else backends[dst].empty(xb), nrec, width, height))
-    frame = assemble(bands, width, height, world, owner)
+    vs = VirtualShards(scene, world, Options(mode=mode, sh_degree=sh_degree, crop=False, cap=cap), device, owner)
+    frame = vs.render(view, proj, width, height)
     torch.cuda.synchronize()
     return frame.cpu().numpy()

@@ -212,3 +212,42 @@ def test_depth_cuts_margin_extremes(built, margin):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout + p.stderr
     print(margin, p.stdout.strip())
+
+
+@pytest.mark.parametrize("world,w,h,binning,path,table", [
+    (2, 640, 360, "bin_first", "orbit", None),
+    (3, 640, 360, "depth_first", "jump", None),
+    (4, 960, 540, "default", "orbit", "interleaved"),
+    (2, 640, 360, "bin_first", "jump", "switch"),   # the owner table changes mid-path: cuts start over
+    (3, 100, 40, "bin_first", "orbit", None),       # two bin rows, three ranks: one owns none
+    (2, 960, 540, "depth_first", "still", None),    # dense, still: the cuts save pairs on every rank
+    (3, 960, 540, "bin_first", "still", "interleaved"),
+])
+def test_depth_cuts_virtual_ranks(built, world, w, h, binning, path, table):
+    """Rank renders of the row scheme carry the depth cuts of
+    their owned bins from frame to frame (quadrant records and cuts indexed by
+    global bin, pixel states by global pixel; another rank's bins get no
+    fallback): every assembled frame is bit-identical to the single-GPU
+    whole-list frame."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd.distributed import VirtualShards
+    dense = path == "still"  # (the bench scene's coverage per pixel, as in the still-camera test above)
+    sc = _scene(1_500_000 if dense else 300000, 41 + world, 0, w / h, scale=2.0 if dense else 1.3)
+    ref = InstancedSplatRenderer(sc, Options(crop=False, depth_split=False))
+    ref.initialize(0)
+    R = (h + 31) // 32
+    inter = np.array([r % world for r in range(R)], np.uint8)
+    vs = VirtualShards(sc, world, Options(crop=False, depth_split=True, binning=binning), 0,
+                       inter if table == "interleaved" else None)
+    saved = [0] * world
+    for k, (V, P) in enumerate(_path(w, h, path, 4 if dense else 6)):
+        if table == "switch" and k == 3:
+            vs.set_rows(inter)
+        a = vs.render(V, P, w, h).cpu().numpy()
+        assert _bits(a, ref.render_host(V, P, w, h)) == 0, k
+        for be in vs.backends:
+            st = be.r.last_stats()
+            assert (st["two_slab"] == 1 or st["pairs"] == 0) and st["pairs_sorted"] <= st["pairs"], (k, be.rank, st)
+            saved[be.rank] = st["pairs"] - st["pairs_sorted"]
+    if dense:  # (the last frame)
+        assert min(saved) > 0, saved
