@@ -347,33 +347,42 @@ std::vector<Xfer> exchange_plan(const std::vector<std::vector<int64_t>>& counts)
 gs_status exchange(gs_group* g, std::vector<int64_t>* nrec) {
     const int W = g->world;
     const int64_t xb = gs_exchange_record_bytes();
+    // the exchange regions (gsplat.h): each moves on its own, region k of a
+    // buffer of n records starting at n x (the earlier regions' bytes)
+    int32_t rb[GS_XREGIONS];
+    const int nreg = gs_exchange_regions(rb);
     std::vector<std::vector<int64_t>> counts((size_t)W);
+    std::vector<int64_t> sent((size_t)W, 0);
     nrec->assign((size_t)W, 0);
     for (int s = 0; s < W; ++s) {
         counts[(size_t)s] = g->r[(size_t)s].counts;
-        for (int d = 0; d < W; ++d) (*nrec)[(size_t)d] += counts[(size_t)s][(size_t)d];
+        for (int d = 0; d < W; ++d) {
+            (*nrec)[(size_t)d] += counts[(size_t)s][(size_t)d];
+            sent[(size_t)s] += counts[(size_t)s][(size_t)d];
+        }
     }
     for (int d = 0; d < W; ++d) GG_HIP(g->r[(size_t)d].recv.reserve(g->r[(size_t)d].dev, (size_t)std::max<int64_t>((*nrec)[(size_t)d], 1) * xb));
     const std::vector<Xfer> plan = exchange_plan(counts);
-    if (g->transport == GS_TRANSPORT_RCCL) {
-        GG_NCCL(g_rccl.group_start());
-        for (const Xfer& x : plan) {  // each transfer: a send on src's communicator, the matching recv on dst's
+    if (g->transport == GS_TRANSPORT_RCCL) GG_NCCL(g_rccl.group_start());
+    int64_t pre = 0;  // bytes per record of the regions before region k
+    for (int k = 0; k < nreg; pre += rb[k], ++k) {
+        const int64_t b = rb[k];
+        for (const Xfer& x : plan) {
             Rank &ks = g->r[(size_t)x.src], &kd = g->r[(size_t)x.dst];
-            GG_NCCL(g_rccl.send(ks.send.as<char>() + x.soff * xb, (size_t)(x.n * xb), ncclUint8, x.dst,
-                                g->comms[(size_t)x.src], ks.st));
-            GG_NCCL(g_rccl.recv(kd.recv.as<char>() + x.roff * xb, (size_t)(x.n * xb), ncclUint8, x.src,
-                                g->comms[(size_t)x.dst], kd.st));
+            char* src = ks.send.as<char>() + pre * sent[(size_t)x.src] + x.soff * b;
+            char* dst = kd.recv.as<char>() + pre * (*nrec)[(size_t)x.dst] + x.roff * b;
+            if (g->transport == GS_TRANSPORT_RCCL) {
+                // each transfer: a send on src's communicator, the matching recv on dst's
+                GG_NCCL(g_rccl.send(src, (size_t)(x.n * b), ncclUint8, x.dst, g->comms[(size_t)x.src], ks.st));
+                GG_NCCL(g_rccl.recv(dst, (size_t)(x.n * b), ncclUint8, x.src, g->comms[(size_t)x.dst], kd.st));
+            } else {
+                GG_HIP(hipSetDevice(kd.dev));
+                GG_HIP(hipStreamWaitEvent(kd.st, ks.ev_ready, 0));
+                GG_HIP(hipMemcpyPeerAsync(dst, kd.dev, src, ks.dev, (size_t)(x.n * b), kd.st));
+            }
         }
-        GG_NCCL(g_rccl.group_end());
-        return GS_OK;
     }
-    for (const Xfer& x : plan) {
-        Rank &ks = g->r[(size_t)x.src], &kd = g->r[(size_t)x.dst];
-        GG_HIP(hipSetDevice(kd.dev));
-        GG_HIP(hipStreamWaitEvent(kd.st, ks.ev_ready, 0));
-        GG_HIP(hipMemcpyPeerAsync(kd.recv.as<char>() + x.roff * xb, kd.dev, ks.send.as<char>() + x.soff * xb, ks.dev,
-                                  (size_t)(x.n * xb), kd.st));
-    }
+    if (g->transport == GS_TRANSPORT_RCCL) GG_NCCL(g_rccl.group_end());
     return GS_OK;
 }
 

@@ -84,7 +84,7 @@ struct gs_handle {
     // per-frame scratch
     DevBuf rec, dkey, rlo, rhi, offsets, partials, keys, vals, tkeys, tvals, sort_scratch, ranges, fb, thr;
     DevBuf dsk, dso, dsl, dsh, dtk, dto, dtl, dth;  // depth sort: keys, order, rect lo/hi (+ ping-pong)
-    DevBuf xmask, xcounts, xtotal, rdkey, rrlo, rrhi;  // multi-GPU exchange
+    DevBuf xmask, xcounts, xtotal;  // multi-GPU exchange
     // depth-slab frames: full-frame ownership; the colour pass
     // (gs_slab_composite) reuses the bin lists of the transmittance pass
     bool slab_frame = false;
@@ -199,7 +199,7 @@ struct gs_handle {
     ~gs_handle() {
         for (DevBuf* b : {&p0, &p1, &p2, &p3, &sh4, &sh1, &rec, &dkey, &rlo, &rhi, &offsets, &partials, &keys,
                           &vals, &tkeys, &tvals, &sort_scratch, &ranges, &fb, &thr, &dsk, &dso, &dsl, &dsh, &dtk, &dto,
-                          &dtl, &dth, &xmask, &xcounts, &xtotal, &rdkey, &rrlo, &rrhi, &owner_dev, &rows_dev, &alt_rec,
+                          &dtl, &dth, &xmask, &xcounts, &xtotal, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &alt_rlo,
                           &alt_rhi, &alt_qrec, &alt_fkeys, &alt_fvals, &seg_sample, &npairs, &fetch, &qrec, &cutbuf,
                           &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart})
@@ -1587,7 +1587,16 @@ gs_status gs_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys
 }
 
 // ---- multi-GPU: tile-row ownership ---------------------------
-int32_t gs_exchange_record_bytes(void) { return gs::kXRecFloat4 * 16; }
+int32_t gs_exchange_record_bytes(void) { return gs::kXRecFloat4 * 16 + gs::kXSideWords * 4; }
+
+int32_t gs_exchange_regions(int32_t* bytes_per_record) {
+    static_assert(GS_XREGIONS == 1 + gs::kXSideWords, "gsplat.h");
+    if (bytes_per_record) {
+        bytes_per_record[0] = gs::kXRecFloat4 * 16;
+        for (int k = 1; k <= gs::kXSideWords; ++k) bytes_per_record[k] = 4;
+    }
+    return GS_XREGIONS;
+}
 
 gs_status gs_shard_configure(gs_handle* h, int32_t rank, int32_t world, int64_t index_base) {
     if (!h || world < 1 || world > gs::kMaxWorld || rank < 0 || rank >= world || index_base < 0 ||
@@ -1619,8 +1628,6 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
     if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "shard frame: bad arguments");
-    if (W > gs::kXMaxDim || H > gs::kXMaxDim)
-        return fail(GS_ERR_UNSUPPORTED, "multi-GPU frames are limited to 4096 x 4096 (packed exchange record)");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     *U = make_uniforms(view, proj, W, H);
     GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));  // a pipelined composite may still read the set
@@ -1652,7 +1659,8 @@ gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, voi
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
     auto pack = [&]() -> hipError_t {
-        return gs::launch_shard_pack(h->rec.as<float4>(), h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
+        return gs::launch_shard_pack(h->rec.as<float4>(), h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(),
+                                     h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
                                      h->xcounts.as<uint32_t>(), h->xtotal.as<uint32_t>(), nb,
                                      static_cast<float4*>(send), st);
     };
@@ -1682,18 +1690,18 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
                           hipStream_t st) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
-    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !(out_rgba || slab_t) || W <= 0 || H <= 0 ||
-        W > gs::kXMaxDim || H > gs::kXMaxDim)
+    if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !(out_rgba || slab_t) || W <= 0 || H <= 0)
         return fail(GS_ERR_INVALID_ARG, "shard render: bad arguments");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     const gs::FrameUniforms U = make_uniforms(I, I, W, H);
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
-    const size_t mm = (size_t)std::max<int64_t>(m, 1);
-    GS_HIP(h->rdkey.reserve(mm * 4));
-    GS_HIP(h->rrlo.reserve(mm * 4));
-    GS_HIP(h->rrhi.reserve(mm * 4));
+    // the exchange regions (gs_exchange_regions): m records, then their
+    // binning rect lo / hi words and depth keys (SoA, source-rank order)
     float4* rv = static_cast<float4*>(recv);
+    const uint32_t* rlo = reinterpret_cast<const uint32_t*>(rv + (size_t)gs::kXRecFloat4 * m);
+    const uint32_t* rhi = rlo + m;
+    const uint32_t* rkey = rhi + m;
     h->fused_prep.ok = false;
     // depth cuts of the owned bins: the cuts and the quadrant
     // records are indexed by global bin, the pixel states by global pixel;
@@ -1704,10 +1712,7 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     if ((s = setup_cuts(h, U, cut_on, st, st)) != GS_OK) return s;
     h->order_pick = h->opt.mode == GS_MODE_MLAB ? -1 : bin_first_order(h, U, (uint32_t)m, own.nrows, cut_on) ? 1 : 0;
     mark(h, 8, st);
-    GS_HIP(gs::launch_recv_unpack(rv, (uint32_t)m, U.cell_mask != 0, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
-                                  h->rrhi.as<uint32_t>(), st));
-    if ((s = bin_sort_composite(h, (uint32_t)m, h->rdkey.as<uint32_t>(), h->rrlo.as<uint32_t>(),
-                                h->rrhi.as<uint32_t>(), rv, gs::kXRecFloat4, U, slab_t ? 0 : 1,
+    if ((s = bin_sort_composite(h, (uint32_t)m, rkey, rlo, rhi, rv, gs::kXRecFloat4, U, slab_t ? 0 : 1,
                                 reinterpret_cast<float4*>(out_rgba), nullptr, st, slab_t)) != GS_OK)
         return s;
     // stage times span both calls: preprocess (project) ... composite; the

@@ -254,8 +254,8 @@ hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 
 // ---- shard.hip (multi-GPU tile-row ownership / depth slabs) ---------------
-constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the record, depth key packed into the rect words
-constexpr int kXMaxDim = 4096;  // frame limit of the packed rect (12-bit coordinates)
+constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the projection's record (its first 48 B)
+constexpr int kXSideWords = 3;  // + binning rect lo, hi and depth key per record (gs_exchange_regions)
 constexpr int kMaxWorld = 32;
 constexpr int kSlabKeys = 1 << kDepthBits;  // 15-bit depth keys
 constexpr int kSlabBinShift = 4;            // slab histogram: 2048 bins of 16 keys
@@ -281,14 +281,12 @@ hipError_t launch_slab_histogram(const uint32_t* dkey, const uint32_t* rect_lo, 
                                  bool masked, unsigned long long* hist, hipStream_t st);
 // Exclusive scan of each destination row; dest_total[world].
 hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32_t* dest_total, hipStream_t st);
-// Pack exchange records grouped by destination, splat-index order inside.
-hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
-                             int world, const uint32_t* counts, const uint32_t* dest_total,
-                             uint32_t nblocks, float4* send, hipStream_t st);
-// Unpack dkey and packed rect of every received exchange record; masked
-// frames (FrameUniforms::cell_mask) get their exclusion masks recomputed.
-hipError_t launch_recv_unpack(float4* recv, uint32_t m, bool masked, uint32_t* dkey, uint32_t* rect_lo,
-                              uint32_t* rect_hi, hipStream_t st);
+// Pack the exchange regions (records, then rect lo / hi and depth-key words
+// of all T = sum(dest_total) records) grouped by destination, splat-index
+// order inside.
+hipError_t launch_shard_pack(const float4* rec, const uint32_t* rlo, const uint32_t* rhi, const uint32_t* dkey,
+                             const uint32_t* dest_mask, uint32_t n, int world, const uint32_t* counts,
+                             const uint32_t* dest_total, uint32_t nblocks, float4* send, hipStream_t st);
 // dst[i] += src[i] for n4 float4s.
 hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStream_t st);
 }  // namespace gs

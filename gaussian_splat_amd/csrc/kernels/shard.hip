@@ -11,21 +11,16 @@
 #include <algorithm>
 
 #include "gs_kernels.h"
-#include "gs_masks.h"
 #include "gs_wave.h"
 
 namespace gs {
 
-// 48-B exchange record = the 48-B record with its rect words repacked as
-// x (12 bits) | y (12 bits) << 12 | 8 bits of the 15-bit depth key << 24
-// (low byte in the lo word, high 7 bits in the hi word); the exclusion masks
-// are dropped and recomputed by the receiver (recv_unpack_kernel).  Frames
-// up to kXMaxDim x kXMaxDim (4K UHD included).
-__device__ __forceinline__ uint32_t xrect_pack(uint32_t xy, uint32_t key8) {
-    return (xy & 0xFFFu) | (((xy >> 16) & 0xFFFu) << 12) | (key8 << 24);
-}
-__device__ __forceinline__ uint32_t xrect_unpack(uint32_t p) { return (p & 0xFFFu) | (((p >> 12) & 0xFFFu) << 16); }
-
+// Exchange buffers (gsplat.h, gs_exchange_regions): n records as four
+// regions, each grouped by destination on the send side: the 48-B records as
+// the projection wrote them (cell masks included), then the binning rect
+// words lo, hi (bin masks included) and the depth keys, 4 B each.  An
+// all-to-all per region leaves the receiver its records and three SoA arrays
+// in source-rank order: the rank bins and sorts straight from them.
 // kShardItems splats per 256-lane workgroup: 4 rounds of 64 per wave, so a
 // rank's shard spreads over many workgroups (750k splats: 733; blocks of
 // 4096 left 183 workgroups on 256 CUs, pack 75 us)
@@ -95,6 +90,8 @@ __global__ __launch_bounds__(256) void rows_scan_kernel(uint32_t* __restrict__ c
 }
 
 __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restrict__ rec,
+                                                         const uint32_t* __restrict__ rlo,
+                                                         const uint32_t* __restrict__ rhi,
                                                          const uint32_t* __restrict__ dkey,
                                                          const uint32_t* __restrict__ dest_mask, uint32_t n,
                                                          int world, const uint32_t* __restrict__ counts,
@@ -103,30 +100,32 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
     __shared__ uint32_t wc[kShWaves][kMaxWorld];   // per-wave counts -> per-wave offsets
     __shared__ uint32_t base_d[kMaxWorld];         // this block's start in destination d
     __shared__ float4 stg[kShWaves][3 * 64];       // per wave: one destination's run of a round
+    __shared__ uint32_t sside[kShWaves][3][kShWaveItems];  // per wave: its side words for one destination
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t base = blockIdx.x * kShardItems + wave * kShWaveItems;
     // Every round's records are loaded up front, before the block's offsets
     // (one memory round trip per wave, not one per round and destination).
-    // The stores go through a per-wave LDS stage: a destination's run of a
-    // round (its records are consecutive in the send buffer) is written by
-    // consecutive lanes, 16 B each, so every store instruction covers whole
-    // cache lines (lane-per-record stores at a 48-B stride left each
-    // instruction a third of every line it touched).
+    // The records go through a per-wave LDS stage: a destination's run of a
+    // round (consecutive in the send buffer) is written by consecutive lanes,
+    // 16 B each, so every store instruction covers whole cache lines (lane-
+    // per-record stores at a 48-B stride left each a third of every line:
+    // 257 -> 165 us for a 6.25M-splat shard at 8 ranks).
     float4 r0[kShIpt], r1[kShIpt], r2[kShIpt];
-    uint32_t mk[kShIpt];
+    uint32_t mk[kShIpt], lo[kShIpt], hi[kShIpt], dk[kShIpt];
 #pragma unroll
     for (int k = 0; k < kShIpt; ++k) {
         const uint32_t i = base + k * 64 + lane;
         mk[k] = i < n ? dest_mask[i] : 0u;
         r0[k] = r1[k] = r2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        lo[k] = hi[k] = dk[k] = 0u;
         if (mk[k]) {
             const float4* src = rec + kRecFloat4 * (size_t)i;
             r0[k] = src[0];
             r1[k] = src[1];
-            const float4 c = src[2];
-            const uint32_t dk = dkey[i];
-            r2[k] = make_float4(c.x, c.y, __uint_as_float(xrect_pack(__float_as_uint(c.z), dk & 0xFFu)),
-                                __uint_as_float(xrect_pack(__float_as_uint(c.w), dk >> 8)));
+            r2[k] = src[2];
+            lo[k] = rlo[i];
+            hi[k] = rhi[i];
+            dk[k] = dkey[i];
         }
     }
     uint32_t cnt = 0;
@@ -151,60 +150,47 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const float4* __restric
         base_d[d] = pre + counts[(size_t)d * nblocks + blockIdx.x];
     }
     __syncthreads();
-    // lane d < world keeps this wave's next slot in destination d
-    uint32_t next = lane < (uint32_t)world ? base_d[lane] + wc[wave][lane] : 0u;
+    // the side regions follow all T records (T = every destination's total)
+    uint32_t T = 0;
+    for (int e = 0; e < world; ++e) T += dest_total[e];
+    uint32_t* const side_lo = reinterpret_cast<uint32_t*>(send + (size_t)kXRecFloat4 * T);
+    uint32_t* const side_hi = side_lo + T;
+    uint32_t* const side_key = side_hi + T;
+    // Destination by destination: this wave's records for d (every round's,
+    // consecutive in d's region from the wave's offset) leave run by run
+    // through the record stage; their side words gather in LDS and leave
+    // together, one coalesced run per region.
     float4* const stage = stg[wave];
+    for (int d = 0; d < world; ++d) {
+        const uint32_t pos0 = base_d[d] + wc[wave][d];
+        uint32_t acc = 0;  // this wave's records for d so far
 #pragma unroll
-    for (int k = 0; k < kShIpt; ++k) {
-        const uint32_t m = mk[k];
-        for (int d = 0; d < world; ++d) {
-            const bool bit = (m >> d) & 1u;
+        for (int k = 0; k < kShIpt; ++k) {
+            const bool bit = (mk[k] >> d) & 1u;
             const uint64_t b = __ballot(bit);
             if (b == 0) continue;
-            const uint32_t c3 = 3u * (uint32_t)__popcll(b);
+            const uint32_t c = (uint32_t)__popcll(b), j = mbcnt(b);
             if (bit) {
-                const uint32_t j = 3u * mbcnt(b);
-                stage[j] = r0[k];
-                stage[j + 1] = r1[k];
-                stage[j + 2] = r2[k];
+                stage[3u * j] = r0[k];
+                stage[3u * j + 1u] = r1[k];
+                stage[3u * j + 2u] = r2[k];
+                sside[wave][0][acc + j] = lo[k];
+                sside[wave][1][acc + j] = hi[k];
+                sside[wave][2][acc + j] = dk[k];
             }
             wave_lds_sync();
-            const uint32_t pos = __shfl(next, d, 64);
-            float4* dst = send + (size_t)kXRecFloat4 * pos;
-            for (uint32_t q = lane; q < c3; q += 64) dst[q] = stage[q];
+            float4* dst = send + (size_t)kXRecFloat4 * (pos0 + acc);
+            for (uint32_t q = lane; q < 3u * c; q += 64) dst[q] = stage[q];
             wave_lds_sync();  // (the stage is refilled by the next run)
-            if (lane == (uint32_t)d) next += c3 / 3u;
+            acc += c;
         }
+        for (uint32_t q = lane; q < acc; q += 64) {
+            side_lo[pos0 + q] = sside[wave][0][q];
+            side_hi[pos0 + q] = sside[wave][1][q];
+            side_key[pos0 + q] = sside[wave][2][q];
+        }
+        wave_lds_sync();  // (the side stage is refilled by the next destination)
     }
-}
-
-// Decode the received records in place: the packed rect words become the
-// standard (x | y << 16) ones, so the composite reads them like local records.
-// In masked frames (FrameUniforms::cell_mask) the exclusion masks the 48-B
-// exchange record has no room for are computed again from the record's own
-// centre, axes and rect (gs_masks.h, the preprocess's function of the same
-// fields): the cell mask into the record, the bin mask into the binning rect,
-// so a rank emits the pairs and culls the cells of the single-GPU frame.
-__global__ __launch_bounds__(256) void recv_unpack_kernel(float4* __restrict__ recv, uint32_t m, bool masked,
-                                                          uint32_t* __restrict__ dkey, uint32_t* __restrict__ rect_lo,
-                                                          uint32_t* __restrict__ rect_hi) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= m) return;
-    float4* r = recv + (size_t)kXRecFloat4 * i;
-    float4 c = r[2];
-    const uint32_t plo = __float_as_uint(c.z), phi = __float_as_uint(c.w);
-    const uint32_t lo = xrect_unpack(plo), hi = xrect_unpack(phi);
-    dkey[i] = (plo >> 24) | ((phi >> 24) << 8);
-    RectMasks rm{0u, 0u};
-    if (masked) {
-        const float4 a = r[0], b = r[1];
-        rm = rect_masks(a.x, a.y, a.z, a.w, b.x, b.y, lo & 0xFFFFu, lo >> 16, hi & 0xFFFFu, hi >> 16);
-    }
-    rect_lo[i] = rect_with_mask(lo, rm.bin & 0xFu, (rm.bin >> 4) & 0xFu);
-    rect_hi[i] = rect_with_mask(hi, (rm.bin >> 8) & 0xFu, rm.bin >> 12);
-    c.z = __uint_as_float(rect_with_mask(lo, rm.cell & 0xFu, (rm.cell >> 4) & 0xFu));
-    c.w = __uint_as_float(rect_with_mask(hi, (rm.cell >> 8) & 0xFu, rm.cell >> 12));
-    r[2] = c;
 }
 
 hipError_t launch_shard_count(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, int world,
@@ -252,11 +238,12 @@ hipError_t launch_rows_scan(uint32_t* counts, uint32_t nblocks, int rows, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_shard_pack(const float4* rec, const uint32_t* dkey, const uint32_t* dest_mask, uint32_t n,
-                             int world, const uint32_t* counts, const uint32_t* dest_total,
-                             uint32_t nblocks, float4* send, hipStream_t st) {
+hipError_t launch_shard_pack(const float4* rec, const uint32_t* rlo, const uint32_t* rhi, const uint32_t* dkey,
+                             const uint32_t* dest_mask, uint32_t n, int world, const uint32_t* counts,
+                             const uint32_t* dest_total, uint32_t nblocks, float4* send, hipStream_t st) {
     if (nblocks == 0) return hipSuccess;
-    shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, dkey, dest_mask, n, world, counts, dest_total, nblocks, send);
+    shard_pack_kernel<<<nblocks, 256, 0, st>>>(rec, rlo, rhi, dkey, dest_mask, n, world, counts, dest_total, nblocks,
+                                               send);
     return hipGetLastError();
 }
 
@@ -277,11 +264,5 @@ hipError_t launch_accumulate(float4* dst, const float4* src, size_t n4, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_recv_unpack(float4* recv, uint32_t m, bool masked, uint32_t* dkey, uint32_t* rect_lo,
-                              uint32_t* rect_hi, hipStream_t st) {
-    if (m == 0) return hipSuccess;
-    recv_unpack_kernel<<<(m + 255) / 256, 256, 0, st>>>(recv, m, masked, dkey, rect_lo, rect_hi);
-    return hipGetLastError();
-}
 
 }  // namespace gs

@@ -121,13 +121,18 @@ def assemble(bands, width: int, height: int, world: int, owner=None):
     return frame[:height]
 
 
-def gather_frame(band, width: int, height: int, world: int, rank: int, owner=None, group=None, p2p=None):
+def gather_frame(band, width: int, height: int, world: int, rank: int, owner=None, group=None, p2p=None,
+                 pending=None):
     """The rank bands -> the full frame on rank 0 (None elsewhere).  With the
     default contiguous ownership over RCCL every rank sends its valid rows
     straight into their place in rank 0's frame (point-to-point, no padded
     bands, no reassembly copies); gloo (host-staged) and custom owner tables
     gather the padded bands and scatter them (`assemble`).  p2p=True forces the
-    point-to-point path (CPU tensors over gloo: its test)."""
+    point-to-point path (CPU tensors over gloo: its test).
+    pending (a list; point-to-point path only): the transfers are left in
+    flight and their works appended to it, so the caller's stream is not made
+    to wait for them (ShardedRenderer's pipelined frames wait on the user's
+    stream, not on the compute stream)."""
     import torch
     import torch.distributed as dist
 
@@ -145,12 +150,18 @@ def gather_frame(band, width: int, height: int, world: int, rank: int, owner=Non
             y0, y1 = spans[0]
             if y1 > y0:
                 frame[y0:y1].copy_(band[: y1 - y0])
-            for q in reqs:
-                q.wait()
+            if pending is not None:
+                pending.extend(reqs)
+            else:
+                for q in reqs:
+                    q.wait()
             return frame
         y0, y1 = spans[rank]
         if y1 > y0:
-            dist.send(band[: y1 - y0], 0, group=group)
+            if pending is not None:
+                pending.append(dist.isend(band[: y1 - y0], 0, group=group))
+            else:
+                dist.send(band[: y1 - y0], 0, group=group)
         return None
     if _host_staged(group):
         hb = band.cpu()
@@ -179,6 +190,7 @@ class HipShardBackend:
                   "gs_shard_set_rows")
         self.world, self.rank, self.device = world, rank, torch.device(f"cuda:{device}")
         self.xbytes = int(lib().gs_exchange_record_bytes())
+        self.xregions = exchange_regions()
         self._send = [torch.empty(max(1, shard.n * world * self.xbytes), dtype=torch.uint8, device=self.device)]
 
     @property
@@ -334,44 +346,86 @@ def _host_staged(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
+def exchange_regions() -> tuple:
+    """Bytes per record of each exchange region (gs_exchange_regions): the
+    48-B records, then the rect lo / hi words and depth keys (gsplat.h)."""
+    n = int(lib().gs_exchange_regions(None))
+    b = (C.c_int32 * n)()
+    lib().gs_exchange_regions(b)
+    return tuple(int(x) for x in b)
+
+
+def region_views(buf, total: int, regions):
+    """The regions of an exchange buffer holding `total` records."""
+    out, o = [], 0
+    for b in regions:
+        out.append(buf[o: o + total * b])
+        o += total * b
+    return out
+
+
 class PendingExchange:
     """A record all_to_all in flight (exchange_start); wait() -> (recv, nrec)."""
 
-    def __init__(self, work, recv, total, dev):
-        self.work, self.recv, self.total, self.dev = work, recv, total, dev
+    def __init__(self, works, recv, total, dev):
+        self.works, self.recv, self.total, self.dev = works, recv, total, dev
 
     def wait(self):
-        if self.work is not None:
-            self.work.wait()  # (RCCL: the current stream waits for the exchange)
-            self.work = None
+        for w in self.works:
+            w.wait()  # (RCCL: the current stream waits for the exchange)
+        self.works = []
         recv = self.recv if self.recv.device == self.dev else self.recv.to(self.dev)
         return recv, self.total
 
 
-def exchange_start(send, counts, xbytes, world, group=None) -> PendingExchange:
-    """all_to_all of counts (the host sizes the receive buffer), then the
-    records' all_to_all started asynchronously."""
+def exchange_start(send, counts, regions, world, group=None) -> PendingExchange:
+    """all_to_all of counts (the host sizes the receive buffer), then one
+    all_to_all per exchange region (records, rect lo, rect hi, depth keys;
+    `regions` = their bytes per record), started asynchronously."""
     import torch
     import torch.distributed as dist
 
+    regions = (regions,) if isinstance(regions, int) else tuple(regions)
+    xb = sum(regions)
     dev = send.device
     cdev = torch.device("cpu") if _host_staged(group) else dev
     sc = torch.tensor(counts, dtype=torch.int64, device=cdev)
     rc = torch.empty(world, dtype=torch.int64, device=cdev)
     dist.all_to_all_single(rc, sc, group=group)
     rcounts = [int(x) for x in rc.cpu().tolist()]
-    total = sum(rcounts)
-    ssz = sum(counts) * xbytes
-    recv = torch.empty(max(1, total * xbytes), dtype=torch.uint8, device=cdev)
-    src = send[:ssz] if cdev == dev else send[:ssz].cpu()
-    work = dist.all_to_all_single(recv[: total * xbytes], src, [c * xbytes for c in rcounts],
-                                  [c * xbytes for c in counts], group=group, async_op=True)
-    return PendingExchange(work, recv, total, dev)
+    total, sent = sum(rcounts), sum(counts)
+    recv = torch.empty(max(1, total * xb), dtype=torch.uint8, device=cdev)
+    src = send[: sent * xb] if cdev == dev else send[: sent * xb].cpu()
+    works = [dist.all_to_all_single(r, q, [c * b for c in rcounts], [c * b for c in counts], group=group,
+                                    async_op=True)
+             for b, r, q in zip(regions, region_views(recv, total, regions), region_views(src, sent, regions))]
+    return PendingExchange(works, recv, total, dev)
 
 
-def exchange(send, counts, xbytes, world, group=None):
-    """all_to_all of counts then of records (bytes); returns (recv, nrec)."""
-    return exchange_start(send, counts, xbytes, world, group).wait()
+def exchange(send, counts, regions, world, group=None):
+    """all_to_all of counts then of the record regions; returns (recv, nrec)."""
+    return exchange_start(send, counts, regions, world, group).wait()
+
+
+def virtual_exchange(sends, regions, world: int):
+    """The all_to_all by slicing (every rank in one process): for each
+    destination its received buffer (region by region, source-rank order
+    inside) and record count, from every source's (send, counts)."""
+    import torch
+
+    regions = (regions,) if isinstance(regions, int) else tuple(regions)
+    out = []
+    for dst in range(world):
+        parts, nrec = [], 0
+        views = [region_views(buf, sum(counts), regions) for buf, counts in sends]
+        for k, b in enumerate(regions):
+            for src in range(world):
+                counts = sends[src][1]
+                off = sum(counts[:dst]) * b
+                parts.append(views[src][k][off: off + counts[dst] * b])
+        nrec = sum(sends[src][1][dst] for src in range(world))
+        out.append((torch.cat(parts) if nrec else None, nrec))
+    return out
 
 
 class ShardedRenderer:
@@ -381,36 +435,74 @@ class ShardedRenderer:
     starts its record exchange on `exchange_group` (its own communicator, so
     it runs beside the gather), then renders and gathers the PREVIOUS frame
     and returns it (None on the first call); flush() finishes the frame still
-    in flight.  Every rank must make the same calls."""
+    in flight.  Every rank must make the same calls.  Over RCCL a pipelined
+    rank computes on its own stream: the band transfers of the gather are
+    waited for by the caller's stream only (rank 0's frame is ready there), so
+    the next frame's projection does not queue behind them."""
 
     def __init__(self, backend, rank: int, world: int, group=None, pipeline: bool = False, exchange_group=None):
+        import torch
+
         self.b, self.rank, self.world, self.group = backend, rank, world, group
         self.pipeline = pipeline
         self.xgroup = exchange_group if exchange_group is not None else group
         self._pending = None
         self._slot = 0
+        dev = getattr(backend, "device", None)
+        self._cs = (torch.cuda.Stream(dev) if pipeline and world > 1 and dev is not None and dev.type == "cuda"
+                    and not _host_staged(group) else None)
+        self._inflight = []  # (works, tensors) of the last gather, until the next frame
 
-    def _finish(self, pend, width, height, gather):
+    def _finish(self, pend, width, height, gather, works=None):
         recv, nrec = pend.wait()
         band = self.b.render(recv, nrec, width, height)
         if not gather:
             return band
         if self.world == 1:
             return assemble([band], width, height, 1)
-        return gather_frame(band, width, height, self.world, self.rank, getattr(self.b, "owner", None), self.group)
+        out = gather_frame(band, width, height, self.world, self.rank, getattr(self.b, "owner", None), self.group,
+                           pending=works)
+        if works is not None:
+            self._inflight.append((band, out))  # (alive until their transfers are done)
+        return out
 
     def render(self, view, proj, width, height, gather: bool = True):
         """Returns the full frame on rank 0 (None elsewhere) when gather=True,
         else this rank's band buffer (pipelined: the previous frame's)."""
         if not self.pipeline:
             send, counts = self.b.project(view, proj, width, height)
-            return self._finish(exchange_start(send, counts, self.b.xbytes, self.world, self.group),
+            return self._finish(exchange_start(send, counts, self.b.xregions, self.world, self.group),
                                 width, height, gather)
+        if self._cs is None:
+            return self._step(view, proj, width, height, gather, None)
+        import torch
+
+        # (the rank's stream does not wait for the caller's: nothing the frame
+        # reads is written there, and the caller's stream holds the waits for
+        # the previous gather, which this frame must not queue behind)
+        user = torch.cuda.current_stream(self._cs.device)
+        works = []
+        with torch.cuda.stream(self._cs):
+            out = self._step(view, proj, width, height, gather, works)
+        return self._land(out, works, user)
+
+    def _step(self, view, proj, width, height, gather, works):
         send, counts = self.b.project(view, proj, width, height, slot=self._slot)
         self._slot ^= 1
-        nxt = (exchange_start(send, counts, self.b.xbytes, self.world, self.xgroup), width, height, gather)
-        out = self._finish(*self._pending) if self._pending is not None else None
+        nxt = (exchange_start(send, counts, self.b.xregions, self.world, self.xgroup), width, height, gather)
+        old, self._inflight = self._inflight, []
+        out = self._finish(*self._pending, works=works) if self._pending is not None else None
+        del old  # (the previous gather's tensors: its transfers were waited for by the caller's stream)
         self._pending = nxt
+        return out
+
+    def _land(self, out, works, user):
+        """The gather's transfers, waited for by the caller's stream; the
+        frame (computed on the rank's stream) is marked in use there."""
+        for w in works:
+            w.wait()
+        if out is not None:
+            out.record_stream(user)
         return out
 
     def flush(self):
@@ -418,7 +510,15 @@ class ShardedRenderer:
         if self._pending is None:
             return None
         p, self._pending = self._pending, None
-        return self._finish(*p)
+        if self._cs is None:
+            return self._finish(*p)
+        import torch
+
+        user = torch.cuda.current_stream(self._cs.device)
+        works = []
+        with torch.cuda.stream(self._cs):
+            out = self._finish(*p, works=works)
+        return self._land(out, works, user)
 
 
 def _all_reduce_sum(t, group):
@@ -461,7 +561,7 @@ class SlabRenderer:
         hist = _all_reduce_sum(self.b.project(view, proj, width, height), self.group)
         bounds = slab_bounds(hist.cpu().numpy(), self.world)
         send, counts = self.b.pack(bounds)
-        recv, nrec = exchange(send, counts, self.b.xbytes, self.world, self.group)
+        recv, nrec = exchange(send, counts, self.b.xregions, self.world, self.group)
         t = self.b.render(recv, nrec, width, height)
         t_all = _all_gather(t, self.world, self.group) if self.world > 1 else t[None]
         out = self.b.composite(t_all)
@@ -492,17 +592,9 @@ def render_virtual_slabs(scene: Scene, world: int, view, proj, width: int, heigh
     hist = sum(be.project(view, proj, width, height) for be in backends)
     bounds = slab_bounds(hist.cpu().numpy(), world)
     sends = [be.pack(bounds) for be in backends]
-    xb = backends[0].xbytes
     ts, recvs = [], []
-    for dst in range(world):
-        chunks = []
-        for src in range(world):
-            buf, counts = sends[src]
-            off = sum(counts[:dst]) * xb
-            chunks.append(buf[off: off + counts[dst] * xb].clone())
-        recv = torch.cat(chunks)
-        nrec = recv.numel() // xb
-        recvs.append(recv if recv.numel() else backends[dst].empty(xb))
+    for dst, (recv, nrec) in enumerate(virtual_exchange(sends, backends[0].xregions, world)):
+        recvs.append(recv if nrec else backends[dst].empty(backends[dst].xbytes))
         ts.append(backends[dst].render(recvs[-1], nrec, width, height))
     t_all = torch.stack(ts)
     contrib = [be.composite(t_all) for be in backends]
@@ -542,17 +634,9 @@ class VirtualShards:
         import torch
 
         sends = [be.project(view, proj, width, height) for be in self.backends]
-        xb = self.backends[0].xbytes
         bands = []
-        for dst, be in enumerate(self.backends):
-            parts = []
-            for src in range(self.world):
-                buf, counts = sends[src]
-                off = sum(counts[:dst]) * xb
-                parts.append(buf[off: off + counts[dst] * xb])
-            recv = torch.cat(parts) if parts else be.empty(0)
-            nrec = recv.numel() // xb
-            bands.append(be.render(recv if recv.numel() else be.empty(xb), nrec, width, height))
+        for be, (recv, nrec) in zip(self.backends, virtual_exchange(sends, self.backends[0].xregions, self.world)):
+            bands.append(be.render(recv if nrec else be.empty(be.xbytes), nrec, width, height))
         return assemble(bands, width, height, self.world, self.owner)
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 9
+#define GSPLAT_ABI_VERSION 10
 
 typedef enum {
     GS_OK = 0,
@@ -213,20 +213,28 @@ gs_status gs_shard_configure(gs_handle *h, int32_t rank, int32_t world, int64_t 
  * Every rank must install the same table (e.g. rebalanced from the last
  * frame's per-row cost). */
 gs_status gs_shard_set_rows(gs_handle *h, const uint8_t *owner, int32_t nrows);
+/* Exchange buffers (send and receive alike) hold n records as GS_XREGIONS
+ * regions one after another: the n 48-B records (the projection's record,
+ * exclusion masks included), then n binning-rect lo words, n hi words and n
+ * 15-bit depth keys (4 B each).  On the send side every region is grouped by
+ * destination (the same counts); an all-to-all moves each region separately
+ * (per-peer sizes = records x that region's bytes per record, listed by
+ * gs_exchange_regions), which leaves the receiver the same layout in
+ * source-rank order. */
+#define GS_XREGIONS 4
 /* Project the local shard and pack, for every visible splat and every rank
  * owning a bin row its rect touches, one exchange record into `send`
  * (device memory, capacity `send_cap_bytes`), grouped by destination, index
  * order inside.  Writes world send counts (in records) to host `send_counts`.
- * Record size: gs_exchange_record_bytes(). */
+ * Bytes per record over all regions: gs_exchange_record_bytes(). */
 gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[16], int32_t width,
                            int32_t height, void *send, int64_t send_cap_bytes, int64_t *send_counts,
                            void *hip_stream);
-/* Bin, sort and composite the received records (concatenated in source-rank
- * order, i.e. global index order) into this rank's band buffer `out_rgba`
- * (device): the owned bin rows stacked in ascending order, 32 pixel rows
- * each, width pixels wide, fp32 RGBA.  `recv` (device) is decoded in place.
- * Multi-GPU frames are limited to 4096 x 4096 (the exchange record packs
- * 12-bit rect coordinates with the depth key). */
+/* Bin, sort and composite the received records (recv_count of them, in the
+ * exchange layout above, concatenated in source-rank order, i.e. global
+ * index order) into this rank's band buffer `out_rgba` (device): the owned
+ * bin rows stacked in ascending order, 32 pixel rows each, width pixels
+ * wide, fp32 RGBA.  `recv` (device) is read only. */
 gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height,
                           float *out_rgba, void *hip_stream);
 
@@ -239,7 +247,10 @@ gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t 
  * gs_render.  With world 1 the band is the whole frame. */
 gs_status gs_band_render(gs_handle *h, const float view[16], const float proj[16], int32_t width, int32_t height,
                          float *out_band, void *stream);
-int32_t gs_exchange_record_bytes(void);
+int32_t gs_exchange_record_bytes(void); /* 60: every region's bytes per record */
+/* Bytes per record of each exchange region into bytes_per_record[GS_XREGIONS]
+ * (may be null); returns GS_XREGIONS. */
+int32_t gs_exchange_regions(int32_t *bytes_per_record);
 
 /* ---- multi-GPU: depth slabs + RGBA reduce --------- */
 /* The north star's scheme: splat-index shards, each rank composites one

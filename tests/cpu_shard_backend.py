@@ -1,36 +1,47 @@
 """CPU stand-in for HipShardBackend (test infrastructure).
 
-Per-rank compute by the oracle; the 48-B exchange record format, the
-destination rule (bin-row owner table) and the band layout are the product's,
-so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer exercise the
-real exchange / gather / assembly protocol on CPU.
+Per-rank compute by the oracle; the exchange layout (gsplat.h: 48-B records,
+then rect lo / hi words and depth keys, each region grouped by destination),
+the destination rule (bin-row owner table) and the band layout are the
+product's, so gloo runs of gaussian_splat_amd.distributed.ShardedRenderer
+exercise the real exchange / gather / assembly protocol on CPU.
 """
 import numpy as np
 
 from oracle import oracle_py as O
 
-XREC = O.RECORD_DTYPE  # 48-B exchange record: rect words repacked with the depth key
+XREC = O.RECORD_DTYPE  # 48-B exchange record: the projection's record
 assert XREC.itemsize == 48
+XREGIONS = (48, 4, 4, 4)
 
 
-def _xpack(xy, key8):
-    return (xy & 0xFFF) | (((xy >> 16) & 0xFFF) << 12) | (key8.astype(np.uint32) << 24)
+def _pack(parts):
+    """Exchange regions of the per-destination (records, depth keys)."""
+    import torch
+
+    recs = np.concatenate([r for r, _ in parts]) if parts else np.zeros(0, XREC)
+    keys = np.concatenate([k for _, k in parts]).astype(np.uint32) if parts else np.zeros(0, np.uint32)
+    buf = np.concatenate([recs.view(np.uint8), recs["rect_lo"].astype(np.uint32).view(np.uint8),
+                          recs["rect_hi"].astype(np.uint32).view(np.uint8), keys.view(np.uint8)])
+    return torch.from_numpy(buf.copy() if buf.size else np.zeros(1, np.uint8))
 
 
-def _xunpack(p):
-    return (p & 0xFFF) | (((p >> 12) & 0xFFF) << 16)
+def _unpack(recv, nrec):
+    raw = recv.numpy()[: nrec * 60]
+    rec = raw[: nrec * 48].copy().view(XREC)
+    dkey = raw[nrec * 56: nrec * 60].copy().view(np.uint32)
+    return rec, dkey
 
 
 class OracleShardBackend:
-    xbytes = 48
+    xbytes = 60
+    xregions = XREGIONS
 
     def __init__(self, shard, rank, world, index_base, sh_degree=0, mode="tile", cap=0):
         self.shard, self.rank, self.world, self.base = shard, rank, world, index_base
         self.sh, self.mode, self.cap = sh_degree, mode, cap
 
     def project(self, view, proj, width, height, slot=0):
-        import torch
-
         from gaussian_splat_amd.distributed import row_owner
 
         rec, dk, nt = O.project(self.shard, view, proj, width, height, sh_degree=self.sh)
@@ -46,22 +57,14 @@ class OracleShardBackend:
             if len(rows):  # a rank owns a contiguous range [rows[0], rows[-1]]
                 touch = (ty0 <= rows[-1]) & (ty1 >= rows[0])
             idx = np.nonzero(vis & touch)[0]
-            x = rec[idx].copy()
-            x["rect_lo"] = _xpack(rec["rect_lo"][idx], dk[idx] & 0xFF)
-            x["rect_hi"] = _xpack(rec["rect_hi"][idx], dk[idx] >> 8)
-            parts.append(x)
+            parts.append((rec[idx], dk[idx]))
             counts.append(len(idx))
-        buf = np.concatenate(parts).view(np.uint8) if parts else np.zeros(0, np.uint8)
-        return torch.from_numpy(np.ascontiguousarray(buf).copy() if buf.size else np.zeros(1, np.uint8)), counts
+        return _pack(parts), counts
 
     def render(self, recv, nrec, width, height):
         import torch
 
-        raw = recv.numpy()[: nrec * 48].copy().view(XREC)
-        rec = raw.copy()
-        dkey = (raw["rect_lo"] >> 24) | ((raw["rect_hi"] >> 24) << 8)
-        rec["rect_lo"] = _xunpack(raw["rect_lo"])
-        rec["rect_hi"] = _xunpack(raw["rect_hi"])
+        rec, dkey = _unpack(recv, nrec)
         from gaussian_splat_amd.distributed import band_rows, row_owner
 
         band = np.zeros((band_rows(height, self.world), width, 4), np.float32)
@@ -86,29 +89,19 @@ class OracleSlabBackend(OracleShardBackend):
         return torch.from_numpy(hist)
 
     def pack(self, bounds):
-        import torch
-
         rec, dk, vis = self._rec, self._dk, self._nt > 0
         slab = np.searchsorted(np.asarray(bounds[1:-1], np.int64), dk.astype(np.int64), side="right")
         parts, counts = [], []
         for d in range(self.world):
             idx = np.nonzero(vis & (slab == d))[0]
-            x = rec[idx].copy()
-            x["rect_lo"] = _xpack(rec["rect_lo"][idx], dk[idx] & 0xFF)
-            x["rect_hi"] = _xpack(rec["rect_hi"][idx], dk[idx] >> 8)
-            parts.append(x)
+            parts.append((rec[idx], dk[idx]))
             counts.append(len(idx))
-        buf = np.concatenate(parts).view(np.uint8)
-        return torch.from_numpy(buf.copy() if buf.size else np.zeros(1, np.uint8)), counts
+        return _pack(parts), counts
 
     def render(self, recv, nrec, width, height):
         import torch
 
-        raw = recv.numpy()[: nrec * 48].copy().view(XREC)
-        self._srec = raw.copy()
-        self._sdk = (raw["rect_lo"] >> 24) | ((raw["rect_hi"] >> 24) << 8)
-        self._srec["rect_lo"] = _xunpack(raw["rect_lo"])
-        self._srec["rect_hi"] = _xunpack(raw["rect_hi"])
+        self._srec, self._sdk = _unpack(recv, nrec)
         return torch.from_numpy(O.composite_slab(self._srec, self._sdk, width, height, 1, mode=self.mode))
 
     def composite(self, t_all):

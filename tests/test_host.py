@@ -23,8 +23,10 @@ def test_library_exports_every_declared_symbol(built):
     for name in sorted(declared):
         assert hasattr(L, name), name
     assert set(_lib.SIGNATURES) == declared
-    assert L.gs_abi_version() == 9
-    assert L.gs_exchange_record_bytes() == 48
+    assert L.gs_abi_version() == 10
+    assert L.gs_exchange_record_bytes() == 60
+    from gaussian_splat_amd.distributed import exchange_regions
+    assert exchange_regions() == (48, 4, 4, 4)
 
 
 def test_errors_are_reported_not_thrown(built):

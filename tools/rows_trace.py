@@ -38,7 +38,7 @@ import torch  # noqa: E402
 
 from gaussian_splat_amd import scene as S  # noqa: E402
 from gaussian_splat_amd.api import Options, default_camera  # noqa: E402
-from gaussian_splat_amd.distributed import HipShardBackend, shard_bounds  # noqa: E402
+from gaussian_splat_amd.distributed import HipShardBackend, shard_bounds, virtual_exchange  # noqa: E402
 
 W, H = 1920, 1080
 sc = S.synthetic_scene(a.splats, seed=2, sh_degree=3, aspect=W / H)
@@ -48,12 +48,9 @@ opt = Options(sh_degree=3, crop=False, frames_in_flight=1)
 g = a.world
 bes = [HipShardBackend(sc.subset(slice(*shard_bounds(sc.n, g, r))), r, g, shard_bounds(sc.n, g, r)[0], opt, 0)
        for r in range(g)]
-xb = bes[0].xbytes
 for _ in range(5):
     sends = [be.project(V, P, W, H) for be in bes]
-    for dst in range(g):
-        parts = [sends[src][0][sum(sends[src][1][:dst]) * xb: sum(sends[src][1][:dst + 1]) * xb] for src in range(g)]
-        recv = torch.cat(parts)
-        bes[dst].render(recv, recv.numel() // xb, W, H)
+    for dst, (recv, nrec) in enumerate(virtual_exchange(sends, bes[0].xregions, g)):
+        bes[dst].render(recv if nrec else bes[dst].empty(bes[dst].xbytes), nrec, W, H)
     torch.cuda.synchronize()
 print("done")
