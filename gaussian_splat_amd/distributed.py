@@ -451,7 +451,7 @@ class ShardedRenderer:
         dev = getattr(backend, "device", None)
         self._cs = (torch.cuda.Stream(dev) if pipeline and world > 1 and dev is not None and dev.type == "cuda"
                     and not _host_staged(group) else None)
-        self._inflight = []  # (works, tensors) of the last gather, until the next frame
+        self._inflight = []  # (band, frame) of the last gather, alive until the next frame
 
     def _finish(self, pend, width, height, gather, works=None):
         recv, nrec = pend.wait()
@@ -497,8 +497,9 @@ class ShardedRenderer:
         return out
 
     def _land(self, out, works, user):
-        """The gather's transfers, waited for by the caller's stream; the
-        frame (computed on the rank's stream) is marked in use there."""
+        """The frame's compute (the rank's stream) and the gather's transfers,
+        waited for by the caller's stream; the frame is marked in use there."""
+        user.wait_stream(self._cs)
         for w in works:
             w.wait()
         if out is not None:
