@@ -440,7 +440,8 @@ class ShardedRenderer:
     waited for by the caller's stream only (rank 0's frame is ready there), so
     the next frame's projection does not queue behind them."""
 
-    def __init__(self, backend, rank: int, world: int, group=None, pipeline: bool = False, exchange_group=None):
+    def __init__(self, backend, rank: int, world: int, group=None, pipeline: bool = False, exchange_group=None,
+                 own_stream: Optional[bool] = None):
         import torch
 
         self.b, self.rank, self.world, self.group = backend, rank, world, group
@@ -449,8 +450,12 @@ class ShardedRenderer:
         self._pending = None
         self._slot = 0
         dev = getattr(backend, "device", None)
-        self._cs = (torch.cuda.Stream(dev) if pipeline and world > 1 and dev is not None and dev.type == "cuda"
-                    and not _host_staged(group) else None)
+        # own_stream: None = over RCCL only (gloo stages through the host,
+        # which waits anyway); True also over gloo (its test on one GPU)
+        if own_stream is None:
+            own_stream = not _host_staged(group)
+        self._cs = (torch.cuda.Stream(dev) if pipeline and own_stream and world > 1 and dev is not None
+                    and dev.type == "cuda" else None)
         self._inflight = []  # (band, frame) of the last gather, alive until the next frame
 
     def _finish(self, pend, width, height, gather, works=None):

@@ -594,26 +594,36 @@ def _rank_worker(rank, world, port, q, scheme="rows"):
         W, H = 800, 600
         sc = S.activate(S.synthetic_raw(60000, seed=51, aspect=W / H), 3)
         b, e = shard_bounds(sc.n, world, rank)
-        Backend, Renderer = (HipShardBackend, ShardedRenderer) if scheme == "rows" else (HipSlabBackend, SlabRenderer)
+        Backend, Renderer = (HipSlabBackend, SlabRenderer) if scheme == "slabs" else (HipShardBackend, ShardedRenderer)
         be = Backend(sc.subset(slice(b, e)), rank, world, b, Options(sh_degree=3, crop=False), 0)
-        V, P = orbit_views(W, H, 1)[0]
-        frame = Renderer(be, rank, world).render(V, P, W, H)
-        if rank == 0:
-            torch.cuda.synchronize()
-            q.put(frame.cpu().numpy())
+        if scheme == "pipe":  # two frames in flight, the rank on its own stream, a camera path
+            sr = ShardedRenderer(be, rank, world, pipeline=True, exchange_group=dist.new_group(backend="gloo"),
+                                 own_stream=True)
+            frames = [sr.render(V, P, W, H) for V, P in orbit_views(W, H, 4)] + [sr.flush()]
+            if rank == 0:
+                torch.cuda.synchronize()
+                q.put([None if f is None else f.cpu().numpy() for f in frames])
+        else:
+            V, P = orbit_views(W, H, 1)[0]
+            frame = Renderer(be, rank, world).render(V, P, W, H)
+            if rank == 0:
+                torch.cuda.synchronize()
+                q.put(frame.cpu().numpy())
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scheme", ["rows", "slabs"])
+@pytest.mark.parametrize("scheme", ["rows", "slabs", "pipe"])
 def test_multiprocess_ranks_bitexact(built, scheme):
     """Two rank processes on the GPU through the product multi-GPU path
     (rows: gs_shard_project -> all_to_all -> gs_shard_render -> gather;
     slabs: gs_slab_project -> all_reduce -> gs_slab_pack -> all_to_all ->
     gs_slab_render -> all_gather -> gs_slab_composite -> reduce), collectives
     over gloo staged through host memory (one GPU here).  Rows: the frame
-    equals the single-GPU render bit for bit; slabs: within 1e-4."""
+    equals the single-GPU render bit for bit; slabs: within 1e-4.  pipe: rows
+    with two frames in flight and each rank computing on its own stream, over
+    a camera path (every frame one call late, bit for bit)."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -632,6 +642,11 @@ def test_multiprocess_ranks_bitexact(built, scheme):
     W, H = 800, 600
     sc = S.activate(S.synthetic_raw(60000, seed=51, aspect=W / H), 3)
     r = _renderer(sc, sh=3, crop=False)
+    if scheme == "pipe":
+        assert got[0] is None and len(got) == 5
+        for k, (V, P) in enumerate(orbit_views(W, H, 4)):
+            assert _compare(got[k + 1], r.render_host(V, P, W, H)) == (0.0, 0), k
+        return
     V, P = orbit_views(W, H, 1)[0]
     ref = r.render_host(V, P, W, H)
     if scheme == "rows":
