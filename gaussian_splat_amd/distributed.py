@@ -438,7 +438,10 @@ class ShardedRenderer:
     in flight.  Every rank must make the same calls.  Over RCCL a pipelined
     rank computes on its own stream: the band transfers of the gather are
     waited for by the caller's stream only (rank 0's frame is ready there), so
-    the next frame's projection does not queue behind them."""
+    the next frame's projection does not queue behind them.  Per call the
+    rank's stream runs projection k+1 then render k; the host exchanges frame
+    k+1's counts while the GPU renders k, and the record exchange of k+1
+    starts from a stream that waited for its projection alone."""
 
     def __init__(self, backend, rank: int, world: int, group=None, pipeline: bool = False, exchange_group=None,
                  own_stream: Optional[bool] = None):
@@ -456,11 +459,16 @@ class ShardedRenderer:
             own_stream = not _host_staged(group)
         self._cs = (torch.cuda.Stream(dev) if pipeline and own_stream and world > 1 and dev is not None
                     and dev.type == "cuda" else None)
+        # the next frame's exchange is issued from a stream that waited only
+        # for its projection, so it does not queue behind this frame's render
+        self._xs = torch.cuda.Stream(dev) if self._cs is not None else None
         self._inflight = []  # (band, frame) of the last gather, alive until the next frame
 
     def _finish(self, pend, width, height, gather, works=None):
         recv, nrec = pend.wait()
-        band = self.b.render(recv, nrec, width, height)
+        return self._gather(self.b.render(recv, nrec, width, height), width, height, gather, works)
+
+    def _gather(self, band, width, height, gather, works=None):
         if not gather:
             return band
         if self.world == 1:
@@ -494,9 +502,33 @@ class ShardedRenderer:
     def _step(self, view, proj, width, height, gather, works):
         send, counts = self.b.project(view, proj, width, height, slot=self._slot)
         self._slot ^= 1
-        nxt = (exchange_start(send, counts, self.b.xregions, self.world, self.xgroup), width, height, gather)
+        if self._xs is None:
+            nxt = (exchange_start(send, counts, self.b.xregions, self.world, self.xgroup), width, height, gather)
+            old, self._inflight = self._inflight, []
+            out = self._finish(*self._pending, works=works) if self._pending is not None else None
+            del old  # (the previous gather's tensors: its transfers were waited for by the caller's stream)
+            self._pending = nxt
+            return out
+        import torch
+
+        # The rank's stream: the previous frame's render is queued right
+        # behind this projection, before the host exchanges the counts (the
+        # GPU renders meanwhile); the exchange starts from its own stream,
+        # which waited for the projection alone; then the gather.
+        projected = torch.cuda.Event()
+        projected.record(self._cs)
         old, self._inflight = self._inflight, []
-        out = self._finish(*self._pending, works=works) if self._pending is not None else None
+        band = None
+        if self._pending is not None:
+            pend, w_, h_, g_ = self._pending
+            recv, nrec = pend.wait()
+            band = self.b.render(recv, nrec, w_, h_)
+        with torch.cuda.stream(self._xs):
+            self._xs.wait_event(projected)
+            nxt = (exchange_start(send, counts, self.b.xregions, self.world, self.xgroup), width, height, gather)
+        if nxt[0].recv.is_cuda:
+            nxt[0].recv.record_stream(self._cs)  # (received on the exchange stream, read on the rank's)
+        out = self._gather(band, *self._pending[1:], works=works) if self._pending is not None else None
         del old  # (the previous gather's tensors: its transfers were waited for by the caller's stream)
         self._pending = nxt
         return out
