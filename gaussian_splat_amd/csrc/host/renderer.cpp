@@ -1622,9 +1622,22 @@ gs_status gs_shard_set_rows(gs_handle* h, const uint8_t* owner, int32_t nrows) {
 
 namespace {
 
-// Preprocess of a shard frame (both multi-GPU schemes).
+// The row scheme's destination buffers: masks, per-block counts, totals.
+gs_status reserve_exchange(gs_handle* h) {
+    const uint32_t n = (uint32_t)h->n;
+    const uint32_t nb = (n + gs::kShardItems - 1) / gs::kShardItems;
+    GS_HIP(h->xmask.reserve((size_t)std::max<uint32_t>(n, 1) * 4));
+    GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
+    GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
+    if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
+    return GS_OK;
+}
+
+// Preprocess of a shard frame (both multi-GPU schemes).  owner (row scheme):
+// the projection also writes the destination masks and per-block counts
+// (ShardFuse), so pack_exchange skips its count kernel.
 gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, int32_t W, int32_t H,
-                           hipStream_t st, gs::FrameUniforms* U) {
+                           hipStream_t st, gs::FrameUniforms* U, const uint8_t* owner = nullptr) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
     if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "shard frame: bad arguments");
@@ -1635,9 +1648,19 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     h->shard_frame = true;
     h->slab_lists = false;
     begin_frame(h, st);
+    gs::ShardFuse sf;
+    if (owner) {
+        if ((s = reserve_exchange(h)) != GS_OK) return s;
+        sf.owner = owner;
+        sf.world = h->world;
+        sf.dest_mask = h->xmask.as<uint32_t>();
+        sf.counts = h->xcounts.as<uint32_t>();
+        sf.nblocks = (uint32_t)((h->n + gs::kShardItems - 1) / gs::kShardItems);
+        if (sf.nblocks) GS_HIP(hipMemsetAsync(sf.counts, 0, (size_t)sf.nblocks * h->world * 4, st));
+    }
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, *U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h)));
+                                 kernel_event(h, 1), fetch_counter(h), gs::PreFuse{}, sf));
     mark(h, 1, st);
     return GS_OK;
 }
@@ -1645,17 +1668,16 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
 // Destination masks by `rule`, per-destination counts (to host), then the
 // exchange records grouped by destination, index order inside.
 gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, void* send, int64_t send_cap_bytes,
-                        int64_t* send_counts, hipStream_t st) {
+                        int64_t* send_counts, hipStream_t st, bool counted = false) {
     const uint32_t n = (uint32_t)h->n;
     const uint32_t nb = (n + gs::kShardItems - 1) / gs::kShardItems;
-    GS_HIP(h->xmask.reserve((size_t)std::max<uint32_t>(n, 1) * 4));
-    GS_HIP(h->xcounts.reserve((size_t)std::max<uint32_t>(nb, 1) * h->world * 4));
-    GS_HIP(h->xtotal.reserve(gs::kMaxWorld * 4));
-    if (!h->host_xtotal) GS_HIP(hipHostMalloc((void**)&h->host_xtotal, gs::kMaxWorld * 4, hipHostMallocDefault));
+    gs_status rs = reserve_exchange(h);
+    if (rs != GS_OK) return rs;
     // (the scan writes every destination's total; with no splats it does not run)
     if (nb == 0) GS_HIP(hipMemsetAsync(h->xtotal.ptr, 0, gs::kMaxWorld * 4, st));
-    GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, rule, masked,
-                                  h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
+    if (!counted)  // (counted: the projection wrote the masks and counts, ShardFuse)
+        GS_HIP(gs::launch_shard_count(h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), n, h->world, rule, masked,
+                                      h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
     auto pack = [&]() -> hipError_t {
@@ -1731,16 +1753,19 @@ gs_status gs_shard_project(gs_handle* h, const float* view, const float* proj, i
                            int64_t send_cap_bytes, int64_t* send_counts, void* stream) {
     if (!send_counts) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (h) h->slab_frame = false;
-    gs::FrameUniforms U;
-    gs_status s = shard_preprocess(h, view, proj, W, H, st, &U);
+    gs_status s = check_ready(h);
     if (s != GS_OK) return s;
+    if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "gs_shard_project: bad arguments");
+    h->slab_frame = false;
+    // the owner table first: the projection counts the destinations itself
     Ownership own;
-    if ((s = frame_ownership(h, U.tiles_y, st, &own)) != GS_OK) return s;
+    if ((s = frame_ownership(h, (H + gs::kBin - 1) / gs::kBin, st, &own)) != GS_OK) return s;
     if (!own.dev.owner) return fail(GS_ERR_STATE, "gs_shard_project: world size 1");
+    gs::FrameUniforms U;
+    if ((s = shard_preprocess(h, view, proj, W, H, st, &U, own.dev.owner)) != GS_OK) return s;
     gs::DestRule rule{};
     rule.owner = own.dev.owner;
-    return pack_exchange(h, rule, U.cell_mask != 0, send, send_cap_bytes, send_counts, st);
+    return pack_exchange(h, rule, U.cell_mask != 0, send, send_cap_bytes, send_counts, st, true);
 }
 
 // Replicated-scene bands (SURVEY §8(e) fallback): the handle

@@ -154,6 +154,13 @@ __device__ __forceinline__ bool owns_bin_row(uint32_t by, const RowOwnership& o)
     return !o.owner || o.owner[by] == o.rank;
 }
 
+// Ranks owning any of the bin rows ty0..ty1 (the row scheme's destinations).
+__device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const uint8_t* __restrict__ owner) {
+    uint32_t m = 0;
+    for (uint32_t by = ty0; by <= ty1; ++by) m |= 1u << owner[by];
+    return m;
+}
+
 // Bin rect of a splat from its packed pixel rect words.  With `masked`
 // (frames up to kCellMaskDim px, FrameUniforms::cell_mask) the words also
 // carry a 16-bit bin-exclusion mask over the first 4x4 bins of the rect

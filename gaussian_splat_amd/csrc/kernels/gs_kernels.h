@@ -36,10 +36,23 @@ struct PreFuse {
     uint32_t* zero = nullptr;
     uint32_t nzero = 0;
 };
+// Row-scheme projections (gs_shard_project): the preprocess also writes each
+// splat's destination mask (the ranks owning a bin row its rect touches) and
+// adds each block's per-destination counts into counts[d * nblocks + b]
+// (kShardItems splats per block; counts zeroed first): what
+// launch_shard_count does otherwise.
+struct ShardFuse {
+    const uint8_t* owner = nullptr;  // null: off
+    int world = 0;
+    uint32_t* dest_mask = nullptr;
+    uint32_t* counts = nullptr;
+    uint32_t nblocks = 0;
+};
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st,
                              hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr,
-                             unsigned long long* zero8 = nullptr, const PreFuse& fuse = PreFuse{});
+                             unsigned long long* zero8 = nullptr, const PreFuse& fuse = PreFuse{},
+                             const ShardFuse& shard = ShardFuse{});
 
 // ---- scan.hip --------------------------------------------------------------
 constexpr int kScanItems = 4096;  // per block

@@ -131,12 +131,12 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 // compiled only into its own instance, so the plain kernel keeps its
 // registers (63 VGPRs, no scratch).
 template <int DEG, int EPI>
-__global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
+__global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
                                                          uint32_t* __restrict__ rect_hi,
                                                          unsigned long long* __restrict__ zero8,
-                                                         const PreFuse fuse) {
+                                                         const PreFuse fuse, const ShardFuse shard) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i < 2 && zero8) zero8[i] = 0ull;
     if constexpr (EPI == 0)
@@ -302,6 +302,30 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
     rect_lo[i] = rlo;
     rect_hi[i] = rhi;
     }
+    if constexpr (EPI == 2) {
+        // the row scheme's destination count (ShardFuse): each splat's
+        // destination mask, and this workgroup's per-destination counts into
+        // its shard block's (lane d of every wave counts destination d)
+        __shared__ uint32_t wc[4][kMaxWorld];
+        uint32_t m = 0u;
+        if (i < s.n) {
+            const BinRect r = bin_rect(rlo, rhi, U.cell_mask != 0);
+            if (!r.empty) m = row_mask(r.by0, r.by1, shard.owner);
+            shard.dest_mask[i] = m;
+        }
+        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+        uint32_t cnt = 0u;
+        for (int d = 0; d < shard.world; ++d) {
+            const uint64_t bal = __ballot((m >> d) & 1u);
+            if (lane == (uint32_t)d) cnt = (uint32_t)__popcll(bal);
+        }
+        if (lane < (uint32_t)kMaxWorld) wc[wave][lane] = cnt;
+        __syncthreads();
+        if (threadIdx.x < (uint32_t)shard.world) {
+            const uint32_t d = threadIdx.x, c = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+            if (c) atomicAdd(&shard.counts[(size_t)d * shard.nblocks + blockIdx.x / (uint32_t)(kShardItems / 256)], c);
+        }
+    }
     if constexpr (EPI == 1) {
         // the scan's reduce half: this workgroup's pairs and visible splats
         // into its scan block's sums (the counts scan_duplicate recomputes)
@@ -330,7 +354,7 @@ __global__ __launch_bounds__(256, GS_PRE_WAVES) void preprocess_kernel(SceneDev 
 
 hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUniforms& U, float4* rec,
                              uint32_t* dkey, uint32_t* rect_lo, uint32_t* rect_hi, hipStream_t st, hipEvent_t t0,
-                             hipEvent_t t1, unsigned long long* zero8, const PreFuse& fuse) {
+                             hipEvent_t t1, unsigned long long* zero8, const PreFuse& fuse, const ShardFuse& shard) {
     if (fuse.part && fuse.nb != (s.n + kScanItems - 1) / kScanItems) return hipErrorInvalidValue;
     if (s.n == 0 && fuse.part) {  // no grid: the fills as copies
         if (fuse.nfill && hipMemsetAsync(fuse.fill, 0xFF, (size_t)fuse.nfill * sizeof(uint2), st) != hipSuccess)
@@ -348,17 +372,21 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
     dim3 grid((s.n + 255) / 256), block(256);
     // t0/t1 (optional) are recorded by the dispatch packet itself: no extra
     // barrier packets around the kernel
-    const int epi = fuse.part ? 1 : 0;
-    switch (sh_degree * 2 + epi) {
+    if (fuse.part && shard.owner) return hipErrorInvalidValue;
+    if (shard.owner && (!shard.dest_mask || !shard.counts || shard.world < 1 || shard.world > kMaxWorld ||
+                        shard.nblocks != (s.n + kShardItems - 1) / kShardItems))
+        return hipErrorInvalidValue;
+    const int epi = fuse.part ? 1 : shard.owner ? 2 : 0;
+    switch (sh_degree * 3 + epi) {
 #define GS_PRE_CASE(D, E)                                                                                          \
-    case D * 2 + E:                                                                                                \
+    case D * 3 + E:                                                                                                \
         hipExtLaunchKernelGGL((preprocess_kernel<D, E>), grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, \
-                              rect_hi, zero8, fuse);                                                               \
+                              rect_hi, zero8, fuse, shard);                                                        \
         break;
-        GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1)
-        GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1)
-        GS_PRE_CASE(2, 0) GS_PRE_CASE(2, 1)
-        GS_PRE_CASE(3, 0) GS_PRE_CASE(3, 1)
+        GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1) GS_PRE_CASE(0, 2)
+        GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1) GS_PRE_CASE(1, 2)
+        GS_PRE_CASE(2, 0) GS_PRE_CASE(2, 1) GS_PRE_CASE(2, 2)
+        GS_PRE_CASE(3, 0) GS_PRE_CASE(3, 1) GS_PRE_CASE(3, 2)
 #undef GS_PRE_CASE
     default: return hipErrorInvalidValue;
     }

@@ -29,12 +29,6 @@ constexpr int kShIpt = kShardItems / 256;
 constexpr int kShWaveItems = 64 * kShIpt;
 static_assert(kShIpt * 256 == kShardItems, "shard block");
 
-// Ranks owning any of the bin rows ty0..ty1.
-__device__ __forceinline__ uint32_t row_mask(uint32_t ty0, uint32_t ty1, const uint8_t* __restrict__ owner) {
-    uint32_t m = 0;
-    for (uint32_t by = ty0; by <= ty1; ++by) m |= 1u << owner[by];
-    return m;
-}
 
 // Depth slab of a key: the d with bounds[d] <= key < bounds[d + 1].
 __device__ __forceinline__ uint32_t slab_of(uint32_t key, const DestRule& r, int world) {
