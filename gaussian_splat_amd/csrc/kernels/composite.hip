@@ -467,214 +467,6 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
     }
 }
 
-// Independent quadrant waves (tile / live50 rules, no cap, no slabs): the
-// same tiles, pixels, records and per-pixel walk as composite_kernel, but
-// every wave streams the bin list on its own, 64 records per batch through
-// its own LDS slots, stages and filters them for its quadrant only, and
-// leaves the list as soon as its 64 pixels are saturated.  No workgroup
-// barrier in the loop: a wave never waits for a sibling's longer walk.  The
-// price: each record is gathered (from L2) and staged by every wave whose
-// quadrant walks that far, instead of once per tile.
-template <int MODE, int PASS>
-__global__ __launch_bounds__(256, 8) __attribute__((amdgpu_num_sgpr(GS_COMPOSITE_SGPRS))) void composite_quad_kernel(CompositeArgs a, uint32_t nwg) {
-    static_assert(MODE == 0 || MODE == 1, "tile / live50 rules");
-    constexpr uint32_t R = 64u;  // records per wave batch
-    __shared__ StagedRec srec[4][R];
-    __shared__ uint16_t wlist[4][R];
-    __shared__ uint32_t wfetch[4];
-
-    const uint32_t orig = blockIdx.x;  // (the XCD-aware bin order of composite_kernel)
-    const uint32_t full = nwg & ~31u;
-    const uint32_t kk = orig >> 3;
-    const uint32_t wg = orig < full ? 32u * (kk >> 2) + 4u * (orig & 7u) + (kk & 3u) : orig;
-    const uint32_t per_row = 4u * (uint32_t)a.tiles_x;
-    const int owned_row = (int)(wg / per_row);
-    const uint32_t k4 = wg - (uint32_t)owned_row * per_row;
-    const int bx = (int)(k4 >> 2);
-    const int by = a.rows ? (int)a.rows[owned_row] : owned_row;
-    const int tx = 2 * bx + (int)(k4 & 1u), ty = 2 * by + (int)((k4 >> 1) & 1u);
-    const int width = a.width, height = a.height;
-    const uint32_t bin = (uint32_t)(by * a.tiles_x + bx);
-    uint32_t* const qr = a.qrec ? a.qrec + (size_t)bin * kQrecWords : nullptr;
-    const uint32_t tq = (k4 & 3u) * 4u;
-    const int tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t lane = tid & 63;
-    const bool trunc = PASS == 1 && a.cut_in && a.cut_in[bin] < kDepthInf;
-    const uint32_t tx0 = (uint32_t)(tx * kTile), ty0 = (uint32_t)(ty * kTile);
-    const uint32_t qx0 = tx0 + (wave & 1u) * 8u, qy0 = ty0 + (wave >> 1) * 8u;  // this wave's quadrant
-    const uint32_t lxi = (wave & 1u) * 8u + (lane & 7u), lyi = (wave >> 1) * 8u + (lane >> 3);
-    const int px = (int)(tx0 + lxi);
-    const int py = (int)(ty0 + lyi);
-    const bool inside = px < width && py < height;
-    const float lx = (float)lxi + 0.5f;
-    const float ly = (float)lyi + 0.5f;
-    const float ftx0 = (float)tx0, fty0 = (float)ty0;
-
-    uint2 rg = decode_range(a.ranges[bin]);
-    if (tx0 >= (uint32_t)width || ty0 >= (uint32_t)height) rg.y = rg.x;
-    float T = inside ? 1.0f : 0.0f;
-    float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-    const int orow = a.compact ? owned_row * kBin + (py - by * kBin) : py;
-    const size_t pix = (size_t)py * width + px;
-    bool resumed = false;
-    if constexpr (PASS == 2) {  // only the quadrants the front list left open resume
-        resumed = qr[16u + tq + wave] != 0u;
-        T = 0.0f;
-        if (!resumed) rg.y = rg.x;
-        if (inside && resumed) {
-            const float4 st = a.state[pix];
-            C0 = st.x;
-            C1 = st.y;
-            C2 = st.z;
-            T = st.w;
-        }
-    }
-    auto finished = [&]() -> bool {
-        if constexpr (MODE == 0) return T <= kTSat;
-        else return T < kTMin;
-    };
-    auto body_v = [&](const float4 aa, const float4 bb, const float2 cc) {
-        const float u = __builtin_fmaf(aa.z, lx, __builtin_fmaf(aa.w, ly, aa.x));
-        const float v = __builtin_fmaf(bb.x, lx, __builtin_fmaf(bb.y, ly, aa.y));
-        const float qq = __builtin_fmaf(v, v, u * u);
-        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= kBoxS && qq <= kQMaxS;
-        if (!finished() && covered) {
-            const float alpha = bb.z * gs_gauss2(qq);
-            if constexpr (MODE == 0) {
-                const float sa = alpha * T;
-                C0 = __builtin_fmaf(bb.w, sa, C0);
-                C1 = __builtin_fmaf(cc.x, sa, C1);
-                C2 = __builtin_fmaf(cc.y, sa, C2);
-                T = T - sa;
-            } else {
-                C0 = __builtin_fmaf(bb.w, T, C0);
-                C1 = __builtin_fmaf(cc.x, T, C1);
-                C2 = __builtin_fmaf(cc.y, T, C2);
-                T = T * (1.0f - alpha);
-            }
-        }
-    };
-
-    // each lane loads its own record of the batch (three 16-B loads, 48-B
-    // stride): it stages the record straight from registers, so the chunks
-    // need no LDS round trip and no cross-lane shuffle
-    StagedRec* const ws = srec[wave];
-    const uint32_t last = rg.y > rg.x ? rg.y - 1u : rg.x;
-    float4 rc[3];
-    uint32_t id_next = 0u;
-    auto gather = [&](uint32_t id) {
-        const float4* r = a.rec + (size_t)a.rec_stride * id;
-        rc[0] = r[0];
-        rc[1] = r[1];
-        rc[2] = r[2];
-    };
-    uint32_t fetched = 0u, wend = 0u;
-    if (rg.y > rg.x) {
-        const uint32_t j = rg.x + lane;
-        gather(a.vals[j < last ? j : last]);
-        id_next = a.vals[j + R < last ? j + R : last];
-        fetched = rg.y - rg.x < R ? rg.y - rg.x : R;
-    }
-    for (uint32_t b = rg.x; b < rg.y; b += R) {
-        if (__ballot(!finished()) == 0) break;  // the quadrant is saturated
-        const uint32_t cnt_b = rg.y - b < R ? rg.y - b : R;
-        // stage the lane's record for this tile (scaled conic, offsets at the
-        // tile origin) if its rect reaches this quadrant and its cell mask
-        // does not rule it out
-        bool hit = false;
-        if (lane < cnt_b) {
-            const float4 r0 = rc[0], r1 = rc[1], r2 = rc[2];
-            const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
-            const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
-            const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
-            hit = !(x1 < qx0 || x0 > qx0 + 7u || y1 < qy0 || y0 > qy0 + 7u);
-            if (a.cell_mask && hit) {
-                const uint32_t cm = rect_cell_mask(wlo, whi);
-                const uint32_t dcx = (qx0 >> 3) - (x0 >> 3), dcy = (qy0 >> 3) - (y0 >> 3);
-                if (dcx < 4u && dcy < 4u && ((cm >> (dcy * 4u + dcx)) & 1u)) hit = false;
-            }
-            if (hit) {
-                const float ax = r0.z * kConicScale, ay = r0.w * kConicScale;
-                const float bxs = r1.x * kConicScale, bys = r1.y * kConicScale;
-                const float ex = ftx0 - r0.x, ey = r0.y - fty0;
-                StagedRec& st = ws[lane];
-                st.a = make_float4(__builtin_fmaf(ax, ex, ay * ey), __builtin_fmaf(bxs, ex, bys * ey), ax, -ay);
-                st.b = make_float4(bxs, -bys, r1.z, r1.w);
-                st.c = r2;
-            }
-        }
-        const uint64_t m = __ballot(hit);
-        if (hit) wlist[wave][mbcnt(m)] = (uint16_t)(lane * sizeof(StagedRec));
-        const uint32_t nl = (uint32_t)__popcll(m);
-        // the next batch's records into registers while this one is walked
-        if (b + R < rg.y) {
-            gather(id_next);
-            const uint32_t j = b + 2u * R + lane;
-            id_next = a.vals[j < last ? j : last];
-            const uint32_t left = rg.y - b - R;
-            fetched += left < R ? left : R;
-        }
-        wave_lds_sync();
-        wend = b + cnt_b;
-        uint32_t i = 0;
-        const uint32_t* wl2 = reinterpret_cast<const uint32_t*>(wlist[wave]);
-        uint32_t w2 = nl >= 2 ? wl2[0] : 0u;
-        for (; i + 1 < nl; i += 2) {
-            if (__ballot(!finished()) == 0) break;
-            const StagedRec& p0 = staged_at(ws, w2 & 0xFFFFu);
-            const StagedRec& p1 = staged_at(ws, w2 >> 16);
-            const float4 a0 = p0.a, b0 = p0.b;
-            const float2 c0 = make_float2(p0.c.x, p0.c.y);
-            const float4 a1 = p1.a, b1 = p1.b;
-            const float2 c1 = make_float2(p1.c.x, p1.c.y);
-            if (i + 3 < nl) w2 = wl2[(i >> 1) + 1];
-            body_v(a0, b0, c0);
-            body_v(a1, b1, c1);
-        }
-        if (i < nl && __ballot(!finished()) != 0) {
-            const StagedRec& p = staged_at(ws, wlist[wave][i]);
-            body_v(p.a, p.b, make_float2(p.c.x, p.c.y));
-        }
-        wave_lds_sync();  // (the walk's reads before the next batch's chunk stores)
-    }
-    if (a.fetched) {  // records the tile fetched from HBM: the furthest wave's
-        if (lane == 0) wfetch[wave] = fetched;
-        __syncthreads();
-        if (tid == 0)
-            (void)atomicAdd(a.fetched,
-                            (unsigned long long)max(max(wfetch[0], wfetch[1]), max(wfetch[2], wfetch[3])));
-    }
-    bool open_w = false, keep = false;
-    if constexpr (PASS == 1) {
-        open_w = __ballot(!finished()) != 0;
-        keep = open_w && trunc;
-    }
-    const bool write = inside && (PASS != 2 || resumed);
-    if (write) {
-        if (keep) {
-            a.state[pix] = make_float4(C0, C1, C2, T);
-        } else {
-            const float4 o = make_float4(C0, C1, C2, 1.0f - T);
-            if (a.out_bgra8)
-                a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(o.x, o.y, o.z, o.w);
-            else
-                a.out[(size_t)orow * width + px] = o;
-        }
-    }
-    if constexpr (PASS == 1) {
-        if (lane == 0) {
-            qr[tq + wave] = open_w ? 0xFFFFFFFFu : wend;
-            qr[16u + tq + wave] = keep ? 1u : 0u;
-            if (keep) (void)atomicAdd(a.open_q_count, 1ull);
-        }
-    }
-}
-
-#ifndef GS_COMPOSITE_QUAD
-#define GS_COMPOSITE_QUAD 0  // (1: composite_quad_kernel)
-#endif
-
 template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
@@ -686,11 +478,6 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
         return hipSuccess;
     }
     // t0/t1 (optional) are recorded by the dispatch packet itself
-    if constexpr (GS_COMPOSITE_QUAD > 0 && (MODE == 0 || MODE == 1) && !CAP && SLAB == 0) {
-        hipExtLaunchKernelGGL(composite_quad_kernel<MODE, PASS>, dim3(nwg), dim3(kTileThreads), 0,
-                              st, t0, t1, 0, a, nwg);
-        return hipGetLastError();
-    }
     hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
                           nwg);
     return hipGetLastError();
