@@ -16,13 +16,19 @@ Multi-GPU is STRONG scaling over one global scene: `--gpus N` (without
 torchrun) starts N rank processes itself (torch.distributed.run, one rank per
 GPU, 127.0.0.1) before anything touches a GPU; under torchrun WORLD_SIZE must
 equal --gpus.  value = global splats / frame time (max over ranks).  The
-exact multi-GPU schemes run by default (--scheme all), each timed on its own:
+exact multi-GPU schemes run by default (--scheme all), each timed on its own,
+and `value` is the faster of the two at this world size:
   rows   rank r renders the splat-index shard [r*N/g, (r+1)*N/g) of the global
          scene (generated chunk-wise, so a rank builds only its shard):
          bin-row ownership + all_to_all of projected records + band gather
   bands  SURVEY §8(e)'s fallback: every rank holds the whole scene and
          renders its own bin rows (gs_band_render), then the band gather
-rows and bands are bit-identical to one GPU's frame.  `value` is the rows
+rows and bands are bit-identical to one GPU's frame.  Rows are link-bound at 2
+ranks (about half of every rank's records cross the one xGMI link between
+them) and bands need no exchange, so the headline scheme follows the world
+size; both are reported in `schemes` and the choice in `scheme_choice`.  Rows frames run one at
+a time unless --pipeline-rows 1 (frame k's exchange under frame k-1's render),
+which stays opt-in until a multi-GPU RCCL run of it is recorded.  `value` is the rows
 scheme's, the north star's splat-index sharding (a replicated
 scene must not become the headline of a splat-sharded config); bands are
 reported beside it in `schemes`.  The north star's depth slabs +
@@ -40,6 +46,10 @@ At N=1 the line also carries
                 FETCH_SIZE x 2 + WRITE_SIZE per launch, MI355X_MICROARCH.md
                 §HBM) and VALU-issue fraction (SQ_INSTS_VALU x 2 cycles per
                 wave64 instruction over 1024 SIMDs at 2.4 GHz)
+  settled       the same K frames timed again after 60 more frames (clock
+                ramp), beside the value
+  orbit         the same K frames on an orbiting camera (--orbit-probe), beside
+                the value: the default still camera is depth cuts' best case
   cpu_baseline  the CPU oracle (oracle/gs_oracle.c, OpenMP) on the same scene
                 and camera on all host threads, and on 1 thread over a
                 bounded subset (cpu_baseline_1core)
@@ -109,6 +119,12 @@ def parse():
     ap.add_argument("--scheme", default="all", choices=["rows", "slabs", "bands", "both", "all"],
                     help="N>1: all = rows (exact; value) + bands (exact); slabs = depth slabs + RGBA reduce "
                          "(approximate, outside the 1e-4 tolerance); both = rows + slabs")
+    ap.add_argument("--pipeline-rows", type=int, default=0,
+                    help="N>1: 1 = rows frames pipelined (frame k's exchange under frame k-1's render, a second "
+                         "communicator); opt-in until a multi-GPU RCCL run of it is recorded (ADVICE r4)")
+    ap.add_argument("--orbit-probe", type=int, default=1,
+                    help="N=1, fixed camera: after the settled probe, time the same K frames once more with an "
+                         "orbiting camera (a new view every frame) and report them as 'orbit' (0 = skip)")
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N>1: seconds before a rendezvous or collective that a peer never joins fails")
     a = ap.parse_args()
@@ -181,7 +197,7 @@ def pmc_passes(args):
     if not exe:
         return None, "rocprofv3 not found"
     bench = [sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1", "--settle", "0", "--cpu-baseline", "0",
-             "--pmc", "0", "--no-stage-timing", "--frames-in-flight", "1", "--splats", str(args.splats),
+             "--pmc", "0", "--orbit-probe", "0", "--no-stage-timing", "--frames-in-flight", "1", "--splats", str(args.splats),
              "--width", str(args.width), "--height", str(args.height), "--sh", str(args.sh), "--mode", args.mode,
              "--seed", str(args.seed), "--profile", args.profile]
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
@@ -328,6 +344,7 @@ def main():
                 "note": "the same frames timed again after the value's run and these extra untimed frames"}
 
     schemes = {}
+    orbit_line = None
     if world == 1:
         r = InstancedSplatRenderer(scene, opts)
         r.initialize(local)
@@ -348,6 +365,34 @@ def main():
         drain = None
         ms = timed(step, args.steps, args.warmup)
         settled_line = settled_probe(step, args.steps)
+        if args.camera == "fixed" and args.orbit_probe:
+            # camera sensitivity: the default camera is the
+            # best case for depth cuts (cuts taken two frames back are exact),
+            # so the same K frames are timed once more on an orbiting camera;
+            # beside the value, never as it.  Afterwards the fixed camera's
+            # frames (kernel and stage timing below) run again.
+            ocam = default_camera(W, H)
+            oviews = []
+            for _ in range(args.warmup + args.steps):
+                ocam.orbit(0.01)
+                oviews.append(ocam.getViewMatrix())
+            of = [0]
+
+            def ostep():
+                r.render(oviews[of[0] % len(oviews)], proj, W, H, out=out)
+                of[0] += 1
+
+            oms = timed(ostep, args.steps, args.warmup, settle=0)
+            os_ = r.last_stats()
+            orbit_line = {"ms_per_step": round(oms, 4), "value": round(N / (oms * 1e-3) / 1e6, 2),
+                          "warmup": args.warmup, "steps": args.steps, "pairs": int(os_["pairs"]),
+                          "pairs_sorted": int(os_.get("pairs_sorted", os_["pairs"])),
+                          "open_tiles": int(os_.get("open_tiles", 0)),
+                          "binning": {1: "depth-first", 2: "bin-first"}.get(int(os_.get("binning", 0)), "?"),
+                          "note": "the same K frames on an orbiting camera (0.01 rad per frame about the target), "
+                                  "after the settled probe, with their own warmup; reported beside the value"}
+            for _ in range(args.warmup):  # (back to the fixed camera for the kernel and stage timing)
+                step()
     else:
         from gaussian_splat_amd.distributed import (BandRenderer, HipBandBackend, HipShardBackend, HipSlabBackend,
                                                     ShardedRenderer, SlabRenderer)
@@ -369,15 +414,21 @@ def main():
                 be = HipShardBackend(scene, rank, world, b, opts, local)
                 # two frames in flight: frame k's record exchange (its own
                 # communicator) overlaps frame k-1's render and gather
-                pipe = args.frames_in_flight >= 2
+                pipe = args.frames_in_flight >= 2 and args.pipeline_rows
                 sr = ShardedRenderer(be, rank, world, pipeline=pipe,
                                      exchange_group=dist.new_group(backend=backend) if pipe else None)
             stp = (lambda s_=sr: s_.render(view, proj, W, H, gather=True))
             drn = getattr(sr, "flush", None) if getattr(sr, "pipeline", False) else None
             schemes[sch] = {"ms": timed(stp, args.steps, args.warmup, drain=drn), "handle": be.r, "step": stp,
                             "drain": drn}
-        # the splat-sharded exact scheme is the headline whenever it ran
-        head = "rows" if "rows" in schemes else order[0]
+        # The headline is the faster of the exact schemes that ran (both timed
+        # over the same K frames, both reported in `schemes`): rows (splat-index
+        # shards + record exchange) are link-bound at 2 ranks, where one xGMI
+        # link carries about half of every rank's records, and the replicated
+        # scene's bands need no exchange.  `scheme_choice` names
+        # the rule; `config.parallelism` the scheme.
+        exact = [k for k in ("rows", "bands") if k in schemes]
+        head = min(exact, key=lambda k: schemes[k]["ms"]) if exact else order[0]
         ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
         drain = schemes[head]["drain"]
         settled_line = settled_probe(step, args.steps, drain=drain)
@@ -432,6 +483,7 @@ def main():
             "settle": {"frames": settled["frames"], "ms": round(settled["ms"], 1),
                        "note": "untimed frames before the warmup (--settle), per timed scheme"},
             "settled": settled_line,
+            "orbit": orbit_line,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)"
                     + ("; orbiting camera, a new view every frame" if args.camera == "orbit" else ""),
@@ -451,7 +503,7 @@ def main():
                        ("single GPU, 2 frames in flight (projection/sort of frame k+1 under the composite of frame k)"
                         if args.frames_in_flight == 2 else "single GPU"),
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning,
-                       "two_slab": bool(s0.get("two_slab", 0)), "pairs_sorted": int(s0.get("pairs_sorted", s0["pairs"])),
+                       "depth_cuts": bool(s0.get("cut_frame", 0)), "pairs_sorted": int(s0.get("pairs_sorted", s0["pairs"])),
                        "open_tiles": int(s0.get("open_tiles", 0))},
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
             "timed_kernel_ms": {k: round(v, 4) for k, v in timed_k.items()},
@@ -463,6 +515,9 @@ def main():
             line["comm"] = {"backend": dist.get_backend(), "ranks": dist.get_world_size()}
             line["schemes"] = {k: {"ms_per_step": round(v["ms"], 4), "value": round(N / (v["ms"] * 1e-3) / 1e6, 2)}
                                for k, v in schemes.items()}
+            line["scheme_choice"] = (f"{head}: the faster exact scheme at world size {world} (rows and bands both "
+                                     "timed over the same frames and reported in schemes; both bit-identical to the "
+                                     "1-GPU frame)") if len(exact) > 1 else head
             if "slabs" in line["schemes"]:
                 line["schemes"]["slabs"]["note"] = ("depth slabs + transmittance all_gather + RGBA reduce "
                                                     "(approximate, outside the 1e-4 tolerance: reassociated transmittance product)")

@@ -37,8 +37,8 @@ class GsStats(C.Structure):
                 ("bytes_sort", C.c_int64), ("bytes_ranges", C.c_int64), ("bytes_composite", C.c_int64),
                 ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
                 ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64),
-                ("pairs_sorted", C.c_int64), ("open_tiles", C.c_int64), ("two_slab", C.c_int32),
-                ("depth_cut", C.c_uint32)]
+                ("pairs_sorted", C.c_int64), ("open_tiles", C.c_int64), ("cut_frame", C.c_int32),
+                ("reserved", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -54,9 +54,12 @@ class Options:
     # bin-list build order: "default" (per frame from the previous frame's pair count at this
     # resolution; depth-first on the first frame), "depth_first", "bin_first"
     binning: str = "default"
-    # bin-first frames in two depth slabs, the second only where the first left pixels open
-    # (True) or in one (False, the default: measured faster); the same image
-    depth_split: bool = True  # per-bin depth cuts (gs_options.depth_split): same image, fewer pairs sorted
+    # per-bin depth cuts (gs_options.depth_split; tile/live50 rules, no cap): a frame's
+    # bin lists hold the pairs in front of the depth at which the bin's tiles saturated two frames
+    # back, and a quadrant those lists leave open finishes from its saved state with the rest of
+    # its bin's pairs.  Single-GPU frames and row-scheme rank renders alike.  The same image bit
+    # for bit, fewer pairs sorted; True is the default (False: whole lists)
+    depth_split: bool = True
 
     def to_c(self) -> GsOptions:
         o = GsOptions()

@@ -108,6 +108,20 @@ def build_dropin_app(lib: Path = LIB) -> Path:
     return DROPIN_BIN
 
 
+RCCL_STUB_SRC = ROOT / "tests" / "cpp" / "rccl_stub.hip"
+RCCL_STUB = ROOT / "tests" / "cpp" / "librccl_stub.so"
+
+
+def build_rccl_stub() -> Path:
+    """Test infrastructure: the RCCL entry points as stream-ordered peer copies
+    (tests/cpp/rccl_stub.hip), loaded only through GS_RCCL_LIB by the GPU
+    tests, so the group's RCCL transport runs on a one-GPU box."""
+    if _stale(RCCL_STUB, [RCCL_STUB_SRC]):
+        _run([_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared",
+              str(RCCL_STUB_SRC), "-o", str(RCCL_STUB)])
+    return RCCL_STUB
+
+
 def build_oracle() -> None:
     """Test infrastructure: the C oracle and, when /root/reference exists, oracle/_ref."""
     _run(["make", "-s", "-C", str(ROOT / "oracle"), "-j4"])
@@ -116,6 +130,7 @@ def build_oracle() -> None:
 def build_all(verbose: bool = False) -> Path:
     lib = build_lib(verbose)
     build_dropin_app(lib)
+    build_rccl_stub()
     build_oracle()
     return lib
 

@@ -80,11 +80,19 @@ struct Rccl {
     decltype(&ncclGetErrorString) error_string = nullptr;
     decltype(&ncclCommGetAsyncError) async_error = nullptr;
     decltype(&ncclCommAbort) comm_abort = nullptr;
+    bool shared_devices = false;  // ranks may share a device (the test stub, tests/cpp/rccl_stub.hip)
     bool load(std::string* why) {
         if (so) return true;
-        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            so = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
-            if (so) break;
+        // GS_RCCL_LIB (tests only): the one library to load instead of RCCL,
+        // e.g. the stub that runs this transport's code on a one-GPU box
+        const char* over = std::getenv("GS_RCCL_LIB");
+        if (over && *over) {
+            so = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+        } else {
+            for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+                so = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+                if (so) break;
+            }
         }
         if (!so) {
             *why = std::string("RCCL not loadable: ") + dlerror();
@@ -108,6 +116,9 @@ struct Rccl {
         sym(async_error, "ncclCommGetAsyncError");
         sym(comm_abort, "ncclCommAbort");
         if (!ok) *why = "RCCL: missing symbols";
+        using SharedFn = int (*)();
+        const auto sh = reinterpret_cast<SharedFn>(dlsym(so, "gs_rccl_stub_shared_devices"));
+        shared_devices = sh && sh() == 1;
         return ok;
     }
 };
@@ -676,16 +687,18 @@ gs_status gs_group_initialize(gs_group* g, const int32_t* devices, int32_t trans
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     if (transport != GS_TRANSPORT_AUTO && transport != GS_TRANSPORT_RCCL && transport != GS_TRANSPORT_COPY)
         return gfail(GS_ERR_INVALID_ARG, "bad transport");
-    if (transport == GS_TRANSPORT_RCCL && !distinct)
-        return gfail(GS_ERR_INVALID_ARG, "RCCL needs one device per rank (GS_TRANSPORT_COPY for shared devices)");
     // RCCL is loaded before any rank state exists: AUTO falls back to peer
     // copies when it cannot be loaded, an explicit RCCL request fails cleanly
     if (transport == GS_TRANSPORT_AUTO) {
         std::string why;
         transport = (distinct && g->world > 1 && g_rccl.load(&why)) ? GS_TRANSPORT_RCCL : GS_TRANSPORT_COPY;
     } else if (transport == GS_TRANSPORT_RCCL) {
+        if (!distinct && !std::getenv("GS_RCCL_LIB"))
+            return gfail(GS_ERR_INVALID_ARG, "RCCL needs one device per rank (GS_TRANSPORT_COPY for shared devices)");
         std::string why;
         if (!g_rccl.load(&why)) return gfail(GS_ERR_COMM, why);
+        if (!distinct && !g_rccl.shared_devices)
+            return gfail(GS_ERR_INVALID_ARG, "RCCL needs one device per rank (GS_TRANSPORT_COPY for shared devices)");
     }
     // Per-rank state; on failure the streams and events made here are
     // released again, so a retry starts clean (gs_initialize is idempotent

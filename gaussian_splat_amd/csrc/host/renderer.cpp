@@ -164,7 +164,10 @@ struct gs_handle {
     // cuts: fbtab, fbn, sorted with scratch2; composite stream only).
     // cstate: the open quadrants' pixel states.  kept: per set, the front
     // lists' pairs [set] and the fallback lists' [2 + set] (gs_last_stats).
-    DevBuf qrec, cutbuf, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
+    // cutord: per buffer set, two bin-order tables beside the cut tables
+    // (the same roles and phase): the composite's longest-first dispatch
+    // order (CompositeArgs::order), single-GPU frames only.
+    DevBuf qrec, cutbuf, cutord, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
     uint32_t cut_bins = 0;       // bins per table in cutbuf
     int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
     int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
@@ -173,10 +176,15 @@ struct gs_handle {
     bool cut_pending = false;    // the frame being enqueued is a depth-cut frame (render_frame)
     const uint32_t* cut_in = nullptr;  // (its cuts; null: none yet, every pair in its lists)
     uint32_t* cut_out = nullptr;
+    const uint32_t* ord_in = nullptr;  // (its bin order, valid with cut_in)
+    uint32_t* ord_out = nullptr;
     bool cut_lists = false;      // the frame in `stats` filtered its lists at the cuts (front pairs: kept[set])
     uint32_t pair_cap = 0;       // pair capacity of the set of the last build_bin_lists
     uint32_t* cut_table(int set, int role) const {
         return cutbuf.as<uint32_t>() + (size_t)(2 * set + ((cut_phase[set] + role) & 1)) * cut_bins;
+    }
+    uint32_t* order_table(int set, int role) const {
+        return cutord.as<uint32_t>() + (size_t)(2 * set + ((cut_phase[set] + role) & 1)) * cut_bins;
     }
     void swap_sets() {
         std::swap(rec, alt_rec);
@@ -586,7 +594,8 @@ using ListTail = std::function<gs_status(const uint32_t* sorted_vals)>;
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
                           hipStream_t st, const uint32_t** vals_out, uint64_t* pairs,
-                          const uint32_t* carry_dkey = nullptr, const ListTail* tail = nullptr) {
+                          const uint32_t* carry_dkey = nullptr, const ListTail* tail = nullptr,
+                          hipStream_t tail_st = nullptr) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     const int bits = list_key_bits(U);
     const gs::SortPlan plan = gs::make_sort_plan(bits);
@@ -678,17 +687,18 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     h->order.frame_pairs = P_all;
     if (P_all >= (uint64_t)UINT32_MAX) return fail(GS_ERR_UNSUPPORTED, "more than 2^32-1 (splat,bin) pairs");
     if (P_all > cap) {
-        // the queued lists were no-ops (ranges still empty): grow, queue again
+        // the queued lists were no-ops (ranges still empty): grow, queue again.
+        // The no-op tail (composite, next cuts, fallback lists) may sit on its
+        // own stream: it reads the pair buffers reserve_pairs frees and counts
+        // into the counters cleared below, so it drains first too.
         GS_HIP(hipStreamSynchronize(st));
+        if (tail && tail_st && tail_st != st) GS_HIP(hipStreamSynchronize(tail_st));
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
         pc = cut_frame ? gs::PassCounts{} : pass_counts(h, m, order == nullptr, plan, cap, P);
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
-        if (tail) {  // (the no-op frame's composite counted into these)
-            GS_HIP(hipStreamSynchronize(st));
-            GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));
-        }
+        if (tail) GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));  // (the no-op frame's composite counted into these)
         GS_HIP(enqueue_lists());
         if ((ts = lists_done()) != GS_OK) return ts;
     }
@@ -729,6 +739,7 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
     }
     h->cut_pending = false;
     h->cut_in = h->cut_out = nullptr;
+    h->ord_in = h->ord_out = nullptr;
     if (!cut_frame) {
         h->cut_valid[h->set] = false;
         return GS_OK;
@@ -737,6 +748,7 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         GS_HIP(hipStreamSynchronize(st));
         GS_HIP(hipStreamSynchronize(sp));
         GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
+        GS_HIP(h->cutord.reserve((size_t)T * 4 * 4));
         h->cut_bins = T;
         h->cut_valid[0] = h->cut_valid[1] = false;
     }
@@ -744,6 +756,10 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
     GS_HIP(reserve_after(h->cstate, (size_t)U.width * U.height * 16, st));
     h->cut_in = h->cut_valid[h->set] ? h->cut_table(h->set, 0) : nullptr;
     h->cut_out = h->cut_table(h->set, 1);
+    // (the order tables are written by single-GPU frames only, and a change
+    // of ownership invalidates the cuts, so a valid cut table has its order)
+    h->ord_in = h->cut_in && T <= gs::kOrderMaxBins ? h->order_table(h->set, 0) : nullptr;
+    h->ord_out = T <= gs::kOrderMaxBins ? h->order_table(h->set, 1) : nullptr;
     h->cut_valid[h->set] = false;  // (true again once this frame's composite is queued)
     h->cut_pending = true;
     return GS_OK;
@@ -774,6 +790,10 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
         fb.kept = h->kept.as<uint32_t>() + 2 + h->set;
         fb.ranges = h->ranges.as<uint2>();
     }
+    // the next composite's longest-first bin order (single-GPU frames), from
+    // the quadrant records and the front lists' ranges (before cut_finalize
+    // clears those for the fallback lists)
+    if (!own.owner && h->ord_out) GS_HIP(gs::launch_order_bins(ca.qrec, ca.ranges, T, h->ord_out, sc));
     GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, (uint32_t)U.tiles_x, own, cut_margin(), sc,
                                    fb));
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
@@ -905,6 +925,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             ca.open_q_count = open_counter(h);
             ca.state = h->cstate.as<float4>();
             ca.cut_in = h->cut_in;
+            ca.order = own.dev.owner ? nullptr : h->ord_in;
         }
         // everything that reads the lists, queued before the host waits for P
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
@@ -939,7 +960,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 7, sc);
             return GS_OK;
         };
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey, &tail);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey, &tail, sc);
         if (s != GS_OK) return s;
         h->order.sample_pairs = P;
         if (cutf) {  // this frame's cuts are read by its set's next frame
@@ -987,6 +1008,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.open_q_count = open_counter(h);
         ca.state = h->cstate.as<float4>();
         ca.cut_in = h->cut_in;
+        ca.order = own.dev.owner ? nullptr : h->ord_in;
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
             gs::CompositeArgs c = ca;
             c.vals = sv;
@@ -999,7 +1021,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 7, sc);
             return GS_OK;
         };
-        gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P, sdk, &tail);
+        gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P, sdk, &tail, sc);
         if (s != GS_OK) return s;
         h->cut_phase[h->set] ^= 1;  // this frame's cuts are read by its set's next frame
         h->cut_valid[h->set] = true;
@@ -1066,7 +1088,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_composite = h->stats_fixed_bytes + 4 * Pi * (4 + 48);
     s.records_fetched = -1;
     s.pairs_sorted = Pi;
-    s.two_slab = h->cut_frame ? 1 : 0;
+    s.cut_frame = h->cut_frame ? 1 : 0;
     h->cut_lists = h->cut_frame && h->cut_in;
     // (depth-cut frames with cuts: the first sort pass reads every pair, keeps
     // the front lists' P1; the rest runs on P1 -- set by gs_last_stats)
@@ -1457,7 +1479,7 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
         GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + 2 * h->stats_set, 8, hipMemcpyDeviceToHost));
         h->stats.records_fetched = (int64_t)v;
         h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
-        if (h->stats.two_slab) {
+        if (h->stats.cut_frame) {
             // depth cuts: the front lists' pairs (the first sort pass reads all
             // P, counting and scattering, and writes the kept P1; the second
             // pass and the per-bin sort run on P1); the tiles those lists left

@@ -26,6 +26,14 @@
 
 namespace gs {
 
+#ifdef GS_COMPOSITE_TRACE
+// Debug build only (tools/composite_trace.py): per strip workgroup, its start
+// and end (s_memrealtime, 100 MHz), its bin pair slot and the fetched record
+// count, written with vector stores by lane 0; read by
+// gs_debug_composite_trace, which no product path calls.
+__device__ unsigned long long g_comp_trace[4 * 65536];
+#endif
+
 // MLAB k-buffer (gaussian_splat.metal:201-361): six premultiplied half
 // layers + half depths per pixel in registers, updated per covering fragment
 // in arrival order with the reference's insertion and under-merge, resolved
@@ -338,11 +346,10 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
             const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
             fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
         }
-        // the wave's gathered chunks into their records' slots (raw layout)
+        // the wave's gathered chunks into their records' slots (raw layout):
+        // chunk c of the wave is float4 192 w + c of the slot array
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-            (cp[i] == 0 ? srec[64u * wave + ck[i]].a : cp[i] == 1 ? srec[64u * wave + ck[i]].b
-                                                                   : srec[64u * wave + ck[i]].c) = rc[i];
+        for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(srec)[192u * wave + lane + 64u * (uint32_t)i] = rc[i];
         wave_lds_sync();  // the wave's 64 slots are only touched by this wave until the barrier
         if (b + tid < rg.y) {
             // record (cx, cy, ax, ay) (bx, by, op, r) (g, b, rect_lo, rect_hi)
@@ -467,17 +474,392 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
     }
 }
 
+// Strip composite: the tile and live50 rules (MODE 0/1; no cap, no depth
+// slabs; depth-cut PASS 0/1/2), the bench frame's kernel.  The same contract
+// as composite_kernel, op for op, with more pixels per record read:
+//  - one 256-lane workgroup per half bin (two 16x16 tiles side by side, the
+//    bin's top or bottom row of tiles), so each bin record is gathered and
+//    staged twice per bin instead of four times;
+//  - each wave a 16x8 strip of one tile, two pixels per lane (tile-local
+//    (lx, ly) and (lx + 8, ly): the two 8x8 quadrants of the strip), so one
+//    broadcast read of a staged record (40 B) serves both quadrants and the
+//    inner fma(-A'y, ly, U0) of the coverage test is shared by them;
+//  - per record and wave a 2-bit quadrant selector (from the record's rect
+//    and 8x8 cell mask, as composite_kernel's per-quadrant filter), tested in
+//    scalar registers: a pixel whose quadrant the record cannot reach skips
+//    its coverage test.
+// Staged slot (48 B): a = (Ax', -Ay', Bx', -By'), b = (opacity, r, g, b),
+// c = (U0, V0) at the left tile's origin, then at the right tile's.
+#ifndef GS_COMPOSITE_LPT  // A/B knob: 0 = row-major bin order even when CompositeArgs::order is set
+#define GS_COMPOSITE_LPT 1
+#endif
+#ifndef GS_STRIP_PIPE  // A/B knob: 1 = the walk reads one record ahead (rolling), 0 = two records per step
+#define GS_STRIP_PIPE 1
+#endif
+#ifndef GS_STRIP_WAVES  // A/B knob: waves per SIMD the strip composite is built for
+#define GS_STRIP_WAVES 8
+#endif
+#ifndef GS_STRIP_PAD
+#define GS_STRIP_PAD 0
+#endif
+template <int MODE, int PASS>
+__global__ __launch_bounds__(256, GS_STRIP_WAVES) __attribute__((amdgpu_num_sgpr(GS_COMPOSITE_SGPRS))) void composite_strip_kernel(
+    CompositeArgs a, uint32_t nwg) {
+    static_assert(MODE == 0 || MODE == 1, "strip composite: tile / live50 rules");
+    __shared__ float4 srec[3 * kTileThreads];    // 256 slots of 48 B (raw record, then staged)
+    __shared__ uint16_t wlist[4][kTileThreads + 4];  // per wave: slot byte offset | selector << 14
+    __shared__ uint8_t sqm[kTileThreads];        // per staged record: the 8 quadrants it may reach
+    __shared__ uint32_t sopen[4];
+#if GS_STRIP_PAD  // A/B knob: LDS padding (bytes) that caps the workgroups per CU
+    __shared__ uint32_t lds_pad[GS_STRIP_PAD / 4];
+    if (a.width < 0) lds_pad[blockIdx.x % (GS_STRIP_PAD / 4)] = 0;  // (never: keeps the array)
+#endif
+
+    // XCD-aware remap (as composite_kernel): blocks b and b + 8 share an XCD,
+    // so a bin's two halves (consecutive wg) run on one XCD and share its list
+    // through that L2; bins dealt round-robin over the XCDs.
+    const uint32_t orig = blockIdx.x;
+    const uint32_t full = nwg & ~15u;
+    const uint32_t kk = orig >> 3;
+    const uint32_t wg = orig < full ? 16u * (kk >> 1) + 2u * (orig & 7u) + (kk & 1u) : orig;
+    const uint32_t per_row = 2u * (uint32_t)a.tiles_x;
+    int owned_row, bx, by;
+    const uint32_t half = wg & 1u;  // the bin's top (0) or bottom (1) row of tiles
+    if (GS_COMPOSITE_LPT && a.order && !a.rows) {  // (single-GPU frames: every row owned)
+        const uint32_t ob = a.order[wg >> 1];
+        owned_row = by = (int)(ob / (uint32_t)a.tiles_x);
+        bx = (int)(ob - (uint32_t)by * (uint32_t)a.tiles_x);
+    } else {
+        owned_row = (int)(wg / per_row);
+        bx = (int)((wg - (uint32_t)owned_row * per_row) >> 1);
+        by = a.rows ? (int)a.rows[owned_row] : owned_row;
+    }
+    const int width = a.width, height = a.height;
+    const uint32_t bin = (uint32_t)(by * a.tiles_x + bx);
+    const uint32_t tx0 = (uint32_t)(bx * kBin), ty0 = (uint32_t)(by * kBin) + 16u * half;  // left tile's origin
+    const int tid = threadIdx.x;
+#ifdef GS_COMPOSITE_TRACE
+    const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63;
+    const uint32_t wt = wave >> 1, ws = wave & 1u;  // the wave's tile (left / right) and strip (top / bottom)
+    // quadrant records of depth-cut frames: tile k4 = 2 half + wt of the bin,
+    // quadrants (x half, y half) = (0, ws) and (1, ws): words 4 k4 + 2 ws + {0, 1}
+    uint32_t* const qr = a.qrec ? a.qrec + (size_t)bin * kQrecWords : nullptr;
+    const uint32_t qA = 4u * (2u * half + wt) + 2u * ws;
+    bool resA = false, resB = false;  // (PASS 2) the quadrants left open by the front list
+    if constexpr (PASS == 2) {
+        const uint4 f0 = *reinterpret_cast<const uint4*>(qr + 16u + 8u * half);
+        const uint4 f1 = *reinterpret_cast<const uint4*>(qr + 20u + 8u * half);
+        if ((f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w) == 0u) return;  // (whole workgroup)
+        resA = qr[16u + qA] != 0u;
+        resB = qr[17u + qA] != 0u;
+    }
+    const bool trunc = PASS == 1 && a.cut_in && a.cut_in[bin] < kDepthInf;
+    // this lane's pixels: A = (ttx0 + lxi, py), B = A + (8, 0), ttx0 = tx0 + 16 wt
+    const uint32_t lxi = lane & 7u, lyi = 8u * ws + (lane >> 3);
+    const float lxA = (float)lxi + 0.5f, lxB = (float)lxi + 8.5f, ly = (float)lyi + 0.5f;  // tile-local (exact)
+    const int pxA = (int)(tx0 + 16u * wt + lxi), pxB = pxA + 8, py = (int)(ty0 + lyi);
+    const bool inA = pxA < width && py < height, inB = pxB < width && py < height;
+    const float ftx0 = (float)tx0, ftx1 = (float)(tx0 + 16u), fty0 = (float)ty0;
+
+    uint2 rg = decode_range(a.ranges[bin]);
+    if (tx0 >= (uint32_t)width || ty0 >= (uint32_t)height) rg.y = rg.x;  // both tiles outside the frame
+    // pixels outside the frame start finished (T = 0), see composite_kernel
+    float TA = inA ? 1.0f : 0.0f, TB = inB ? 1.0f : 0.0f;
+    float A0 = 0.0f, A1 = 0.0f, A2 = 0.0f, B0 = 0.0f, B1 = 0.0f, B2 = 0.0f;
+    const size_t pixA = (size_t)py * width + pxA, pixB = pixA + 8;
+    if constexpr (PASS == 2) {
+        TA = 0.0f;
+        TB = 0.0f;
+        if (inA && resA) {
+            const float4 st = a.state[pixA];
+            A0 = st.x, A1 = st.y, A2 = st.z, TA = st.w;
+        }
+        if (inB && resB) {
+            const float4 st = a.state[pixB];
+            B0 = st.x, B1 = st.y, B2 = st.z, TB = st.w;
+        }
+    }
+    auto fin = [](float T) -> bool {
+        if constexpr (MODE == 0) return T <= kTSat;
+        else return T < kTMin;
+    };
+    // One pixel and one record (composite_kernel's body_v): coverage, the
+    // gaussian alpha and the update, the update exec-masked (an uncovered or
+    // finished pixel adds an exact zero).
+    auto pixel = [&](float lx, float tu, float tv, const float4& aa, const float4& bb, float& T, float& C0, float& C1,
+                     float& C2) {
+        const float u = __builtin_fmaf(aa.x, lx, tu);
+        const float v = __builtin_fmaf(aa.z, lx, tv);
+        const float qq = __builtin_fmaf(v, v, u * u);
+        const bool covered = fmaxf(fabsf(u), fabsf(v)) <= kBoxS && qq <= kQMaxS;
+        if (!fin(T) && covered) {
+            const float alpha = bb.x * gs_gauss2(qq);
+            if constexpr (MODE == 0) {
+                const float sa = alpha * T;
+                C0 = __builtin_fmaf(bb.y, sa, C0);
+                C1 = __builtin_fmaf(bb.z, sa, C1);
+                C2 = __builtin_fmaf(bb.w, sa, C2);
+                T = T - sa;
+            } else {
+                C0 = __builtin_fmaf(bb.y, T, C0);
+                C1 = __builtin_fmaf(bb.z, T, C1);
+                C2 = __builtin_fmaf(bb.w, T, C2);
+                T = T * (1.0f - alpha);
+            }
+        }
+    };
+    // a record for both of the wave's quadrants; sel (scalar): bit 0 quadrant
+    // A may be reached, bit 1 quadrant B
+    auto body = [&](const float4& aa, const float4& bb, const float2& cc, uint32_t sel) {
+        const float tu = __builtin_fmaf(aa.y, ly, cc.x);  // fma(-A'y, ly, U0)
+        const float tv = __builtin_fmaf(aa.w, ly, cc.y);  // fma(-B'y, ly, V0)
+        if (sel & 1u) pixel(lxA, tu, tv, aa, bb, TA, A0, A1, A2);
+        if (sel & 2u) pixel(lxB, tu, tv, aa, bb, TB, B0, B1, B2);
+    };
+
+    // Gathers as composite_kernel: wave w loads records 64w..64w+63 of a
+    // batch as 192 adjacent 16-B chunks (lane + 64 i), the next batch in
+    // flight while the current one is composited.
+    const uint32_t last = rg.y > rg.x ? rg.y - 1u : rg.x;
+    float4 rc[3] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f),
+                    make_float4(0.f, 0.f, 0.f, 0.f)};
+    uint32_t id_next = 0;
+    // (the chunk's record and part are recomputed per gather from a lane id
+    // the compiler cannot hoist: kept live across the walk they spilled)
+    auto gather = [&](uint32_t own_id) {
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(ln));
+        ln = __builtin_amdgcn_mbcnt_hi(~0u, ln);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t c = ln + 64u * (uint32_t)i;
+            const uint32_t ck = (c * 43691u) >> 17;  // c / 3 for c < 2^15
+            const uint32_t idk = (uint32_t)__shfl((int)own_id, (int)ck, 64);
+            rc[i] = a.rec[idk * (uint32_t)a.rec_stride + (c - 3u * ck)];
+        }
+    };
+    if (rg.y > rg.x) {
+        const uint32_t j = rg.x + tid;
+        gather(a.vals[j < last ? j : last]);
+        id_next = a.vals[j + kTileThreads < last ? j + kTileThreads : last];
+    }
+    const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;
+    uint32_t fetched = len < (uint32_t)kTileThreads ? len : (uint32_t)kTileThreads;
+    uint32_t wendA = 0u, wendB = 0u;  // (PASS 1) end of the last batch each quadrant walked with an open pixel
+    const uint32_t* const wl2 = reinterpret_cast<const uint32_t*>(wlist[wave]);
+    for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
+        if (b != rg.x) {  // early out (one LDS barrier, as composite_kernel)
+            const bool open = __ballot(!fin(TA) || !fin(TB)) != 0;
+            if (lane == 0) sopen[wave] = open ? 1u : 0u;
+            block_lds_sync();
+            const uint4 o = *reinterpret_cast<const uint4*>(sopen);
+            if ((o.x | o.y | o.z | o.w) == 0u) break;
+        }
+        if (rg.y - b > (uint32_t)kTileThreads) {
+            const uint32_t left = rg.y - b - (uint32_t)kTileThreads;
+            fetched += left < (uint32_t)kTileThreads ? left : (uint32_t)kTileThreads;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) srec[192u * wave + lane + 64u * (uint32_t)i] = rc[i];
+        wave_lds_sync();  // the wave's 64 slots are only touched by this wave until the barrier
+        if (b + tid < rg.y) {
+            // raw (cx, cy, ax, ay) (bx, by, op, r) (g, b, rect_lo, rect_hi),
+            // staged for both tiles (scaled conic, offsets at each tile's origin)
+            float4* st = &srec[3u * tid];
+            const float4 r0 = st[0], r1 = st[1], r2 = st[2];
+            const float ax = r0.z * kConicScale, ay = r0.w * kConicScale;
+            const float bxs = r1.x * kConicScale, bys = r1.y * kConicScale;
+            const float exl = ftx0 - r0.x, exr = ftx1 - r0.x, ey = r0.y - fty0;
+            const float aye = ay * ey, bye = bys * ey;
+            st[0] = make_float4(ax, -ay, bxs, -bys);
+            st[1] = make_float4(r1.z, r1.w, r2.x, r2.y);
+            st[2] = make_float4(__builtin_fmaf(ax, exl, aye), __builtin_fmaf(bxs, exl, bye), __builtin_fmaf(ax, exr, aye),
+                                __builtin_fmaf(bxs, exr, bye));
+            // the 8 quadrants (columns c = 0..3 of 8 px from tx0, rows r = 0..1
+            // from ty0) the rect reaches and the cell mask does not rule out;
+            // bit 4 (c >> 1) + 2 r + (c & 1): wave w's selector is bits 2w, 2w+1
+            const uint32_t wlo = __float_as_uint(r2.z), whi = __float_as_uint(r2.w);
+            const uint32_t lo = rect_coords(wlo, a.cell_mask), hi = rect_coords(whi, a.cell_mask);
+            const int rx0 = (int)(lo & 0xFFFFu) - (int)tx0, rx1 = (int)(hi & 0xFFFFu) - (int)tx0;
+            const int ry0 = (int)(lo >> 16) - (int)ty0, ry1 = (int)(hi >> 16) - (int)ty0;
+            const int cl = max(rx0, 0) >> 3, ch = min(rx1, 31) >> 3;
+            const int rl = max(ry0, 0) >> 3, rh = min(ry1, 15) >> 3;
+            uint32_t cols = rx1 >= 0 && cl <= ch ? (2u << ch) - (1u << cl) : 0u;
+            const uint32_t rows = ry1 >= 0 && rl <= rh ? (2u << rh) - (1u << rl) : 0u;
+            uint32_t ex0 = 0u, ex1 = 0u;  // excluded columns in rows 0 / 1
+            if (a.cell_mask) {
+                const uint32_t cm = rect_cell_mask(wlo, whi);
+                // the rect's cell grid starts at (x0 >> 3, y0 >> 3); column c is
+                // rect cell dx + c, row r rect cell dy + r
+                const int dx = (int)(tx0 >> 3) - (int)((lo & 0xFFFFu) >> 3);
+                const int dy = (int)(ty0 >> 3) - (int)(lo >> 19);
+                auto row_excl = [&](int dcy) -> uint32_t {
+                    if (dcy < 0 || dcy > 3) return 0u;
+                    const uint32_t rb = (cm >> (4 * dcy)) & 0xFu;  // rect cells 0..3 of that row
+                    if (dx >= 4 || dx <= -4) return 0u;
+                    return (dx >= 0 ? rb >> dx : rb << (-dx)) & 0xFu;
+                };
+                ex0 = row_excl(dy);
+                ex1 = row_excl(dy + 1);
+            }
+            auto spread = [](uint32_t c4) { return (c4 & 3u) | ((c4 & 0xCu) << 2); };  // columns -> bits 0,1,4,5
+            const uint32_t qm = ((rows & 1u) ? spread(cols & ~ex0) : 0u) | ((rows & 2u) ? spread(cols & ~ex1) << 2 : 0u);
+            sqm[tid] = (uint8_t)qm;
+        }
+        __syncthreads();
+        {
+            const uint32_t j = b + 2u * kTileThreads + tid;
+            gather(id_next);
+            id_next = a.vals[j < last ? j : last];
+        }
+        const uint32_t cnt_b = rg.y - b < (uint32_t)kTileThreads ? rg.y - b : (uint32_t)kTileThreads;
+        // wave-level compaction of the records reaching an open quadrant of
+        // this strip (index order kept), with their selectors
+        const uint32_t open2 = (__ballot(!fin(TA)) != 0 ? 1u : 0u) | (__ballot(!fin(TB)) != 0 ? 2u : 0u);
+        if constexpr (PASS == 1) {
+            if (open2 & 1u) wendA = b + cnt_b;
+            if (open2 & 2u) wendB = b + cnt_b;
+        }
+        uint32_t nl = 0;
+        if (open2) {
+            for (uint32_t k0 = 0; k0 < cnt_b; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                const uint32_t sel = k < cnt_b ? (sqm[k] >> (2u * wave)) & open2 : 0u;
+                const uint64_t m = __ballot(sel != 0u);
+                if (sel) wlist[wave][nl + mbcnt(m)] = (uint16_t)(k * 48u | sel << 14);
+                nl += (uint32_t)__popcll(m);
+            }
+            // three empty entries (selector 0) after the list: the half pair of an
+            // odd list and the walk's unconditional read-ahead of the next pair
+            if (lane < 3u) wlist[wave][nl + lane] = 0;
+        }
+        wave_lds_sync();  // wlist[wave] is only touched by this wave
+        // two records per step, both records' LDS reads issued before either
+        // body; the next pair of entries is read one step ahead.  The c half
+        // read depends on the wave's tile, so the walk is instantiated per tile.
+        auto walk = [&](auto tile) {
+            constexpr uint32_t kC = 32u + 8u * decltype(tile)::value;
+            const char* base = reinterpret_cast<const char*>(srec);
+            if (nl == 0u) return;
+            auto ld4 = [&](uint32_t o) { return *reinterpret_cast<const float4*>(base + o); };
+            auto ld2 = [&](uint32_t o) { return *reinterpret_cast<const float2*>(base + o); };
+#if GS_STRIP_PIPE
+            // Rolling read-ahead, one record deep: while record i is
+            // composited, record i + 1's reads are in flight (two register
+            // sets, A and B, alternate), so every LDS read has a record's
+            // bodies to hide behind.
+            uint32_t w2 = wl2[0];
+            uint32_t o = w2 & 0x3FFFu;
+            float4 aA = ld4(o), bA = ld4(o + 16u);
+            float2 cA = ld2(o + kC);
+            for (uint32_t i = 0; i < nl; i += 2) {
+                if (__ballot(!fin(TA) || !fin(TB)) == 0) break;
+                const uint32_t e = __builtin_amdgcn_readfirstlane(w2);
+                o = (w2 >> 16) & 0x3FFFu;
+                const float4 aB = ld4(o), bB = ld4(o + 16u);
+                const float2 cB = ld2(o + kC);
+                w2 = wl2[(i >> 1) + 1];  // (past the list: empty entries)
+                body(aA, bA, cA, (e >> 14) & 3u);
+                o = w2 & 0x3FFFu;
+                aA = ld4(o);
+                bA = ld4(o + 16u);
+                cA = ld2(o + kC);
+                body(aB, bB, cB, e >> 30);
+            }
+#else
+            uint32_t w2 = wl2[0];
+            for (uint32_t i = 0; i < nl; i += 2) {
+                if (__ballot(!fin(TA) || !fin(TB)) == 0) break;
+                const uint32_t e = __builtin_amdgcn_readfirstlane(w2);
+                const uint32_t o0 = w2 & 0x3FFFu, o1 = (w2 >> 16) & 0x3FFFu;
+                const float4 a0 = ld4(o0), b0 = ld4(o0 + 16u);
+                const float2 c0 = ld2(o0 + kC);
+                const float4 a1 = ld4(o1), b1 = ld4(o1 + 16u);
+                const float2 c1 = ld2(o1 + kC);
+                if (i + 2 < nl) w2 = wl2[(i >> 1) + 1];
+                body(a0, b0, c0, (e >> 14) & 3u);
+                body(a1, b1, c1, e >> 30);
+            }
+#endif
+        };
+        if (wt) walk(std::integral_constant<uint32_t, 1>{});
+        else walk(std::integral_constant<uint32_t, 0>{});
+    }
+    if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
+#ifdef GS_COMPOSITE_TRACE
+    __syncthreads();
+    if (tid == 0 && blockIdx.x < 65536u) {
+        g_comp_trace[4u * blockIdx.x + 0] = trace_t0;
+        g_comp_trace[4u * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        g_comp_trace[4u * blockIdx.x + 2] = wg;
+        g_comp_trace[4u * blockIdx.x + 3] = fetched;
+    }
+#endif
+    // PASS 1, per quadrant: a pixel still open at the end of a cut list keeps
+    // its state for the fallback lists instead of its final value
+    bool openA = false, openB = false, keepA = false, keepB = false;
+    if constexpr (PASS == 1) {
+        openA = __ballot(!fin(TA)) != 0;
+        openB = __ballot(!fin(TB)) != 0;
+        keepA = openA && trunc;
+        keepB = openB && trunc;
+    }
+    // (pixel positions recomputed from a fresh lane id: kept live across the
+    // loop they cost registers the walk needs)
+    uint32_t ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(ln));
+    ln = __builtin_amdgcn_mbcnt_hi(~0u, ln);
+    const int qx = (int)(tx0 + 16u * wt + (ln & 7u)), qy = (int)(ty0 + 8u * ws + (ln >> 3));
+    const int orow = a.compact ? owned_row * kBin + (qy - by * kBin) : qy;
+    auto store = [&](bool res, bool keep, int px, float C0, float C1, float C2, float T) {
+        if (px >= width || qy >= height || (PASS == 2 && !res)) return;  // (PASS 2: the rest was written by pass 1)
+        const size_t pix = (size_t)qy * width + px;
+        if (keep) {
+            a.state[pix] = make_float4(C0, C1, C2, T);
+        } else if (a.out_bgra8) {
+            a.out_bgra8[(size_t)orow * width + px] = pack_bgra8(C0, C1, C2, 1.0f - T);
+        } else {
+            a.out[(size_t)orow * width + px] = make_float4(C0, C1, C2, 1.0f - T);
+        }
+    };
+    store(resA, keepA, qx, A0, A1, A2, TA);
+    store(resB, keepB, qx + 8, B0, B1, B2, TB);
+    if constexpr (PASS == 1) {
+        if (lane == 0) {
+            qr[qA] = openA ? 0xFFFFFFFFu : wendA;
+            qr[qA + 1u] = openB ? 0xFFFFFFFFu : wendB;
+            qr[16u + qA] = keepA ? 1u : 0u;
+            qr[17u + qA] = keepB ? 1u : 0u;
+            const uint32_t nk = (keepA ? 1u : 0u) + (keepB ? 1u : 0u);
+            if (nk) (void)atomicAdd(a.open_q_count, (unsigned long long)nk);
+        }
+    }
+}
+
+#ifndef GS_COMPOSITE_STRIP  // A/B knob: 0 = the tile/live50 frames on composite_kernel
+#define GS_COMPOSITE_STRIP 1
+#endif
+
 template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
-    const uint32_t nwg = (uint32_t)(4 * a.tiles_x * a.nrows);
+    constexpr bool kStrip = GS_COMPOSITE_STRIP && (MODE == 0 || MODE == 1) && !CAP && SLAB == 0;
+    const uint32_t nwg = (uint32_t)((kStrip ? 2 : 4) * a.tiles_x * a.nrows);
     if (nwg == 0) {  // no owned tiles: the timing events still mark the (empty) stage
         if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
         if (t1 && hipEventRecord(t1, st) != hipSuccess) return hipGetLastError();
         return hipSuccess;
     }
     // t0/t1 (optional) are recorded by the dispatch packet itself
+    if constexpr (kStrip) {
+        hipExtLaunchKernelGGL(composite_strip_kernel<MODE < 2 ? MODE : 0, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0,
+                              t1, 0, a, nwg);
+        return hipGetLastError();
+    }
     hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
                           nwg);
     return hipGetLastError();
@@ -486,6 +868,7 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const bool cap = a.cap > 0;
     if (cap && !a.thr) return hipErrorInvalidValue;
+    if (a.order && (a.rows || a.compact || a.nrows != a.tiles_y)) return hipErrorInvalidValue;  // (whole frames only)
     if (a.pass) {  // depth-cut frames: tile / live50 rules, no cap, no depth slabs (owned rows allowed)
         if (cap || a.slab || (!a.out && !a.out_bgra8) || !a.qrec || !a.state ||
             (mode != 0 && mode != 1) || a.pass > 2 || (a.pass == 1 && !a.open_q_count))
@@ -556,6 +939,61 @@ hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const
                                                              fb);
     return hipGetLastError();
 }
+
+// Longest-first bin order (launch_order_bins): one 1024-lane workgroup, a
+// counting sort of the bins into 128 cost buckets (log2 with two mantissa
+// bits), costliest first.
+__global__ __launch_bounds__(1024) void order_bins_kernel(const uint32_t* __restrict__ qrec,
+                                                          const uint2* __restrict__ ranges, uint32_t nbins,
+                                                          uint32_t* __restrict__ order) {
+    constexpr int kB = 128;
+    __shared__ uint32_t cnt[kB];
+    const uint32_t tid = threadIdx.x;
+    if (tid < kB) cnt[tid] = 0u;
+    __syncthreads();
+    auto bucket = [&](uint32_t b) -> uint32_t {
+        const uint2 rg = decode_range(ranges[b]);
+        const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;  // (empty bins: {~0, 0})
+        const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);
+        uint32_t w = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 v = q[i];
+            w = max(w, max(max(v.x, v.y), max(v.z, v.w)));
+        }
+        const uint32_t cost = w == 0xFFFFFFFFu ? len : (w > rg.x && len ? min(w - rg.x, len) : 0u);
+        if (cost == 0u) return 0u;
+        const uint32_t e = 31u - (uint32_t)__builtin_clz(cost);  // <= 31
+        const uint32_t m = e >= 2u ? (cost >> (e - 2u)) & 3u : (cost << (2u - e)) & 3u;
+        return min(1u + e * 4u + m, (uint32_t)kB - 1u);
+    };
+    for (uint32_t b = tid; b < nbins; b += 1024u) atomicAdd(&cnt[bucket(b)], 1u);
+    __syncthreads();
+    if (tid == 0) {  // exclusive offsets, costliest bucket first
+        uint32_t run = 0u;
+        for (int k = kB - 1; k >= 0; --k) {
+            const uint32_t c = cnt[k];
+            cnt[k] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < nbins; b += 1024u) order[atomicAdd(&cnt[bucket(b)], 1u)] = b;
+}
+
+hipError_t launch_order_bins(const uint32_t* qrec, const uint2* ranges, uint32_t nbins, uint32_t* order,
+                             hipStream_t st) {
+    if (nbins == 0) return hipSuccess;
+    if (!qrec || !ranges || !order || nbins > kOrderMaxBins) return hipErrorInvalidValue;
+    order_bins_kernel<<<1, 1024, 0, st>>>(qrec, ranges, nbins, order);
+    return hipGetLastError();
+}
+
+#ifdef GS_COMPOSITE_TRACE
+extern "C" int gs_debug_composite_trace(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_comp_trace), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st) {
     if (a.cap <= 0 || !a.thr_out) return hipErrorInvalidValue;

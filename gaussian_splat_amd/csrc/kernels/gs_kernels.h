@@ -230,6 +230,13 @@ struct CompositeArgs {
     unsigned long long* open_q_count;
     float4* state;
     const uint32_t* cut_in;   // may be null: no list was cut
+    // Dispatch order of the bins (tile / live50 strip composite, single-GPU
+    // frames; null: row-major): order[p] is the bin of the p-th pair of
+    // workgroups, a permutation of [0, tiles_x * tiles_y) written by
+    // launch_order_bins from an earlier frame's quadrant records, costliest
+    // bins first, so the launch's last workgroups are short ones.  Which
+    // workgroup renders which bin does not change any pixel.
+    const uint32_t* order;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals
@@ -265,6 +272,14 @@ hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
+// Longest-first bin order for the next composite on this buffer set (one
+// workgroup): a bin's cost is the length of list its quadrants walked in the
+// frame that wrote qrec (every pair while a quadrant stayed open), from the
+// lists' ranges; order = the bins by cost, descending, in 128 log-spaced
+// buckets (ties in any order).  nbins <= kOrderMaxBins.
+constexpr uint32_t kOrderMaxBins = 1u << 16;
+hipError_t launch_order_bins(const uint32_t* qrec, const uint2* ranges, uint32_t nbins, uint32_t* order,
+                             hipStream_t st);
 
 // ---- shard.hip (multi-GPU tile-row ownership / depth slabs) ---------------
 constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the projection's record (its first 48 B)

@@ -1,7 +1,8 @@
-// gs_masks.h — the exclusion masks of a visible splat's rect:
-// computed by the preprocess from its record, and again by a receiving rank
-// of the row scheme from the same record fields (shard.hip), so both sides
-// hold the same masks bit for bit (the exchange record has no room for them).
+// gs_masks.h — the exclusion masks of a visible splat's rect,
+// computed once, by the preprocess, from its record.  The row scheme's
+// receiving ranks do not recompute them: the 8x8-cell mask travels in the
+// exchanged 48-B record's rect words and the 32x32-bin mask in the exchanged
+// binning rect lo / hi words (gs_exchange_regions).
 #pragma once
 
 #include "gs_device.h"

@@ -154,6 +154,88 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
     }
 }
 
+// a / b for the small quotients of the emission (a < 2^32, b < 2^16): float
+// reciprocal, then one correction step (the estimate is off by at most one)
+__device__ __forceinline__ uint32_t udiv_est(uint32_t a, uint32_t b) {
+    uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
+    const int64_t r = (int64_t)a - (int64_t)q * b;
+    if (r < 0) --q;
+    else if (r >= (int64_t)b) ++q;
+    return q;
+}
+
+// Position (0..15) of the i-th set bit of a 16-bit mask (i < popcount).
+__device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
+    uint32_t b = 0;
+    uint32_t c = (uint32_t)__builtin_popcount(m & 0xFFu);
+    if (i >= c) { i -= c; m >>= 8; b += 8; }
+    c = (uint32_t)__builtin_popcount(m & 0xFu);
+    if (i >= c) { i -= c; m >>= 4; b += 4; }
+    c = (uint32_t)__builtin_popcount(m & 0x3u);
+    if (i >= c) { i -= c; m >>= 2; b += 2; }
+    return b + (i >= (m & 1u) ? 1u : 0u);
+}
+
+// Wave-cooperative emission of 64 consecutive items' pairs (every bin row
+// owned): the items own the contiguous pair range [off0, off0 + T); lane q of
+// a 64-pair chunk writes pair off0 + q0 + q (coalesced).  Its item: the last
+// lane whose range starts at or before it (start marks in mk, this wave's 64
+// LDS words, an inclusive max-scan); its bin: the (q - start)-th bin of that
+// item's rect in row-major order, minus the excluded bins -- exactly what
+// emit_bin_pairs writes there.  c: the item's pair count (0: none), start:
+// its first pair - off0.  on_pair(g, bin) runs for every pair written (g
+// absolute).
+template <typename F>
+__device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t c, uint32_t start,
+                                          uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
+                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, F&& on_pair) {
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c > 0u ? start + c : 0u), 63);
+    const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u;
+    uint32_t inc = 0;  // with excluded bins (rect <= 4x4 bins): the included ones, bit dy*4 + dx
+    if (r.excl) {
+        const uint32_t rm = (1u << cols) - 1u;
+#pragma unroll
+        for (uint32_t dy = 0; dy < 4u; ++dy)
+            if (dy < rows) inc |= rm << (4u * dy);
+        inc &= ~r.excl;
+    }
+    const uint32_t pa = r.bx0 | (r.by0 << 16), pb = (cols & 0xFFFFu) | (inc << 16);
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
+        wave_lds_sync();  // the last chunk's mark reads are done
+        mk[lane] = 0u;
+        wave_lds_sync();
+        if (c > 0u && start >= q0 && start - q0 < 64u) mk[start - q0] = lane + 1u;
+        wave_lds_sync();
+        uint32_t own1 = wave_scan_dpp<true>(mk[lane]);
+        own1 = own1 > carry ? own1 : carry;
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)own1, 63);
+        const int ol = (int)(own1 > 0u ? own1 - 1u : 0u);
+        const uint32_t o_start = (uint32_t)__shfl((int)start, ol, 64);
+        const uint32_t o_pa = (uint32_t)__shfl((int)pa, ol, 64);
+        const uint32_t o_pb = (uint32_t)__shfl((int)pb, ol, 64);
+        const uint32_t o_val = (uint32_t)__shfl((int)val, ol, 64);
+        const uint32_t o_khi = (uint32_t)__shfl((int)khi, ol, 64);
+        const uint32_t q = q0 + lane;
+        if (q < T) {
+            const uint32_t li = q - o_start, oinc = o_pb >> 16, ocols = o_pb & 0xFFFFu;
+            uint32_t dy, dx;
+            if (oinc) {
+                const uint32_t b = nth_bit16(oinc, li);
+                dy = b >> 2;
+                dx = b & 3u;
+            } else {
+                dy = udiv_est(li, ocols);
+                dx = li - dy * ocols;
+            }
+            const uint32_t bin = ((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx;
+            keys[off0 + q] = o_khi | bin;
+            vals[off0 + q] = o_val;
+            on_pair(off0 + q, bin);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }  // LDS bank spread
 
 // Down-sweep fused with the duplicate: the block's pair offsets are scanned
@@ -166,6 +248,9 @@ __device__ __forceinline__ uint32_t pad32(uint32_t i) { return i + (i >> 5); }  
 #define GS_DUP_THREADS 1024
 #endif
 constexpr int kDupThreads = GS_DUP_THREADS;          // 16 waves: many waves to hide the pair stores
+#ifndef GS_DUP_COOP  // A/B knob: 1 = wave-cooperative emission when every bin row is owned
+#define GS_DUP_COOP 1
+#endif
 constexpr int kDupIpt = kScanItems / kDupThreads;    // 4 items per lane
 
 // Exclusive scan over a kDupThreads-lane workgroup (LDS-only barriers).
@@ -199,6 +284,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
+    __shared__ uint32_t mk[kDupThreads / 64][64];        // coop_emit's start marks, per wave
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
@@ -251,6 +337,31 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // without its key re-read): the block's pairs are contiguous from its
     // partial, so its first kDupCountTiles tiles count in LDS
     const uint32_t t_lo = pc.C ? (uint32_t)(part / pc.tile) : 0u;
+    auto count = [&](uint32_t g, uint32_t bin) {  // (pc.C) the pair's digit into its sort tile's counts
+        const uint32_t t = udiv_est(g, pc.tile), d = bin & pc.mask;
+        if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
+        else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
+    };
+    if (GS_DUP_COOP && !src.own.owner) {
+        // wave-cooperative emission (every bin row owned): each wave's 64
+        // consecutive items of a round own one contiguous pair run, written
+        // 64 pairs per step by all lanes, so a large splat does not hold its
+        // wave's other lanes idle (coop_emit; the same pairs at the same
+        // offsets as the per-lane loop below)
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+#pragma unroll
+        for (int k = 0; k < kDupIpt; ++k) {
+            const uint32_t i = k * kDupThreads + tid, j = blk + i;
+            const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);  // (items past n: the empty rect)
+            const uint32_t c = j < n && !r.empty ? rect_tile_count(rlo[k], rhi[k], src.own, src.masked) : 0u;
+            const uint32_t off = st[pad32(i)];
+            const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
+            const uint32_t khi = dkey ? dk[k] << bin_bits : 0u;
+            const uint32_t val = order ? ord[k] : j;
+            if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, count);
+            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, [](uint32_t, uint32_t) {});
+        }
+    } else
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid, j = blk + i;
@@ -346,28 +457,6 @@ __global__ __launch_bounds__(256) void duplicate_kernel(CountSrc src, uint32_t n
     emit_bin_pairs(r, tiles_x, src.own, dks ? dks[j] << bin_bits : 0u, order ? order[j] : j, offsets[j], keys, vals);
 }
 
-// a / b for the small quotients of the emission (a < 2^32, b < 2^16): float
-// reciprocal, then one correction step (the estimate is off by at most one)
-__device__ __forceinline__ uint32_t udiv_est(uint32_t a, uint32_t b) {
-    uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
-    const int64_t r = (int64_t)a - (int64_t)q * b;
-    if (r < 0) --q;
-    else if (r >= (int64_t)b) ++q;
-    return q;
-}
-
-// Position (0..15) of the i-th set bit of a 16-bit mask (i < popcount).
-__device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
-    uint32_t b = 0;
-    uint32_t c = (uint32_t)__builtin_popcount(m & 0xFFu);
-    if (i >= c) { i -= c; m >>= 8; b += 8; }
-    c = (uint32_t)__builtin_popcount(m & 0xFu);
-    if (i >= c) { i -= c; m >>= 4; b += 4; }
-    c = (uint32_t)__builtin_popcount(m & 0x3u);
-    if (i >= c) { i -= c; m >>= 2; b += 2; }
-    return b + (i >= (m & 1u) ? 1u : 0u);
-}
-
 // Depth-ordered duplicate, wave-cooperative (every bin row owned): in depth
 // order the splats' sizes follow their depth, so one splat per lane leaves
 // most lanes idle behind a few large near splats.  A wave's 64 splats own the
@@ -398,50 +487,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     const BinRect r = bin_rect(lo, hi, src.masked);
     const uint32_t c = rect_tile_count(lo, hi, src.own, src.masked);
     const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
-    const uint32_t start = off - off0;
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c > 0u ? start + c : 0u), 63);
-    const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u;
-    uint32_t inc = 0;  // with excluded bins (rect <= 4x4 bins): the included ones, bit dy*4 + dx
-    if (r.excl) {
-        const uint32_t rm = (1u << cols) - 1u;
-#pragma unroll
-        for (uint32_t dy = 0; dy < 4u; ++dy)
-            if (dy < rows) inc |= rm << (4u * dy);
-        inc &= ~r.excl;
-    }
-    const uint32_t pa = r.bx0 | (r.by0 << 16), pb = (cols & 0xFFFFu) | (inc << 16);
-    uint32_t carry = 0;
-    for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
-        wave_lds_sync();  // the last chunk's mark reads are done
-        mk[wave][lane] = 0u;
-        wave_lds_sync();
-        if (c > 0u && start >= q0 && start - q0 < 64u) mk[wave][start - q0] = lane + 1u;
-        wave_lds_sync();
-        uint32_t own1 = wave_scan_dpp<true>(mk[wave][lane]);
-        own1 = own1 > carry ? own1 : carry;
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)own1, 63);
-        const int ol = (int)(own1 > 0u ? own1 - 1u : 0u);
-        const uint32_t o_start = (uint32_t)__shfl((int)start, ol, 64);
-        const uint32_t o_pa = (uint32_t)__shfl((int)pa, ol, 64);
-        const uint32_t o_pb = (uint32_t)__shfl((int)pb, ol, 64);
-        const uint32_t o_val = (uint32_t)__shfl((int)val, ol, 64);
-        const uint32_t o_khi = dks ? (uint32_t)__shfl((int)khi, ol, 64) : 0u;
-        const uint32_t q = q0 + lane;
-        if (q < T) {
-            const uint32_t li = q - o_start, oinc = o_pb >> 16, ocols = o_pb & 0xFFFFu;
-            uint32_t dy, dx;
-            if (oinc) {
-                const uint32_t b = nth_bit16(oinc, li);
-                dy = b >> 2;
-                dx = b & 3u;
-            } else {
-                dy = udiv_est(li, ocols);
-                dx = li - dy * ocols;
-            }
-            keys[off0 + q] = o_khi | (((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx);
-            vals[off0 + q] = o_val;
-        }
-    }
+    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, [](uint32_t, uint32_t) {});
 }
 
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,

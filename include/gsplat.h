@@ -77,8 +77,9 @@ typedef struct gs_options {
                               at a resolution goes depth-first), 1 = depth-first (global depth
                               sort of the splats, then binning), 2 = bin-first (bin lists in
                               arrival order, then a stable per-bin depth sort).  DESIGN.md §1 */
-    int32_t depth_split;   /* per-bin depth cuts (single-GPU frames, modes
-                              tile/live50, no cap): 1 (gs_default_options) = a frame's bin lists
+    int32_t depth_split;   /* per-bin depth cuts (modes tile/live50, no cap;
+                              single-GPU frames and the row scheme's rank renders,
+                              gs_shard_render, alike): 1 (gs_default_options) = a frame's bin lists
                               hold only the pairs at or in front of their bin's cut, the depth at
                               which the bin's tiles saturated in the previous frame on the same
                               buffer set, plus a margin; a tile those lists leave open finishes
@@ -130,12 +131,12 @@ typedef struct gs_stats {
        depth-cut frames, gs_options.depth_split: the front lists' pairs plus
        the fallback lists'), the 8x8-pixel quadrants the front lists left
        open (open_tiles), and
-       two_slab = 1 for a depth-cut frame.  Read with records_fetched.
-       depth_cut: unused (0). */
+       cut_frame = 1 for a depth-cut frame.  Read with records_fetched.
+       reserved: 0. */
     int64_t pairs_sorted;
     int64_t open_tiles;
-    int32_t two_slab;
-    uint32_t depth_cut;
+    int32_t cut_frame;
+    uint32_t reserved;
 } gs_stats;
 
 typedef struct gs_handle gs_handle;

@@ -91,7 +91,7 @@ def test_depth_cuts_bitexact(built, n, w, h, mode, sh, scale, path, binning):
         b = whole.render_host(V, P, w, h)
         assert _bits(a, b) == 0, k
         st, so = cut.last_stats(), whole.last_stats()
-        assert st["two_slab"] == 1 and so["two_slab"] == 0
+        assert st["cut_frame"] == 1 and so["cut_frame"] == 0
         # (front lists: dkey <= cut; fallback lists: a subset of the rest)
         assert st["pairs"] == so["pairs"] and st["pairs_sorted"] <= st["pairs"]
         assert 0 <= st["open_tiles"] <= 16 * st["tiles"]  # (8x8 quadrants left open)
@@ -183,7 +183,7 @@ def test_depth_cuts_pipelined_camera_path(built, binning):
     torch.cuda.synchronize()
     for k, o in enumerate(outs):
         assert _bits(o.cpu().numpy(), refs[k // 3]) == 0, k
-    assert r.last_stats()["two_slab"] == 1
+    assert r.last_stats()["cut_frame"] == 1
 
 
 _CHILD = r"""
@@ -196,7 +196,7 @@ opened = 0
 for V, P in _path(640, 360, "orbit", 8):
     a = cut.render_host(V, P, 640, 360); b = whole.render_host(V, P, 640, 360)
     st = cut.last_stats()
-    assert st["two_slab"] == 1 and _bits(a, b) == 0, (st, _bits(a, b))
+    assert st["cut_frame"] == 1 and _bits(a, b) == 0, (st, _bits(a, b))
     opened += st["open_tiles"]
 print("ok", st["pairs"], st["pairs_sorted"], opened)
 """
@@ -247,7 +247,7 @@ def test_depth_cuts_virtual_ranks(built, world, w, h, binning, path, table):
         assert _bits(a, ref.render_host(V, P, w, h)) == 0, k
         for be in vs.backends:
             st = be.r.last_stats()
-            assert (st["two_slab"] == 1 or st["pairs"] == 0) and st["pairs_sorted"] <= st["pairs"], (k, be.rank, st)
+            assert (st["cut_frame"] == 1 or st["pairs"] == 0) and st["pairs_sorted"] <= st["pairs"], (k, be.rank, st)
             saved[be.rank] = st["pairs"] - st["pairs_sorted"]
     if dense:  # (the last frame)
         assert min(saved) > 0, saved

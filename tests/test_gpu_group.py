@@ -2,7 +2,8 @@
 §8(b)/(e)).  On a one-GPU box the ranks are virtual (devices [0, 0, ...],
 peer-copy transport): the same gs_shard_* / gs_slab_* steps and buffers as
 on 8 GPUs, with hipMemcpyPeerAsync in place of RCCL.  The RCCL transport
-runs when the box has two or more GPUs.
+runs on real devices when the box has two or more GPUs, and on one GPU
+through the test stub of its entry points (test_group_rccl_stub_bitexact).
 
 Bar: the bin-row scheme is bit-identical to the 1-GPU frame; the depth-slab
 scheme is bit-identical to the Python virtual-slab path (same passes, same
@@ -109,6 +110,70 @@ def test_group_rccl_two_gpus(built):
         else:
             check_slab_frame(got, ref)
         g.close()
+
+
+_STUB_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import orbit_views
+from gaussian_splat_amd import InstancedSplatRenderer, Options, ShardedGroup
+from gaussian_splat_amd import scene as S
+
+def run(world, scheme, mode, sh, W, H, n, seed):
+    sc = S.activate(S.synthetic_raw(n, seed=seed, aspect=W / H, rest=sh > 0), sh)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    frames = {}
+    for tr in ("rccl", "copy"):
+        if scheme == "bands":
+            g = ShardedGroup(r, world, replicated=True)
+            g.initialize([0] * world, tr)
+        else:
+            g = ShardedGroup(r, world)
+            g.initialize([0] * world, tr)
+            g.set_scheme(scheme)
+        assert g.transport == tr, (g.transport, tr)
+        frames[tr] = [g.render_host(V, P, W, H) for V, P in orbit_views(W, H, 2)]
+        g.close()
+    for (V, P), a, b in zip(orbit_views(W, H, 2), frames["rccl"], frames["copy"]):
+        nd = int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32)))
+        assert nd == 0, (world, scheme, "rccl vs copy", nd)
+        if scheme != "slabs":  # rows and bands: the 1-GPU frame
+            ref = r.render_host(V, P, W, H)
+            assert int(np.count_nonzero(a.view(np.uint32) != ref.view(np.uint32))) == 0, (world, scheme, "vs 1 GPU")
+    print("ok", world, scheme, mode, sh)
+
+run(2, "rows", "tile", 3, 640, 400, 60000, 111)
+run(3, "rows", "live50", 0, 960, 540, 80000, 112)
+run(2, "slabs", "tile", 0, 640, 400, 60000, 113)
+run(3, "slabs", "live50", 3, 640, 400, 60000, 114)
+run(2, "bands", "tile", 3, 640, 400, 60000, 115)
+"""
+
+
+def test_group_rccl_stub_bitexact(built):
+    """The group's RCCL transport (grouped ncclSend/ncclRecv all-to-all and
+    band gather, ncclAllReduce / ncclAllGather / ncclReduce of the slab
+    scheme) on a one-GPU box: GS_RCCL_LIB points the group's dlopen at the
+    test stub (tests/cpp/rccl_stub.hip: the same entry points as
+    stream-ordered peer copies, ranks sharing device 0).  Every frame equals
+    the copy transport's bit for bit, and rows and bands the 1-GPU frame.
+    Its own process: RCCL is resolved once per process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from gaussian_splat_amd.build import RCCL_STUB
+    root = Path(__file__).resolve().parents[1]
+    assert RCCL_STUB.exists(), "build() makes tests/cpp/librccl_stub.so"
+    env = dict(os.environ, GS_RCCL_LIB=str(RCCL_STUB))
+    p = subprocess.run([sys.executable, "-c", _STUB_SCRIPT, str(root)], env=env, capture_output=True, text=True,
+                       timeout=170)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert p.stdout.count("ok ") == 5, p.stdout
 
 
 def test_group_bounded_wait(built):

@@ -121,3 +121,20 @@ def test_comm_release_rule_aborts_each_communicator_once(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "comm_set: ok" in r.stdout
+
+
+def test_rccl_stub_exports_every_resolved_symbol(built):
+    """The test-only RCCL stub (tests/cpp/rccl_stub.hip, loaded by the GPU
+    suite through GS_RCCL_LIB) defines every entry point the group resolves
+    from librccl (csrc/host/group.cpp, Rccl::load), plus its shared-device
+    marker; nothing in the product links it."""
+    import subprocess
+
+    from gaussian_splat_amd.build import RCCL_STUB
+    src = (ROOT / "gaussian_splat_amd" / "csrc" / "host" / "group.cpp").read_text()
+    wanted = set(re.findall(r'sym\(\w+, "(nccl\w+)"\)', src))
+    assert len(wanted) >= 12, wanted
+    out = subprocess.run(["nm", "-D", "--defined-only", str(RCCL_STUB)], capture_output=True, text=True, check=True)
+    have = {ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln}
+    assert wanted <= have, wanted - have
+    assert "gs_rccl_stub_shared_devices" in have
