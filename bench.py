@@ -387,7 +387,7 @@ def main():
             orbit_line = {"ms_per_step": round(oms, 4), "value": round(N / (oms * 1e-3) / 1e6, 2),
                           "warmup": args.warmup, "steps": args.steps, "pairs": int(os_["pairs"]),
                           "pairs_sorted": int(os_.get("pairs_sorted", os_["pairs"])),
-                          "open_tiles": int(os_.get("open_tiles", 0)),
+                          "open_tiles": int(os_.get("open_tiles", 0)), "cut_dilate": int(os_.get("cut_dilate", 0)),
                           "binning": {1: "depth-first", 2: "bin-first"}.get(int(os_.get("binning", 0)), "?"),
                           "note": "the same K frames on an orbiting camera (0.01 rad per frame about the target), "
                                   "after the settled probe, with their own warmup; reported beside the value"}
@@ -504,7 +504,7 @@ def main():
                         if args.frames_in_flight == 2 else "single GPU"),
                        "pairs": int(s0["pairs"]), "visible": int(s0["visible"]), "binning": binning,
                        "depth_cuts": bool(s0.get("cut_frame", 0)), "pairs_sorted": int(s0.get("pairs_sorted", s0["pairs"])),
-                       "open_tiles": int(s0.get("open_tiles", 0))},
+                       "open_tiles": int(s0.get("open_tiles", 0)), "cut_dilate": int(s0.get("cut_dilate", 0))},
             "stages": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in st.items()},
             "timed_kernel_ms": {k: round(v, 4) for k, v in timed_k.items()},
             "timed_kernel_note": (f"dispatch-packet events on {n_co} frames run as the timed ones, after them "

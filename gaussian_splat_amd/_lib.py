@@ -38,7 +38,7 @@ class GsStats(C.Structure):
                 ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
                 ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64),
                 ("pairs_sorted", C.c_int64), ("open_tiles", C.c_int64), ("cut_frame", C.c_int32),
-                ("reserved", C.c_uint32)]
+                ("cut_dilate", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

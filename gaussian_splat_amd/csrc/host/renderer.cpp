@@ -43,6 +43,10 @@ gs_status fail(gs_status s, const std::string& msg) {
                         std::string(#expr) + ": " + hipGetErrorString(e_));                        \
     } while (0)
 
+#ifndef GS_DUP_FILTER_COUNT  // A/B knob: 1 = a depth-cut frame's duplicate counts the filtered pass's digits
+#define GS_DUP_FILTER_COUNT 1
+#endif
+
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -167,7 +171,14 @@ struct gs_handle {
     // cutord: per buffer set, two bin-order tables beside the cut tables
     // (the same roles and phase): the composite's longest-first dispatch
     // order (CompositeArgs::order), single-GPU frames only.
-    DevBuf qrec, cutbuf, cutord, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
+    // cutdil: per set, the dilated copy of the cut table a moving camera's
+    // frame reads (cut_r[set] > 0); cut_r: the set's dilation radius in bins,
+    // raised while its frames leave quadrants open (the counts come back in
+    // host_total[6 + set], written by cut_finalize) and lowered again after
+    // kCutCalm frames with none.
+    DevBuf qrec, cutbuf, cutord, cutdil, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
+    int cut_r[2] = {0, 0};
+    int cut_calm[2] = {0, 0};
     uint32_t cut_bins = 0;       // bins per table in cutbuf
     int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
     int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
@@ -368,11 +379,24 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int n
     const double P = known ? (double)o.frame_pairs * (double)m / (double)o.n : 0.0;  // pairs scale with items
     o.n = (int64_t)m;  // items of this frame (the scan that follows reads its P)
     if (!known) return false;
-    const double W = o.wmax_pairs > 0 ? (double)o.wmax * P / (double)o.wmax_pairs : 0.07 * P;
     const double Ps = cuts ? 0.3 * P : P;             // pairs through the per-bin sort
     const double f = cuts ? 0.0 : o.long_share;      // (front lists fit LDS)
     const double bins = nrows >= 0 ? (double)nrows * U.tiles_x : (double)T;
-    const double bin_ps = 75.0 * W + 6.0 * Ps * (1.0 - f) + 20.0 * Ps * f + 4900.0 * bins;
+    // The index-order duplicate: every bin row owned (nrows < 0), it emits
+    // wave-cooperatively (scan.hip coop_emit), so its cost follows the pairs
+    // and the splats (round 5: 68 / 83 / 658 us at 1080p / heavy-tailed
+    // 1080p / 50M @4K, 12.6 / 18.1 / 188M pairs); with an owner table, one
+    // splat per lane, its cost follows the wave-max work W the fused
+    // preprocess measures (round 4: 67 / 354 / 1003 us against W = 0.73M /
+    // 3.53M / 15.9M).
+    double dup_ps;
+    if (nrows < 0) {
+        dup_ps = 2.6 * P + 3.0 * (double)m;
+    } else {
+        const double W = o.wmax_pairs > 0 ? (double)o.wmax * P / (double)o.wmax_pairs : 0.07 * P;
+        dup_ps = 75.0 * W;
+    }
+    const double bin_ps = dup_ps + 6.0 * Ps * (1.0 - f) + 20.0 * Ps * f + 4900.0 * bins;
     const double depth_ps = 21.0 * (double)m + 4.7 * P;
     return bin_ps < depth_ps;
 }
@@ -394,6 +418,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
         GS_HIP(hipHostMalloc((void**)&h->host_total, 64, hipHostMallocMapped | hipHostMallocCoherent));
         GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
+        h->host_total[6] = h->host_total[7] = ~0ull;  // (the sets' open-quadrant counts: none yet)
     }
     if (!h->seg_sample.ptr) {
         GS_HIP(h->seg_sample.reserve(16));
@@ -619,7 +644,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         flt.bmask = (1u << bits) - 1u;
         flt.dshift = bits;
         flt.kept = h->kept.as<uint32_t>() + h->set;
-        pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
+        pc.cut = h->cut_in;  // (the duplicate counts only the pairs the filtered first pass keeps)
+#if !GS_DUP_FILTER_COUNT
+        pc = gs::PassCounts{};
+#endif
     }
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
@@ -696,7 +724,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
-        pc = cut_frame ? gs::PassCounts{} : pass_counts(h, m, order == nullptr, plan, cap, P);
+        pc = pass_counts(h, m, order == nullptr, plan, cap, P);
+        if (cut_frame) pc.cut = h->cut_in;
+#if !GS_DUP_FILTER_COUNT
+        if (cut_frame) pc = gs::PassCounts{};
+#endif
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         if (tail) GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));  // (the no-op frame's composite counted into these)
         GS_HIP(enqueue_lists());
@@ -718,6 +750,9 @@ hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
 
 // Depth cuts apply to this frame's composite rule and size:
 // tile / live50 rules, no fragment cap, the depth key above the bin id.
+constexpr int kCutDilateMax = 4;  // bins (a 9x9 neighbourhood)
+constexpr int kCutCalm = 8;       // frames with no open quadrant before the radius drops by one
+
 bool cut_rule(const gs_handle* h, const gs::FrameUniforms& U) {
     return h->opt.cap == 0 && (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) &&
            list_key_bits(U) + gs::kDepthBits <= 32;
@@ -756,6 +791,39 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
     GS_HIP(reserve_after(h->cstate, (size_t)U.width * U.height * 16, st));
     h->cut_in = h->cut_valid[h->set] ? h->cut_table(h->set, 0) : nullptr;
     h->cut_out = h->cut_table(h->set, 1);
+    // Dilation (a moving camera): a bin's content moves between the frame that
+    // left its cut and this one, so a quadrant whose new content saturates
+    // deeper is left open and finishes from the fallback lists, whose first
+    // sort pass reads every pair of the frame.  While the set's frames leave
+    // quadrants open, its cuts are dilated: each bin reads the deepest cut
+    // within cut_r bins of it (a still camera leaves none open: r stays 0).
+    {
+        const int S = h->set;
+        const uint64_t opened = h->host_total ? h->host_total[6 + S] : ~0ull;
+        if (h->host_total) h->host_total[6 + S] = ~0ull;  // (consumed; ~0: no new count since)
+        if (opened != ~0ull) {
+            if (opened > 0) {
+                h->cut_r[S] = std::min(h->cut_r[S] + 1, kCutDilateMax);
+                h->cut_calm[S] = 0;
+            } else if (h->cut_r[S] > 0 && ++h->cut_calm[S] >= kCutCalm) {
+                --h->cut_r[S];
+                h->cut_calm[S] = 0;
+            }
+        }
+        static const char* fixed_r = std::getenv("GS_CUT_DILATE");  // (A/B: a fixed radius)
+        if (fixed_r) h->cut_r[S] = std::max(0, std::atoi(fixed_r));
+        if (h->cut_in && h->cut_r[S] > 0) {
+            if (h->cutdil.bytes < (size_t)2 * T * 4) {  // (a composite may still read the other set's table)
+                GS_HIP(hipStreamSynchronize(st));
+                GS_HIP(hipStreamSynchronize(sp));
+                GS_HIP(h->cutdil.reserve((size_t)2 * T * 4));
+            }
+            uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)S * T;
+            GS_HIP(gs::launch_cut_dilate(h->cut_in, d, (uint32_t)U.tiles_x, (uint32_t)U.tiles_y, h->cut_r[S], sp));
+            h->cut_in = d;
+            h->stats.cut_dilate = (uint32_t)h->cut_r[S];
+        }
+    }
     // (the order tables are written by single-GPU frames only, and a change
     // of ownership invalidates the cuts, so a valid cut table has its order)
     h->ord_in = h->cut_in && T <= gs::kOrderMaxBins ? h->order_table(h->set, 0) : nullptr;
@@ -789,6 +857,7 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
         fb.n = h->fbn.as<uint32_t>();
         fb.kept = h->kept.as<uint32_t>() + 2 + h->set;
         fb.ranges = h->ranges.as<uint2>();
+        if (h->dev_total) fb.host_open = reinterpret_cast<unsigned long long*>(h->dev_total) + 6 + h->set;
     }
     // the next composite's longest-first bin order (single-GPU frames), from
     // the quadrant records and the front lists' ranges (before cut_finalize
@@ -1423,7 +1492,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             fuse.nb = nb;
             fuse.fill = h->ranges.as<uint2>();
             fuse.nfill = T;
-            if (h->cut_in) h->fused_prep.pc = gs::PassCounts{};  // (the filtered first pass counts its own digits)
+            h->fused_prep.pc.cut = h->cut_in;  // (with cuts: the duplicate counts only the pairs the filter keeps)
+#if !GS_DUP_FILTER_COUNT
+            if (h->cut_in) h->fused_prep.pc = gs::PassCounts{};
+#endif
             fuse.zero = h->fused_prep.pc.C;
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
             h->fused_prep.ok = true;

@@ -493,6 +493,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
 #ifndef GS_COMPOSITE_LPT  // A/B knob: 0 = row-major bin order even when CompositeArgs::order is set
 #define GS_COMPOSITE_LPT 1
 #endif
+#ifndef GS_STRIP_PRIO  // A/B knob: 1 = issue priority falls with the batches a workgroup has walked
+#define GS_STRIP_PRIO 0
+#endif
 #ifndef GS_STRIP_PIPE  // A/B knob: 1 = the walk reads one record ahead (rolling), 0 = two records per step
 #define GS_STRIP_PIPE 1
 #endif
@@ -651,6 +654,18 @@ __global__ __launch_bounds__(256, GS_STRIP_WAVES) __attribute__((amdgpu_num_sgpr
     uint32_t wendA = 0u, wendB = 0u;  // (PASS 1) end of the last batch each quadrant walked with an open pixel
     const uint32_t* const wl2 = reinterpret_cast<const uint32_t*>(wlist[wave]);
     for (uint32_t b = rg.x; b < rg.y; b += kTileThreads) {
+#if GS_STRIP_PRIO
+        // (A/B) progress-ordered issue priority: a workgroup's waves drop
+        // priority as they walk batches, so late-started workgroups are not
+        // starved behind older ones (age arbitration) into a long drain
+        {
+            const uint32_t nb = (b - rg.x) / kTileThreads;
+            if (nb == 0) __builtin_amdgcn_s_setprio(3);
+            else if (nb == 2) __builtin_amdgcn_s_setprio(2);
+            else if (nb == 4) __builtin_amdgcn_s_setprio(1);
+            else if (nb == 6) __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         if (b != rg.x) {  // early out (one LDS barrier, as composite_kernel)
             const bool open = __ballot(!fin(TA) || !fin(TB)) != 0;
             if (lane == 0) sopen[wave] = open ? 1u : 0u;
@@ -899,6 +914,7 @@ __global__ __launch_bounds__(256) void cut_finalize_kernel(const uint32_t* __res
     if (fb.cut_in && b == 0) {
         *fb.n = any_open ? *fb.npairs : 0u;
         *fb.kept = 0u;
+        if (fb.host_open) *fb.host_open = *fb.open;
     }
     if (b >= nbins) return;
     if (!owns_bin_row(b / tiles_x, own)) {  // (another rank's bin: no record, no pairs)
@@ -979,6 +995,28 @@ __global__ __launch_bounds__(1024) void order_bins_kernel(const uint32_t* __rest
     }
     __syncthreads();
     for (uint32_t b = tid; b < nbins; b += 1024u) order[atomicAdd(&cnt[bucket(b)], 1u)] = b;
+}
+
+__global__ __launch_bounds__(256) void cut_dilate_kernel(const uint32_t* __restrict__ cut, uint32_t* __restrict__ out,
+                                                         uint32_t tiles_x, uint32_t tiles_y, int r) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b >= tiles_x * tiles_y) return;
+    const int by = (int)(b / tiles_x), bx = (int)(b - (uint32_t)by * tiles_x);
+    const int y0 = max(by - r, 0), y1 = min(by + r, (int)tiles_y - 1);
+    const int x0 = max(bx - r, 0), x1 = min(bx + r, (int)tiles_x - 1);
+    uint32_t m = 0u;
+    for (int y = y0; y <= y1; ++y)
+        for (int x = x0; x <= x1; ++x) m = max(m, cut[(uint32_t)y * tiles_x + (uint32_t)x]);
+    out[b] = m;
+}
+
+hipError_t launch_cut_dilate(const uint32_t* cut, uint32_t* out, uint32_t tiles_x, uint32_t tiles_y, int r,
+                             hipStream_t st) {
+    const uint32_t n = tiles_x * tiles_y;
+    if (n == 0) return hipSuccess;
+    if (!cut || !out || r < 0) return hipErrorInvalidValue;
+    cut_dilate_kernel<<<(n + 255) / 256, 256, 0, st>>>(cut, out, tiles_x, tiles_y, r);
+    return hipGetLastError();
 }
 
 hipError_t launch_order_bins(const uint32_t* qrec, const uint2* ranges, uint32_t nbins, uint32_t* order,

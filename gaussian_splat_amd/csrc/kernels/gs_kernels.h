@@ -88,6 +88,10 @@ hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uin
 struct PassCounts {
     uint32_t* C = nullptr;
     uint32_t tile = 0, mask = 0, ntiles = 0;
+    // (depth-cut frames) count only the pairs the sort's filtered first pass
+    // keeps, dkey <= cut[bin] (SortFilter::keep), so that pass needs no count
+    // kernel of its own (launch_radix_sort first_counted with the filter)
+    const uint32_t* cut = nullptr;
 };
 constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts in LDS (the rest: global atomics)
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
@@ -264,6 +268,10 @@ struct CutFallback {
     uint32_t* n = nullptr;
     uint32_t* kept = nullptr;
     uint2* ranges = nullptr;
+    // (optional) host-mapped word: the frame's open-quadrant count, written by
+    // the kernel's first lane, read by the host's dilation controller later
+    // without a sync (a stale value only delays its reaction)
+    unsigned long long* host_open = nullptr;
 };
 hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const uint32_t* dkey, uint32_t* cut_out,
                                uint32_t nbins, uint32_t tiles_x, const RowOwnership& own, uint32_t margin,
@@ -272,6 +280,12 @@ hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const
 // walks each pixel's covering fragments in arrival order and records the id
 // of the a.cap-th one in a.thr_out (tile.metal:7,199-202; 50layer.metal:8,170).
 hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
+// Spatially dilated cuts (a moving camera): out[bin] = the
+// largest cut over the bins within r rows / columns of it (clamped to the
+// grid).  A deeper cut only moves pairs from the fallback lists into the front
+// lists, so any r gives the same image.
+hipError_t launch_cut_dilate(const uint32_t* cut, uint32_t* out, uint32_t tiles_x, uint32_t tiles_y, int r,
+                             hipStream_t st);
 // Longest-first bin order for the next composite on this buffer set (one
 // workgroup): a bin's cost is the length of list its quadrants walked in the
 // frame that wrote qrec (every pair while a quadrant stayed open), from the

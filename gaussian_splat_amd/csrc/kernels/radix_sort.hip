@@ -429,7 +429,9 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                                   uint32_t* const* vals, uint32_t* tmp_keys, uint32_t* const* tmp_vals, uint32_t n,
                                   int bits, uint32_t* scratch, bool* result_in_tmp, uint2* ranges, hipStream_t st,
                                   const uint32_t* n_dev, bool first_counted, const SortFilter& flt = SortFilter{}) {
-    if (flt.cut && (NV != 1 || first_counted || !flt.kept)) return hipErrorInvalidValue;
+    // (first_counted with a filter: the producer counted only the kept items,
+    // PassCounts::cut; not with the strided fallback grids)
+    if (flt.cut && (NV != 1 || !flt.kept || (first_counted && flt.stride_grid))) return hipErrorInvalidValue;
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -477,8 +479,9 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                 continue;
             }
             if (filt) {
-                rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
-                                                                        tiles, n_dev, flt);
+                if (!first_counted)
+                    rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                                                                            tiles, n_dev, flt);
                 rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
                 e = launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
                                           tiles, rg, rmask, n_dev, flt);

@@ -183,8 +183,8 @@ __device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
 // LDS words, an inclusive max-scan); its bin: the (q - start)-th bin of that
 // item's rect in row-major order, minus the excluded bins -- exactly what
 // emit_bin_pairs writes there.  c: the item's pair count (0: none), start:
-// its first pair - off0.  on_pair(g, bin) runs for every pair written (g
-// absolute).
+// its first pair - off0.  on_pair(g, bin, key) runs for every pair written
+// (g absolute).
 template <typename F>
 __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t c, uint32_t start,
                                           uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
@@ -231,7 +231,7 @@ __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const Bin
             const uint32_t bin = ((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx;
             keys[off0 + q] = o_khi | bin;
             vals[off0 + q] = o_val;
-            on_pair(off0 + q, bin);
+            on_pair(off0 + q, bin, o_khi | bin);
         }
     }
 }
@@ -337,7 +337,8 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // without its key re-read): the block's pairs are contiguous from its
     // partial, so its first kDupCountTiles tiles count in LDS
     const uint32_t t_lo = pc.C ? (uint32_t)(part / pc.tile) : 0u;
-    auto count = [&](uint32_t g, uint32_t bin) {  // (pc.C) the pair's digit into its sort tile's counts
+    auto count = [&](uint32_t g, uint32_t bin, uint32_t key) {  // (pc.C) the pair's digit into its tile's counts
+        if (pc.cut && (key >> bin_bits) > pc.cut[bin]) return;  // (behind its bin's cut: the filter drops it)
         const uint32_t t = udiv_est(g, pc.tile), d = bin & pc.mask;
         if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
         else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
@@ -359,7 +360,8 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             const uint32_t khi = dkey ? dk[k] << bin_bits : 0u;
             const uint32_t val = order ? ord[k] : j;
             if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, count);
-            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, [](uint32_t, uint32_t) {});
+            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+                           [](uint32_t, uint32_t, uint32_t) {});
         }
     } else
 #pragma unroll
@@ -378,6 +380,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                     ++t;
                     next += pc.tile;
                 }
+                if (pc.cut && key_hi >> bin_bits > pc.cut[bin]) return;  // (dropped by the filtered pass)
                 const uint32_t d = bin & pc.mask;
                 if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
                 else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
@@ -487,7 +490,8 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     const BinRect r = bin_rect(lo, hi, src.masked);
     const uint32_t c = rect_tile_count(lo, hi, src.own, src.masked);
     const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
-    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, [](uint32_t, uint32_t) {});
+    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+              [](uint32_t, uint32_t, uint32_t) {});
 }
 
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,

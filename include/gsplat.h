@@ -132,11 +132,13 @@ typedef struct gs_stats {
        the fallback lists'), the 8x8-pixel quadrants the front lists left
        open (open_tiles), and
        cut_frame = 1 for a depth-cut frame.  Read with records_fetched.
-       reserved: 0. */
+       cut_dilate: the radius in 32-px bins over which the frame's cuts were
+       dilated (0 unless the buffer set's recent frames left quadrants open:
+       a moving camera). */
     int64_t pairs_sorted;
     int64_t open_tiles;
     int32_t cut_frame;
-    uint32_t reserved;
+    uint32_t cut_dilate;
 } gs_stats;
 
 typedef struct gs_handle gs_handle;

@@ -251,3 +251,37 @@ def test_depth_cuts_virtual_ranks(built, world, w, h, binning, path, table):
             saved[be.rank] = st["pairs"] - st["pairs_sorted"]
     if dense:  # (the last frame)
         assert min(saved) > 0, saved
+
+
+def test_binning_model_heavy_orbit_picks_bin_first(built):
+    """on a heavy-tailed scene under an orbiting camera the
+    binning-order model (renderer.cpp bin_first_order) must pick bin-first
+    once it has seen a frame: the index-order duplicate emits
+    wave-cooperatively (scan.hip coop_emit), so large splats no longer make it
+    slower than the depth sort (round 5, profiles/r05/binning_heavy_orbit.json:
+    0.92 against 1.05 ms a frame at 6M splats).  Every frame stays
+    bit-identical to the forced depth-first frame."""
+    import torch
+
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd import scene as S
+    from gaussian_splat_amd.api import default_camera
+    W, H = 1280, 720
+    sc = S.activate(S.synthetic_raw(1_500_000, seed=9, aspect=W / H, rest=True, profile="heavy"), 3)
+    cam = default_camera(W, H)
+    P = cam.getProjectionMatrix()
+    auto = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False))
+    auto.initialize(0)
+    ref = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False, binning="depth_first"))
+    ref.initialize(0)
+    picks = []
+    for k in range(8):
+        V = cam.getViewMatrix()
+        cam.orbit(0.01)
+        a = auto.render_host(V, P, W, H)
+        picks.append(int(auto.last_stats()["binning"]))
+        b = ref.render_host(V, P, W, H)
+        assert int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32))) == 0, k
+    torch.cuda.synchronize()
+    assert picks[0] == 1, picks  # (the first frame at a resolution: depth-first, P unknown)
+    assert all(p == 2 for p in picks[1:]), picks  # (2 = bin-first)
