@@ -179,7 +179,7 @@ def cpu_baseline(scene, view, proj, w, h, sh, threads, seconds, max_frames=50):
                       f"(oracle/gs_oracle.c, OpenMP, {threads} thread{'s' if threads > 1 else ''}), {dt:.1f} s"}
 
 
-KERNEL_NAME = {"preprocess": "preprocess_kernel", "composite": "composite_kernel"}
+KERNEL_NAME = {"preprocess": "preprocess_kernel", "composite": "composite_"}  # (composite_kernel, composite_strip_kernel)
 # (depth-cut frames: the composite's pass 2 over the fallback lists is a separate, usually empty
 # launch; the dispatch-packet events and the PMC means are the front lists' pass)
 KERNEL_EXCLUDE = {"composite": ", 2>"}

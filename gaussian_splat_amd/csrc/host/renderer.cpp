@@ -44,7 +44,7 @@ gs_status fail(gs_status s, const std::string& msg) {
     } while (0)
 
 #ifndef GS_DUP_FILTER_COUNT  // A/B knob: 1 = a depth-cut frame's duplicate counts the filtered pass's digits
-#define GS_DUP_FILTER_COUNT 1
+#define GS_DUP_FILTER_COUNT 0
 #endif
 
 struct DevBuf {
@@ -176,7 +176,7 @@ struct gs_handle {
     // raised while its frames leave quadrants open (the counts come back in
     // host_total[6 + set], written by cut_finalize) and lowered again after
     // kCutCalm frames with none.
-    DevBuf qrec, cutbuf, cutord, cutdil, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
+    DevBuf qrec, cutbuf, cutord, cutdil, wcost, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
     int cut_r[2] = {0, 0};
     int cut_calm[2] = {0, 0};
     uint32_t cut_bins = 0;       // bins per table in cutbuf
@@ -784,6 +784,7 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         GS_HIP(hipStreamSynchronize(sp));
         GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
         GS_HIP(h->cutord.reserve((size_t)T * 4 * 4));
+        GS_HIP(h->wcost.reserve((size_t)T * 2 * 4));
         h->cut_bins = T;
         h->cut_valid[0] = h->cut_valid[1] = false;
     }
@@ -859,12 +860,11 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
         fb.ranges = h->ranges.as<uint2>();
         if (h->dev_total) fb.host_open = reinterpret_cast<unsigned long long*>(h->dev_total) + 6 + h->set;
     }
-    // the next composite's longest-first bin order (single-GPU frames), from
-    // the quadrant records and the front lists' ranges (before cut_finalize
-    // clears those for the fallback lists)
-    if (!own.owner && h->ord_out) GS_HIP(gs::launch_order_bins(ca.qrec, ca.ranges, T, h->ord_out, sc));
     GS_HIP(gs::launch_cut_finalize(ca.qrec, ca.vals, dkey, h->cut_out, T, (uint32_t)U.tiles_x, own, cut_margin(), sc,
                                    fb));
+    // the set's next composite's longest-first bin order (single-GPU frames),
+    // from what this frame's workgroups fetched
+    if (ca.wcost && h->ord_out) GS_HIP(gs::launch_order_bins(ca.wcost, T, h->ord_out, sc));
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
 #ifdef GS_AB_NO_FALLBACK  // timing ablation build only: exact only while no quadrant is left open
     return GS_OK;
@@ -995,6 +995,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             ca.state = h->cstate.as<float4>();
             ca.cut_in = h->cut_in;
             ca.order = own.dev.owner ? nullptr : h->ord_in;
+            ca.wcost = own.dev.owner ? nullptr : h->wcost.as<uint32_t>();
         }
         // everything that reads the lists, queued before the host waits for P
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
@@ -1078,6 +1079,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.state = h->cstate.as<float4>();
         ca.cut_in = h->cut_in;
         ca.order = own.dev.owner ? nullptr : h->ord_in;
+        ca.wcost = own.dev.owner ? nullptr : h->wcost.as<uint32_t>();
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
             gs::CompositeArgs c = ca;
             c.vals = sv;

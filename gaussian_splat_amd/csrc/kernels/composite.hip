@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
 #define GS_COMPOSITE_LPT 1
 #endif
 #ifndef GS_STRIP_PRIO  // A/B knob: 1 = issue priority falls with the batches a workgroup has walked
-#define GS_STRIP_PRIO 0
+#define GS_STRIP_PRIO 1
 #endif
 #ifndef GS_STRIP_PIPE  // A/B knob: 1 = the walk reads one record ahead (rolling), 0 = two records per step
 #define GS_STRIP_PIPE 1
@@ -804,6 +804,7 @@ __global__ __launch_bounds__(256, GS_STRIP_WAVES) __attribute__((amdgpu_num_sgpr
         else walk(std::integral_constant<uint32_t, 0>{});
     }
     if (tid == 0 && a.fetched) (void)atomicAdd(a.fetched, (unsigned long long)fetched);
+    if (PASS == 1 && tid == 0 && a.wcost) a.wcost[2u * bin + half] = fetched;  // (the next bin order's cost)
 #ifdef GS_COMPOSITE_TRACE
     __syncthreads();
     if (tid == 0 && blockIdx.x < 65536u) {
@@ -959,42 +960,35 @@ hipError_t launch_cut_finalize(const uint32_t* qrec, const uint32_t* vals, const
 // Longest-first bin order (launch_order_bins): one 1024-lane workgroup, a
 // counting sort of the bins into 128 cost buckets (log2 with two mantissa
 // bits), costliest first.
-__global__ __launch_bounds__(1024) void order_bins_kernel(const uint32_t* __restrict__ qrec,
-                                                          const uint2* __restrict__ ranges, uint32_t nbins,
+__global__ __launch_bounds__(1024) void order_bins_kernel(const uint32_t* __restrict__ wcost, uint32_t nbins,
                                                           uint32_t* __restrict__ order) {
     constexpr int kB = 128;
     __shared__ uint32_t cnt[kB];
-    const uint32_t tid = threadIdx.x;
+    __shared__ uint8_t bk[kOrderMaxBins];  // each bin's bucket, between the two phases
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
     if (tid < kB) cnt[tid] = 0u;
     __syncthreads();
-    auto bucket = [&](uint32_t b) -> uint32_t {
-        const uint2 rg = decode_range(ranges[b]);
-        const uint32_t len = rg.y > rg.x ? rg.y - rg.x : 0u;  // (empty bins: {~0, 0})
-        const uint4* q = reinterpret_cast<const uint4*>(qrec + (size_t)b * kQrecWords);
-        uint32_t w = 0u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint4 v = q[i];
-            w = max(w, max(max(v.x, v.y), max(v.z, v.w)));
+    for (uint32_t b = tid; b < nbins; b += 1024u) {
+        const uint2 c2 = reinterpret_cast<const uint2*>(wcost)[b];  // (the bin's two halves)
+        const uint32_t cost = c2.x + c2.y;
+        uint32_t k = 0u;
+        if (cost) {
+            const uint32_t e = 31u - (uint32_t)__builtin_clz(cost);  // <= 31
+            const uint32_t m = e >= 2u ? (cost >> (e - 2u)) & 3u : (cost << (2u - e)) & 3u;
+            k = min(1u + e * 4u + m, (uint32_t)kB - 1u);
         }
-        const uint32_t cost = w == 0xFFFFFFFFu ? len : (w > rg.x && len ? min(w - rg.x, len) : 0u);
-        if (cost == 0u) return 0u;
-        const uint32_t e = 31u - (uint32_t)__builtin_clz(cost);  // <= 31
-        const uint32_t m = e >= 2u ? (cost >> (e - 2u)) & 3u : (cost << (2u - e)) & 3u;
-        return min(1u + e * 4u + m, (uint32_t)kB - 1u);
-    };
-    for (uint32_t b = tid; b < nbins; b += 1024u) atomicAdd(&cnt[bucket(b)], 1u);
-    __syncthreads();
-    if (tid == 0) {  // exclusive offsets, costliest bucket first
-        uint32_t run = 0u;
-        for (int k = kB - 1; k >= 0; --k) {
-            const uint32_t c = cnt[k];
-            cnt[k] = run;
-            run += c;
-        }
+        bk[b] = (uint8_t)k;
+        atomicAdd(&cnt[k], 1u);
     }
     __syncthreads();
-    for (uint32_t b = tid; b < nbins; b += 1024u) order[atomicAdd(&cnt[bucket(b)], 1u)] = b;
+    if (tid < 64u) {  // exclusive offsets, costliest bucket first: one wave, two buckets a lane
+        const uint32_t hi = cnt[kB - 1 - 2 * lane], lo = cnt[kB - 2 - 2 * lane];
+        const uint32_t inc = wave_scan_dpp<false>(hi + lo);
+        cnt[kB - 1 - 2 * lane] = inc - hi - lo;
+        cnt[kB - 2 - 2 * lane] = inc - lo;
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < nbins; b += 1024u) order[atomicAdd(&cnt[bk[b]], 1u)] = b;
 }
 
 __global__ __launch_bounds__(256) void cut_dilate_kernel(const uint32_t* __restrict__ cut, uint32_t* __restrict__ out,
@@ -1019,11 +1013,10 @@ hipError_t launch_cut_dilate(const uint32_t* cut, uint32_t* out, uint32_t tiles_
     return hipGetLastError();
 }
 
-hipError_t launch_order_bins(const uint32_t* qrec, const uint2* ranges, uint32_t nbins, uint32_t* order,
-                             hipStream_t st) {
+hipError_t launch_order_bins(const uint32_t* wcost, uint32_t nbins, uint32_t* order, hipStream_t st) {
     if (nbins == 0) return hipSuccess;
-    if (!qrec || !ranges || !order || nbins > kOrderMaxBins) return hipErrorInvalidValue;
-    order_bins_kernel<<<1, 1024, 0, st>>>(qrec, ranges, nbins, order);
+    if (!wcost || !order || nbins > kOrderMaxBins) return hipErrorInvalidValue;
+    order_bins_kernel<<<1, 1024, 0, st>>>(wcost, nbins, order);
     return hipGetLastError();
 }
 

@@ -93,7 +93,7 @@ struct PassCounts {
     // kernel of its own (launch_radix_sort first_counted with the filter)
     const uint32_t* cut = nullptr;
 };
-constexpr uint32_t kDupCountTiles = 4;  // sort tiles a duplicate block counts in LDS (the rest: global atomics)
+constexpr uint32_t kDupCountTiles = 8;  // sort tiles a duplicate block counts in LDS (the rest: global atomics)
 // Down-sweep fused with the duplicate: for j < n, item j (splat order[j], or j
 // when order is null) with rect (rect_lo[j], rect_hi[j]) emits (bin, splat)
 // for each bin of its rect whose row this rank owns, minus the excluded bins,
@@ -241,6 +241,9 @@ struct CompositeArgs {
     // bins first, so the launch's last workgroups are short ones.  Which
     // workgroup renders which bin does not change any pixel.
     const uint32_t* order;
+    // (optional, strip composite pass 1) wcost[2 bin + half] = the records the
+    // bin's top / bottom half workgroup fetched: launch_order_bins' costs
+    uint32_t* wcost;
 };
 // One 256-lane workgroup per owned 16x16 tile.  mode 0 = tile rule (A >= 0.99
 // break), 1 = live50 rule (T < 0.01 break), 2 = MLAB k-buffer (a.vals
@@ -287,13 +290,12 @@ hipError_t launch_cap_threshold(const CompositeArgs& a, hipStream_t st);
 hipError_t launch_cut_dilate(const uint32_t* cut, uint32_t* out, uint32_t tiles_x, uint32_t tiles_y, int r,
                              hipStream_t st);
 // Longest-first bin order for the next composite on this buffer set (one
-// workgroup): a bin's cost is the length of list its quadrants walked in the
-// frame that wrote qrec (every pair while a quadrant stayed open), from the
-// lists' ranges; order = the bins by cost, descending, in 128 log-spaced
-// buckets (ties in any order).  nbins <= kOrderMaxBins.
+// workgroup): a bin's cost is the records its two half-bin workgroups
+// fetched in the front lists' composite (CompositeArgs::wcost); order = the
+// bins by cost, descending, in 128 log-spaced buckets (ties in any order).
+// nbins <= kOrderMaxBins.
 constexpr uint32_t kOrderMaxBins = 1u << 16;
-hipError_t launch_order_bins(const uint32_t* qrec, const uint2* ranges, uint32_t nbins, uint32_t* order,
-                             hipStream_t st);
+hipError_t launch_order_bins(const uint32_t* wcost, uint32_t nbins, uint32_t* order, hipStream_t st);
 
 // ---- shard.hip (multi-GPU tile-row ownership / depth slabs) ---------------
 constexpr int kXRecFloat4 = 3;  // 48-B exchange record: the projection's record (its first 48 B)

@@ -6,7 +6,9 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/art; mkdir -p $O
 step() { name=$1; shift; echo "== $name"; "$@"; rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-for s in ${STEPS:-tests bench prof pmc configs heavy orbit ranks timeline}; do case $s in
+for s in ${STEPS:-tests driver bench prof pmc configs heavy orbit ranks timeline}; do case $s in
+driver) step driver bash -c "timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_command.json 2> $O/bench_driver_command.err"
+       python -c "import json;d=json.load(open('$O/bench_driver_command.json'));print('driver', d['ms_per_step'], d['settled']['ms_per_step'], d['orbit']['ms_per_step'], d['roofline']['frac'], d['roofline']['kernels']['composite']['ms'])" ;;
 tests) step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
        tail -1 $O/pytest_gpu.log ;;
 bench) step bench bash -c "timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err"; cat $O/bench_default.json ;;
@@ -18,7 +20,11 @@ pmc)   B="python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --pmc 0 --no-sta
        step sq2 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d $O/pmc/sq2 -o run --output-format csv -- $B > $O/pmc_sq2.log 2>&1
        step fetch timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- $B > $O/pmc_fetch.log 2>&1
        step write timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- $B > $O/pmc_write.log 2>&1
-       python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A1 "composite_kernel<0\|preprocess_kernel<3>" $O/pmc_summary.txt ;;
+       python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A1 "composite_strip_kernel<0, 1>\|preprocess_kernel<3, 1>" $O/pmc_summary.txt ;;
+prof50m) for c in 4k 50m; do
+         step prof_$c bash -c "timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run --output-format csv -- \
+           python bench.py --config $c --steps 20 --frames-in-flight 1 --pmc 0 --cpu-baseline 0 --settled-probe 0 --orbit-probe 0 > $O/bench_${c}_profiled.json 2> $O/bench_${c}_profiled.err"
+         cp $(find $O/prof_$c -name "*kernel_stats.csv" | head -1) $O/bench_${c}_profiled_kernel_stats.csv; done ;;
 configs) for c in 1m 4k 50m; do
          step cfg_$c bash -c "timeout -k 10 600 python bench.py --config $c --steps 30 --cpu-baseline 0 > $O/bench_$c.json 2> $O/bench_$c.err"
          python -c "import json;d=json.load(open('$O/bench_$c.json'));print('$c', d['ms_per_step'], d['value'], d['config']['binning'], d['roofline']['kernels']['composite']['ms'])"; done ;;
