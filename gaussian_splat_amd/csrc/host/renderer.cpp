@@ -46,6 +46,12 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_DUP_FILTER_COUNT  // A/B knob: 1 = a depth-cut frame's duplicate counts the filtered pass's digits
 #define GS_DUP_FILTER_COUNT 0
 #endif
+#ifndef GS_DUP_FLAG  // A/B knob: 1 = the bin-first duplicate marks the pairs behind their cut (kBehindFlag)
+#define GS_DUP_FLAG 1
+#endif
+#ifndef GS_BAND_LOCAL  // A/B knob: 1 = contiguous band frames bin without an owner table (gs_handle::band_local)
+#define GS_BAND_LOCAL 1
+#endif
 
 struct DevBuf {
     void* ptr = nullptr;
@@ -107,6 +113,11 @@ struct gs_handle {
     int kev_slot = 0;          // slot of the frame being enqueued
     bool kev_pending = false;  // last frame's kernel times not yet copied into stats
     bool shard_frame = false;
+    // a band frame whose owned rows are contiguous: the projection clips the
+    // rects to the band, so the binning needs no owner table (every pair it
+    // emits lies in an owned row) and runs the single-GPU chain (fused scan,
+    // cooperative duplicate, depth cuts); the composite keeps the table
+    bool band_local = false;
     bool events = false;
     uint32_t* last_keys = nullptr;  // sorted pair arrays of the last frame
     uint32_t* last_vals = nullptr;
@@ -390,7 +401,7 @@ bool bin_first_order(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int n
     // preprocess measures (round 4: 67 / 354 / 1003 us against W = 0.73M /
     // 3.53M / 15.9M).
     double dup_ps;
-    if (nrows < 0) {
+    if (nrows < 0 || h->band_local) {  // (a clipped band bins without its owner table)
         dup_ps = 2.6 * P + 3.0 * (double)m;
     } else {
         const double W = o.wmax_pairs > 0 ? (double)o.wmax * P / (double)o.wmax_pairs : 0.07 * P;
@@ -648,6 +659,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 #if !GS_DUP_FILTER_COUNT
         pc = gs::PassCounts{};
 #endif
+        // the duplicate marks the pairs behind the cut from an LDS copy of the
+        // table, so the filtered pass and its count test a bit instead of
+        // gathering cut[bin] per pair (index order, every bin row owned)
+        flt.flag = GS_DUP_FLAG && !order && !own.dev.owner && T <= gs::kDupCutBins &&
+                   bits + gs::kDepthBits <= 31 ? 1u : 0u;
     }
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
@@ -670,7 +686,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         hipError_t e = gs::launch_scan_duplicate(order, rect_lo, rect_hi, h->partials.as<uint64_t>(), m,
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
-                                                 np, st, h->offsets.as<uint32_t>(), pc);
+                                                 np, st, h->offsets.as<uint32_t>(), pc,
+                                                 flt.flag ? h->cut_in : nullptr, flt.flag ? T : 0u);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         // (depth-cut frames: sorted into fkeys/fvals, so keys/vals keep every
@@ -878,6 +895,9 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     flt.dshift = bits;
     flt.kept = fb.kept;
     flt.behind = 1;
+    // (a marked frame's pairs carry kBehindFlag above the depth key: the test
+    // and the kept keys go without it)
+    if (bits + gs::kDepthBits <= 31) flt.kmask = ~gs::kBehindFlag;
     // (usually no quadrant is open and the sort's input is empty: a fixed
     // grid that loops over the tiles then costs a few workgroups, not one
     // per tile of the frame's pairs)
@@ -924,6 +944,9 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     Ownership own;
     gs_status so = frame_ownership(h, U.tiles_y, st, &own);
     if (so != GS_OK) return so;
+    // the binning's ownership: none for a clipped band (h->band_local)
+    Ownership bown = own;
+    if (h->band_local && !slab_t) bown.dev = gs::RowOwnership{nullptr, 0};
     const size_t mm = (size_t)std::max<uint32_t>(m, 1);
     for (DevBuf* b : {&h->dsk, &h->dso, &h->dsl, &h->dsh, &h->dtk, &h->dto, &h->dtl, &h->dth})
         GS_HIP(b->reserve(mm * 4));
@@ -955,7 +978,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     if (mlab) {
         // MLAB k-buffer: arrival (index) order per pixel, no depth sort
         mark(h, 2, st);
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, bown, true, st, &vals, &P);
         if (s != GS_OK) return s;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
@@ -1030,7 +1053,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 7, sc);
             return GS_OK;
         };
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, true, st, &vals, &P, dkey, &tail, sc);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, bown, true, st, &vals, &P, dkey, &tail, sc);
         if (s != GS_OK) return s;
         h->order.sample_pairs = P;
         if (cutf) {  // this frame's cuts are read by its set's next frame
@@ -1043,7 +1066,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
     if (ca.cap > 0) {
         // 0. per-pixel cap thresholds from the lists in arrival (index) order
         GS_HIP(h->thr.reserve((size_t)U.width * U.height * 4));
-        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, own, false, st, &vals, &P);
+        gs_status s = build_bin_lists(h, m, nullptr, rect_lo, rect_hi, U, bown, false, st, &vals, &P);
         if (s != GS_OK) return s;
         ca.vals = vals;
         ca.ranges = h->ranges.as<uint2>();
@@ -1092,7 +1115,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 7, sc);
             return GS_OK;
         };
-        gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P, sdk, &tail, sc);
+        gs_status s = build_bin_lists(h, m, order, slo, shi, U, bown, true, st, &vals, &P, sdk, &tail, sc);
         if (s != GS_OK) return s;
         h->cut_phase[h->set] ^= 1;  // this frame's cuts are read by its set's next frame
         h->cut_valid[h->set] = true;
@@ -1100,7 +1123,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         return GS_OK;
     }
     // 2. bin lists in depth order
-    gs_status s = build_bin_lists(h, m, order, slo, shi, U, own, true, st, &vals, &P);
+    gs_status s = build_bin_lists(h, m, order, slo, shi, U, bown, true, st, &vals, &P);
     if (s != GS_OK) return s;
     ca.vals = vals;
     ca.ranges = h->ranges.as<uint2>();
@@ -1421,7 +1444,8 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     if (T == 0 || bits_for(T) > 32) return fail(GS_ERR_UNSUPPORTED, "bad tile count");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
-    int compact = 0;
+    int compact = 0, band_nrows = -1;
+    h->band_local = false;
     if (band) {
         // this rank's owned bin rows into a compact band; with contiguous
         // ownership the rects are clipped to the band's pixel rows (splats
@@ -1438,8 +1462,12 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         if (own.dev.owner && (int)rows.back() - (int)rows.front() + 1 == (int)rows.size()) {
             U.band_y0 = (int32_t)rows.front() * gs::kBin;
             U.band_y1 = std::min(H, ((int32_t)rows.back() + 1) * gs::kBin) - 1;
+            h->band_local = GS_BAND_LOCAL != 0;
+        } else if (!own.dev.owner) {
+            h->band_local = GS_BAND_LOCAL != 0;  // (world 1: the band is the frame)
         }
         compact = own.dev.owner ? 1 : 0;
+        band_nrows = own.nrows;
     }
     const size_t bytes = (size_t)W * H * (bgra8 ? 4 : 16);
     void* out = out_user;
@@ -1475,10 +1503,11 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     gs::PreFuse fuse;
     h->fused_prep = gs_handle::ListPrep{};
     h->order_pick = -1;
-    const bool cut_on = depth_cuts_on(h) && !band && h->world == 1 && cut_rule(h, U);
+    const bool whole = band ? h->band_local : h->world == 1;  // (the binning owns every row it sees)
+    const bool cut_on = depth_cuts_on(h) && whole && cut_rule(h, U);
     bool cut_frame = false;
-    if (!band && h->world == 1 && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
-        const bool bf = bin_first_order(h, U, (uint32_t)h->n, -1, cut_on);
+    if (whole && h->n > 0 && h->opt.mode != GS_MODE_MLAB && !(fs_env && fs_env[0] == '0')) {
+        const bool bf = bin_first_order(h, U, (uint32_t)h->n, h->band_local ? band_nrows : -1, cut_on);
         h->order_pick = bf ? 1 : 0;
         cut_frame = cut_on;
         if ((s = setup_cuts(h, U, cut_frame, st, sp)) != GS_OK) return s;

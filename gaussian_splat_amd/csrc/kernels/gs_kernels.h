@@ -103,11 +103,19 @@ constexpr uint32_t kDupCountTiles = 8;  // sort tiles a duplicate block counts i
 // Index order runs one fused kernel; depth order (order set) a down-sweep
 // into offsets (n words of scratch) and a one-splat-per-lane duplicate.
 // Nothing is written when *npairs == 0 (see launch_tile_count_totals).
+// fcut (optional; index order, every bin row owned, nbins <= kDupCutBins,
+// bin_bits + kDepthBits <= 31): the depth-cut frame's cut table.  Each block
+// stages it in LDS and sets bit 31 (kBehindFlag) of every pair key behind its
+// bin's cut, so the sort's filtered first pass tests one bit (SortFilter::flag)
+// instead of gathering cut[bin] per pair.
+constexpr uint32_t kDupCutBins = 16384;
+constexpr uint32_t kBehindFlag = 0x80000000u;
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
-                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{});
+                                 uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
+                                 const uint32_t* fcut = nullptr, uint32_t nbins = 0);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -171,8 +179,15 @@ struct SortFilter {
     uint32_t* kept = nullptr;
     uint32_t behind = 0;
     uint32_t stride_grid = 0;  // > 0: every pass on at most this many workgroups, looping over the tiles
+    // flag: the duplicate marked the pairs behind their cut (kBehindFlag), the
+    // front lists keep the unmarked ones (cut is then only the "filter on"
+    // sign); kmask: the key bits below the flag (the depth test of a marked
+    // frame's fallback lists; the pass stores kept keys masked with it)
+    uint32_t flag = 0;
+    uint32_t kmask = ~0u;
     __device__ __forceinline__ bool keep(uint32_t key) const {
-        return ((key >> dshift) <= cut[key & bmask]) != (behind != 0u);
+        if (flag) return (key & kBehindFlag) == 0u;
+        return (((key & kmask) >> dshift) <= cut[key & bmask]) != (behind != 0u);
     }
 };
 hipError_t launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys, uint32_t* vals,

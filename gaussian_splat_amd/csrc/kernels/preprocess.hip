@@ -122,6 +122,10 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 }
 
 
+#ifndef GS_PRE_EARLY  // A/B knob: 1 = rotation, scale (and the SH0 colour) loaded with the position
+#define GS_PRE_EARLY 0     // (one dependent round trip fewer, bytes for culled splats too)
+#endif
+
 #ifndef GS_PRE_WAVES  // A/B knob: min waves per SIMD (caps the VGPRs)
 #define GS_PRE_WAVES 8
 #endif
@@ -148,12 +152,25 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
     const float* VP = U.VP;
 
     float4 a0 = scene_load(&s.p0[i]);
+#if GS_PRE_EARLY
+    float4 q_e = scene_load(&s.p1[i]);
+    float4 a2_e = scene_load(&s.p2[i]);
+    [[maybe_unused]] float2 a3_e;
+    if constexpr (DEG == 0) a3_e = scene_load(&s.p3[i]);
+#endif
     float px = a0.x, py = a0.y, pz = a0.z;
     // K3: view position, zFront (tile.metal:94-105)
     float vx = xform_row(V, 0, px, py, pz);
     float vy = xform_row(V, 1, px, py, pz);
     float vz = xform_row(V, 2, px, py, pz);
     float zf = -vz;
+#if GS_PRE_EARLY
+    // (an empty asm consuming the early loads: the compiler otherwise sinks
+    // them back into the branch that uses them)
+    asm volatile("" : "+v"(q_e.x), "+v"(q_e.y), "+v"(q_e.z), "+v"(q_e.w), "+v"(a2_e.x), "+v"(a2_e.y), "+v"(a2_e.z),
+                 "+v"(a2_e.w));
+    if constexpr (DEG == 0) asm volatile("" : "+v"(a3_e.x), "+v"(a3_e.y));
+#endif
     if (zf >= 1e-4f) {
         // K6 z-clip on NDC z in [0,1] (tile.metal:145-152)
         float clx = xform_row(VP, 0, px, py, pz);
@@ -163,8 +180,12 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
         float invw = 1.0f / clw;
         float ndcz = clz * invw;
         if (ndcz >= 0.0f && ndcz <= 1.0f && zf >= 0.001f) {
+#if GS_PRE_EARLY
+            const float4 q = q_e, a2 = a2_e;
+#else
             float4 q = scene_load(&s.p1[i]);
             float4 a2 = scene_load(&s.p2[i]);
+#endif
             // K1 (tile.metal:40-49)
             float qs = q.x * q.x;
             qs = __builtin_fmaf(q.y, q.y, qs);
@@ -263,7 +284,13 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
                     // (colour inputs loaded only for splats on screen; loading
                     // them with the shape, a round trip earlier, was measured
                     // slower: 0.30-0.33 vs 0.29 ms, 45 more live registers)
+#if GS_PRE_EARLY
+                    float2 a3;
+                    if constexpr (DEG == 0) a3 = a3_e;
+                    else a3 = scene_load(&s.p3[i]);
+#else
                     const float2 a3 = scene_load(&s.p3[i]);
+#endif
                     ShCoef<DEG> coef;
                     if constexpr (DEG > 0) sh_load<DEG>(s, i, coef);
                     sh_color<DEG>(coef, px, py, pz, U.campos, a2.w, a3.x, a3.y, cr, cg, cbl);

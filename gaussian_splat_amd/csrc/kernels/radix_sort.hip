@@ -180,7 +180,12 @@ __global__ __launch_bounds__(kRsScanThreads) void rts_scan_kernel(uint32_t* __re
 // STRIDE: a fixed grid loops over the tiles (the depth-cut fallback lists'
 // sort, whose input is usually empty: a small grid then costs little).
 template <int NV, int BITS, bool FILT, bool STRIDE = false>
-__global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
+#ifdef GS_RS_PASS_W8  // A/B knob: every pass at 8 waves per SIMD (the filtered ones spill)
+#define GS_RS_PASS_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define GS_RS_PASS_ATTR
+#endif
+__global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pass_kernel(SortIO<NV> io, uint32_t n, int shift, uint32_t mask,
                                                        const uint32_t* __restrict__ C,
                                                        const uint32_t* __restrict__ totals, uint32_t ntiles,
                                                        uint2* __restrict__ ranges, uint32_t rmask,
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) void rts_pass_kernel(SortIO<
     // value arrays
 #pragma unroll
     for (int k = 0; k < IPT; ++k)
-        if (kept(k)) stage[pos[k]] = key[k];
+        if (kept(k)) stage[pos[k]] = FILT ? key[k] & flt.kmask : key[k];
     block_lds_sync();
     uint32_t gdst[IPT];
 #pragma unroll

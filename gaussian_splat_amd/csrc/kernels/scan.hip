@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
 // item's rect in row-major order, minus the excluded bins -- exactly what
 // emit_bin_pairs writes there.  c: the item's pair count (0: none), start:
 // its first pair - off0.  on_pair(g, bin, key) runs for every pair written
-// (g absolute).
+// (g absolute) and returns the key stored.
 template <typename F>
 __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t c, uint32_t start,
                                           uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
@@ -229,9 +229,8 @@ __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const Bin
                 dx = li - dy * ocols;
             }
             const uint32_t bin = ((o_pa >> 16) + dy) * tiles_x + (o_pa & 0xFFFFu) + dx;
-            keys[off0 + q] = o_khi | bin;
+            keys[off0 + q] = on_pair(off0 + q, bin, o_khi | bin);
             vals[off0 + q] = o_val;
-            on_pair(off0 + q, bin, o_khi | bin);
         }
     }
 }
@@ -279,12 +278,14 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                                                      uint32_t tiles_x, uint32_t* __restrict__ keys,
                                                                      uint32_t* __restrict__ vals,
                                                                      const uint32_t* __restrict__ npairs,
-                                                                     PassCounts pc) {
+                                                                     PassCounts pc, const uint32_t* __restrict__ fcut,
+                                                                     uint32_t nbins) {
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     __shared__ uint32_t mk[kDupThreads / 64][64];        // coop_emit's start marks, per wave
+    __shared__ uint16_t scut[kDupCutBins];               // (fcut) the cut table, min(cut, 0xFFFF)
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
@@ -303,6 +304,8 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         dk[k] = dsrc[j];
         ord[k] = osrc[j];
     }
+    if (fcut)  // (a depth key is < 2^15: min(cut, 0xFFFF) keeps every comparison)
+        for (uint32_t i = tid; i < nbins; i += kDupThreads) scut[i] = (uint16_t)min(fcut[i], 0xFFFFu);
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
 #pragma unroll
@@ -337,11 +340,21 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // without its key re-read): the block's pairs are contiguous from its
     // partial, so its first kDupCountTiles tiles count in LDS
     const uint32_t t_lo = pc.C ? (uint32_t)(part / pc.tile) : 0u;
-    auto count = [&](uint32_t g, uint32_t bin, uint32_t key) {  // (pc.C) the pair's digit into its tile's counts
-        if (pc.cut && (key >> bin_bits) > pc.cut[bin]) return;  // (behind its bin's cut: the filter drops it)
+    // (fcut) the behind-the-cut mark, from the LDS table
+    auto mark = [&](uint32_t bin, uint32_t key) -> uint32_t {
+        return (key >> bin_bits) > (uint32_t)scut[bin] ? key | kBehindFlag : key;
+    };
+    auto count = [&](uint32_t g, uint32_t bin, uint32_t key) -> uint32_t {  // (pc.C) the pair's digit into its tile's counts
+        if (fcut) {
+            key = mark(bin, key);
+            if (key & kBehindFlag) return key;  // (the filter drops it)
+        } else if (pc.cut && (key >> bin_bits) > pc.cut[bin]) {
+            return key;  // (behind its bin's cut: the filter drops it)
+        }
         const uint32_t t = udiv_est(g, pc.tile), d = bin & pc.mask;
         if (t - t_lo < kDupCountTiles) atomicAdd(&lh[t - t_lo][d], 1u);
         else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
+        return key;
     };
     if (GS_DUP_COOP && !src.own.owner) {
         // wave-cooperative emission (every bin row owned): each wave's 64
@@ -360,8 +373,11 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             const uint32_t khi = dkey ? dk[k] << bin_bits : 0u;
             const uint32_t val = order ? ord[k] : j;
             if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, count);
+            else if (fcut)
+                coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+                          [&](uint32_t, uint32_t bin, uint32_t key) { return mark(bin, key); });
             else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
-                           [](uint32_t, uint32_t, uint32_t) {});
+                           [](uint32_t, uint32_t, uint32_t key) { return key; });
         }
     } else
 #pragma unroll
@@ -491,7 +507,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     const uint32_t c = rect_tile_count(lo, hi, src.own, src.masked);
     const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
     coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
-              [](uint32_t, uint32_t, uint32_t) {});
+              [](uint32_t, uint32_t, uint32_t key) { return key; });
 }
 
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
@@ -529,12 +545,16 @@ hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uin
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
-                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc) {
+                                 const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
+                                 const uint32_t* fcut, uint32_t nbins) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     // (order: dkey holds the items' depth keys in that order)
     if (dkey && bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked};
+    // (the marks: index order, the cooperative emission, the flag above the depth key)
+    if (fcut && (order || own.owner || !GS_DUP_COOP || !dkey || nbins > kDupCutBins || bin_bits + kDepthBits > 31))
+        return hipErrorInvalidValue;
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
         scan_down_kernel<<<nb, 256, 0, st>>>(src, n, partials, offsets);
@@ -549,7 +569,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
         return hipGetLastError();
     }
     scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
-                                                      npairs, pc);
+                                                      npairs, pc, fcut, nbins);
     return hipGetLastError();
 }
 

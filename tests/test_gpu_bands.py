@@ -63,3 +63,50 @@ def test_band_custom_owner_and_idle_rank(built):
     owner = np.array([0, 2, 0, 2, 2, 0, 0, 2, 0, 2], np.uint8)  # rank 1 owns nothing
     got = _bands(sc, opt, 3, V, P, W, H, owner=owner)
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("world,binning,path", [(2, "bin_first", "orbit"), (3, "bin_first", "jump"),
+                                                 (2, "depth_first", "orbit")])
+def test_band_frames_depth_cuts_bitexact(built, world, binning, path):
+    """Contiguous bands over a camera path: a clipped band bins without its
+    owner table (gs_handle::band_local), so from a buffer set's second frame
+    on its lists carry depth cuts, the bin-first duplicate marks the pairs
+    behind them, and open quadrants finish from the fallback lists.  Every
+    frame of every rank equals the 1-GPU frame bit for bit."""
+    import torch
+
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd.api import default_camera
+    from gaussian_splat_amd.distributed import HipBandBackend, assemble
+    W, H = 640, 384
+    sc = _scene(700000, 71 + world, 0, W / H)
+    sc.scale *= np.float32(2.0)  # (the bench scene's coverage per pixel: the lists saturate)
+    opt = Options(crop=False, binning=binning)
+    ref_r = InstancedSplatRenderer(sc, opt)
+    ref_r.initialize(0)
+    ranks = [HipBandBackend(sc, r, world, opt, 0) for r in range(world)]
+    cut_frames = sorted_lt_pairs = opened = ref_lt = 0
+    for k in range(8):
+        cam = default_camera(W, H)
+        if path == "orbit":
+            cam.orbit(0.02 * k, 0.005 * k)
+        else:  # still, then a jump that leaves quadrants open behind the old cuts
+            cam.orbit(0.0 if k < 5 else 0.5, 0.0 if k < 5 else 0.1)
+        V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+        ref = ref_r.render_host(V, P, W, H)
+        rs = ref_r.last_stats()
+        ref_lt += int(rs["pairs_sorted"] < rs["pairs"])
+        bands = [be.render(V, P, W, H) for be in ranks]
+        torch.cuda.synchronize()
+        got = assemble(bands, W, H, world).cpu().numpy()
+        assert int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))) == 0, f"frame {k}"
+        for be in ranks:
+            st = be.r.last_stats()
+            cut_frames += int(st["cut_frame"])
+            sorted_lt_pairs += int(st["pairs_sorted"] < st["pairs"])
+            opened += int(st["open_tiles"])
+    assert cut_frames >= world * 4, cut_frames  # (each rank: frames 3..8 have cuts)
+    assert ref_lt > 0  # (the scene saturates: the 1-GPU cuts drop pairs)
+    assert sorted_lt_pairs > 0
+    if path == "jump":
+        assert opened > 0

@@ -21,6 +21,12 @@ pmc)   B="python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --pmc 0 --no-sta
        step fetch timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- $B > $O/pmc_fetch.log 2>&1
        step write timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- $B > $O/pmc_write.log 2>&1
        python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt; grep -A1 "composite_strip_kernel<0, 1>\|preprocess_kernel<3, 1>" $O/pmc_summary.txt ;;
+pmc50m) B="python bench.py --config 50m --steps 3 --warmup 2 --cpu-baseline 0 --pmc 0 --no-stage-timing --frames-in-flight 1 --settled-probe 0 --orbit-probe 0"
+       step p50sq1 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d $O/pmc50m/sq1 -o run --output-format csv -- $B > $O/pmc50m_sq1.log 2>&1
+       step p50sq2 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE -d $O/pmc50m/sq2 -o run --output-format csv -- $B > $O/pmc50m_sq2.log 2>&1
+       step p50fetch timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc50m/fetch -o run --output-format csv -- $B > $O/pmc50m_fetch.log 2>&1
+       step p50write timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc50m/write -o run --output-format csv -- $B > $O/pmc50m_write.log 2>&1
+       python tools/pmc_summary.py $O/pmc50m > $O/pmc50m_summary.txt; grep -A1 "scan_duplicate\|rts_pass_kernel<1, 7, true" $O/pmc50m_summary.txt ;;
 prof50m) for c in 4k 50m; do
          step prof_$c bash -c "timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run --output-format csv -- \
            python bench.py --config $c --steps 20 --frames-in-flight 1 --pmc 0 --cpu-baseline 0 --settled-probe 0 --orbit-probe 0 > $O/bench_${c}_profiled.json 2> $O/bench_${c}_profiled.err"
