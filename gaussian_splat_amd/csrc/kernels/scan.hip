@@ -185,10 +185,16 @@ __device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
 // emit_bin_pairs writes there.  c: the item's pair count (0: none), start:
 // its first pair - off0.  on_pair(g, bin, key) runs for every pair written
 // (g absolute) and returns the key stored.
+// gen: the wave's chunk counter (GS_DUP_TAG: a mark carries its chunk's
+// number, so stale marks are ignored instead of cleared; mk starts at ~0).
+#ifndef GS_DUP_TAG  // A/B knob
+#define GS_DUP_TAG 0
+#endif
 template <typename F>
 __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t c, uint32_t start,
                                           uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
-                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, F&& on_pair) {
+                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t& gen,
+                                          F&& on_pair) {
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c > 0u ? start + c : 0u), 63);
     const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u;
     uint32_t inc = 0;  // with excluded bins (rect <= 4x4 bins): the included ones, bit dy*4 + dx
@@ -202,12 +208,21 @@ __device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const Bin
     const uint32_t pa = r.bx0 | (r.by0 << 16), pb = (cols & 0xFFFFu) | (inc << 16);
     uint32_t carry = 0;
     for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
+#if GS_DUP_TAG
+        ++gen;
+        wave_lds_sync();  // the last chunk's mark reads are done
+        if (c > 0u && start >= q0 && start - q0 < 64u) mk[start - q0] = gen << 7 | (lane + 1u);
+        wave_lds_sync();
+        const uint32_t mv = mk[lane];
+        uint32_t own1 = wave_scan_dpp<true>(mv >> 7 == gen ? mv & 127u : 0u);
+#else
         wave_lds_sync();  // the last chunk's mark reads are done
         mk[lane] = 0u;
         wave_lds_sync();
         if (c > 0u && start >= q0 && start - q0 < 64u) mk[start - q0] = lane + 1u;
         wave_lds_sync();
         uint32_t own1 = wave_scan_dpp<true>(mk[lane]);
+#endif
         own1 = own1 > carry ? own1 : carry;
         carry = (uint32_t)__builtin_amdgcn_readlane((int)own1, 63);
         const int ol = (int)(own1 > 0u ? own1 - 1u : 0u);
@@ -285,7 +300,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     __shared__ uint32_t mk[kDupThreads / 64][64];        // coop_emit's start marks, per wave
-    __shared__ uint16_t scut[kDupCutBins];               // (fcut) the cut table, min(cut, 0xFFFF)
+    extern __shared__ uint16_t scut[];                   // (fcut, dynamic: nbins words) the cut table, min(cut, 0xFFFF)
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
@@ -363,6 +378,8 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         // wave's other lanes idle (coop_emit; the same pairs at the same
         // offsets as the per-lane loop below)
         const uint32_t lane = tid & 63u, wave = tid >> 6;
+        uint32_t gen = 0;
+        mk[wave][lane] = ~0u;  // (no chunk's tag)
 #pragma unroll
         for (int k = 0; k < kDupIpt; ++k) {
             const uint32_t i = k * kDupThreads + tid, j = blk + i;
@@ -372,11 +389,11 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
             const uint32_t khi = dkey ? dk[k] << bin_bits : 0u;
             const uint32_t val = order ? ord[k] : j;
-            if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, count);
+            if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen, count);
             else if (fcut)
-                coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+                coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
                           [&](uint32_t, uint32_t bin, uint32_t key) { return mark(bin, key); });
-            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
                            [](uint32_t, uint32_t, uint32_t key) { return key; });
         }
     } else
@@ -506,7 +523,9 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     const BinRect r = bin_rect(lo, hi, src.masked);
     const uint32_t c = rect_tile_count(lo, hi, src.own, src.masked);
     const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
-    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals,
+    uint32_t gen = 0;
+    mk[wave][lane] = ~0u;  // (no chunk's tag)
+    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
               [](uint32_t, uint32_t, uint32_t key) { return key; });
 }
 
@@ -568,8 +587,11 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
                                                               bin_bits);
         return hipGetLastError();
     }
-    scan_duplicate_kernel<<<nb, kDupThreads, 0, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
-                                                      npairs, pc, fcut, nbins);
+    // (the cut table sized to the frame: a block that fits beside the previous
+    // composite's workgroups starts sooner)
+    const size_t lds = fcut ? ((size_t)nbins * 2 + 15) & ~(size_t)15 : 0;
+    scan_duplicate_kernel<<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
+                                                        npairs, pc, fcut, nbins);
     return hipGetLastError();
 }
 

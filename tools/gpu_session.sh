@@ -12,5 +12,5 @@ run bands_4k 300 --frames 10 --width 3840 --height 2160
 run bands_50m 500 --frames 8 --splats 50000000 --width 3840 --height 2160 --sh 0 --seed 4
 # A/B: pw8 (every sort pass at 8 waves per SIMD), ipt4 (2048-pair sort tiles), nomask (timing
 # ablation: no exclusion masks in the projection; changes the pairs) at configs 5 and 3
-STEPS=ab ROUNDS=1 VARIANTS="base pw8 ipt4 nomask" BENCH_ARGS="--config 50m --steps 20 --settled-probe 0 --orbit-probe 0" bash tools/gpu_r05.sh || exit 1
-STEPS=ab ROUNDS=2 VARIANTS="base pw8 ipt4" bash tools/gpu_r05.sh || exit 1
+STEPS=ab ROUNDS=1 VARIANTS="base tag pw8 ipt4 nomask" BENCH_ARGS="--config 50m --steps 20 --settled-probe 0 --orbit-probe 0" bash tools/gpu_r05.sh || exit 1
+STEPS=ab ROUNDS=2 VARIANTS="base notag tag" bash tools/gpu_r05.sh || exit 1
