@@ -364,6 +364,7 @@ def main():
         rh = r
         drain = None
         ms = timed(step, args.steps, args.warmup)
+        s_timed = r.last_stats()  # (the timed frames' lists, before the probes below move the camera)
         settled_line = settled_probe(step, args.steps)
         if args.camera == "fixed" and args.orbit_probe:
             # camera sensitivity: the default camera is the
@@ -391,7 +392,10 @@ def main():
                           "binning": {1: "depth-first", 2: "bin-first"}.get(int(os_.get("binning", 0)), "?"),
                           "note": "the same K frames on an orbiting camera (0.01 rad per frame about the target), "
                                   "after the settled probe, with their own warmup; reported beside the value"}
-            for _ in range(args.warmup):  # (back to the fixed camera for the kernel and stage timing)
+            # back to the fixed camera for the kernel and stage timing, for as
+            # many frames as the orbit's cut dilation takes to decay (one bin of
+            # radius per 8 frames without an open quadrant, per buffer set)
+            for _ in range(args.warmup + 2 * 8 * 5):
                 step()
     else:
         from gaussian_splat_amd.distributed import (BandRenderer, HipBandBackend, HipShardBackend, HipSlabBackend,
@@ -434,7 +438,7 @@ def main():
         settled_line = settled_probe(step, args.steps, drain=drain)
     value = N / (ms * 1e-3) / 1e6
 
-    s0 = rh.last_stats()
+    s0 = s_timed if world == 1 else rh.last_stats()
     binning = {1: "depth-first", 2: "bin-first"}.get(int(s0.get("binning", 0)), "?")
     pipelined = world == 1 and args.frames_in_flight >= 2
     timed_k, n_co = {}, min(max(args.steps, 3), 64)

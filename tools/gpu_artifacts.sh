@@ -39,7 +39,7 @@ heavy) step heavy bash -c "timeout -k 10 600 python bench.py --profile heavy --s
 orbit) for p in uniform heavy; do
          step orbit_$p bash -c "timeout -k 10 600 python bench.py --camera orbit --profile $p --steps 50 --cpu-baseline 0 --pmc 0 > $O/bench_orbit_$p.json 2> $O/bench_orbit_$p.err"
          python -c "import json;d=json.load(open('$O/bench_orbit_$p.json'));c=d['config'];print('orbit $p', d['ms_per_step'], c['pairs'], c['pairs_sorted'], c['open_tiles'])"; done ;;
-timeline) step timeline bash -c "timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pmc 0 --no-stage-timing > $O/tl.log 2>&1"
+timeline) step timeline bash -c "timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pmc 0 --no-stage-timing --settled-probe 0 --orbit-probe 0 > $O/tl.log 2>&1"
        python tools/trace_timeline.py $(find $O/tl -name "*kernel_trace.csv" | head -1) 3 > $O/timeline_fif2.txt; head -30 $O/timeline_fif2.txt ;;
 rows50m) step rows50m bash -c "timeout -k 10 900 python tools/rows_probe.py --splats 50000000 --width 3840 --height 2160 --sh 0 --frames 10 > $O/rows_probe_virtual_ranks_50m.json 2> $O/rows_probe_50m.err"
        tail -5 $O/rows_probe_50m.err ;;
