@@ -57,8 +57,8 @@ class Options:
     # per-bin depth cuts (gs_options.depth_split; tile/live50 rules, no cap): a frame's
     # bin lists hold the pairs in front of the depth at which the bin's tiles saturated two frames
     # back, and a quadrant those lists leave open finishes from its saved state with the rest of
-    # its bin's pairs.  Single-GPU frames and row-scheme rank renders alike.  The same image bit
-    # for bit, fewer pairs sorted; True is the default (False: whole lists)
+    # its bin's pairs.  Single-GPU frames, row-scheme rank renders and contiguous band renders alike.
+    # The same image bit for bit, fewer pairs sorted; True is the default (False: whole lists)
     depth_split: bool = True
 
     def to_c(self) -> GsOptions:

@@ -78,8 +78,9 @@ typedef struct gs_options {
                               sort of the splats, then binning), 2 = bin-first (bin lists in
                               arrival order, then a stable per-bin depth sort).  DESIGN.md §1 */
     int32_t depth_split;   /* per-bin depth cuts (modes tile/live50, no cap;
-                              single-GPU frames and the row scheme's rank renders,
-                              gs_shard_render, alike): 1 (gs_default_options) = a frame's bin lists
+                              single-GPU frames, the row scheme's rank renders
+                              (gs_shard_render) and band renders of contiguous rows
+                              (gs_band_render) alike): 1 (gs_default_options) = a frame's bin lists
                               hold only the pairs at or in front of their bin's cut, the depth at
                               which the bin's tiles saturated in the previous frame on the same
                               buffer set, plus a margin; a tile those lists leave open finishes

@@ -285,3 +285,28 @@ def test_binning_model_heavy_orbit_picks_bin_first(built):
     torch.cuda.synchronize()
     assert picks[0] == 1, picks  # (the first frame at a resolution: depth-first, P unknown)
     assert all(p == 2 for p in picks[1:]), picks  # (2 = bin-first)
+
+
+@pytest.mark.parametrize("w,h", [(4128, 4128), (1920, 1080)])
+def test_depth_cuts_cut_table_sizes(built, w, h):
+    """The duplicate marks the pairs behind their cut from an LDS copy of the
+    cut table when the frame has at most kDupCutBins (16,384) bins; a larger
+    frame (129 x 129 bins) keeps the sort's own gather of cut[bin].  Both,
+    with a jump that opens quadrants (the fallback filter masks the mark off),
+    equal whole lists bit for bit."""
+    from gaussian_splat_amd.api import default_camera
+    sc = _scene(400000, 41, 0, w / h, scale=1.2)
+    cut, whole = _pair(sc, binning="bin_first")
+    far = default_camera(w, h)
+    far.setDistance(7.0)
+    near = default_camera(w, h)
+    near.setDistance(2.5)
+    near.orbit(0.3, 0.1)
+    opened = sorted_lt = 0
+    for cam in (far, far, far, near, near, far):
+        V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
+        assert _bits(cut.render_host(V, P, w, h), whole.render_host(V, P, w, h)) == 0
+        st = cut.last_stats()
+        opened += st["open_tiles"]
+        sorted_lt += int(st["pairs_sorted"] < st["pairs"])
+    assert sorted_lt > 0 and opened > 0
