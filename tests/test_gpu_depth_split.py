@@ -287,15 +287,15 @@ def test_binning_model_heavy_orbit_picks_bin_first(built):
     assert all(p == 2 for p in picks[1:]), picks  # (2 = bin-first)
 
 
-@pytest.mark.parametrize("w,h", [(4128, 4128), (1920, 1080)])
-def test_depth_cuts_cut_table_sizes(built, w, h):
+@pytest.mark.parametrize("w,h,n,scale", [(4128, 4128, 400000, 1.2), (1920, 1080, 1500000, 2.0)])
+def test_depth_cuts_cut_table_sizes(built, w, h, n, scale):
     """The duplicate marks the pairs behind their cut from an LDS copy of the
     cut table when the frame has at most kDupCutBins (16,384) bins; a larger
     frame (129 x 129 bins) keeps the sort's own gather of cut[bin].  Both,
     with a jump that opens quadrants (the fallback filter masks the mark off),
     equal whole lists bit for bit."""
     from gaussian_splat_amd.api import default_camera
-    sc = _scene(400000, 41, 0, w / h, scale=1.2)
+    sc = _scene(n, 41, 0, w / h, scale=scale)
     cut, whole = _pair(sc, binning="bin_first")
     far = default_camera(w, h)
     far.setDistance(7.0)
