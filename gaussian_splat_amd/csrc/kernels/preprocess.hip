@@ -126,6 +126,10 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 #define GS_PRE_EARLY 0     // (one dependent round trip fewer, bytes for culled splats too)
 #endif
 
+#ifndef GS_PRE_FULLREC  // A/B knob: 1 = culled splats of a full frame write a zero record (whole-line record stores)
+#define GS_PRE_FULLREC 1
+#endif
+
 #ifndef GS_PRE_WAVES  // A/B knob: min waves per SIMD (caps the VGPRs)
 #define GS_PRE_WAVES 8
 #endif
@@ -325,6 +329,18 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
             }
         }
     }
+#if GS_PRE_FULLREC
+    // a culled splat writes a zero record too, so a wave's record stores
+    // cover whole lines instead of leaving holes (partially written lines);
+    // no list ever holds a culled splat, so its record is never read.  Not in
+    // band frames, whose clipped rects cull most splats: there the zeros
+    // would outweigh the records.
+    if (rlo == kEmptyRectLo && U.band_y0 == 0 && U.band_y1 == U.height - 1) {  // (a visible splat's x0 < 0xFFFF)
+        float4* o = rec + kRecFloat4 * (size_t)i;
+#pragma unroll
+        for (int k = 0; k < kRecFloat4; ++k) o[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#endif
     dkey[i] = key;
     rect_lo[i] = rlo;
     rect_hi[i] = rhi;
