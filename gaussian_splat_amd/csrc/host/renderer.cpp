@@ -49,6 +49,12 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_DUP_FLAG  // A/B knob: 1 = the bin-first duplicate marks the pairs behind their cut (kBehindFlag)
 #define GS_DUP_FLAG 1
 #endif
+#ifndef GS_CUT_DILATE_AHEAD  // A/B knob: 1 = the next frame's dilated cuts are made by this frame's tail
+#define GS_CUT_DILATE_AHEAD 1
+#endif
+#ifndef GS_FB_LDS  // A/B knob: 1 = the fallback lists' filter tests an LDS copy of its table
+#define GS_FB_LDS 1
+#endif
 #ifndef GS_BAND_LOCAL  // A/B knob: 1 = contiguous band frames bin without an owner table (gs_handle::band_local)
 #define GS_BAND_LOCAL 1
 #endif
@@ -186,10 +192,13 @@ struct gs_handle {
     // frame reads (cut_r[set] > 0); cut_r: the set's dilation radius in bins,
     // raised while its frames leave quadrants open (the counts come back in
     // host_total[6 + set], written by cut_finalize) and lowered again after
-    // kCutCalm frames with none.
+    // kCutCalm frames with none.  dil_r: the radius of the set's table in
+    // cutdil dilated ahead, by the tail of the frame that wrote the cuts (on
+    // the composite stream, off the next frame's critical path); 0 = none.
     DevBuf qrec, cutbuf, cutord, cutdil, wcost, cstate, fkeys, fvals, fbtab, fbn, scratch2, kept;
     int cut_r[2] = {0, 0};
     int cut_calm[2] = {0, 0};
+    int dil_r[2] = {0, 0};
     uint32_t cut_bins = 0;       // bins per table in cutbuf
     int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
     int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
@@ -232,7 +241,7 @@ struct gs_handle {
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &alt_rlo,
                           &alt_rhi, &alt_qrec, &alt_fkeys, &alt_fvals, &seg_sample, &npairs, &fetch, &qrec, &cutbuf,
-                          &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart})
+                          &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart, &cutord, &cutdil, &wcost})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -767,8 +776,19 @@ hipError_t reserve_after(DevBuf& b, size_t bytes, hipStream_t st) {
 
 // Depth cuts apply to this frame's composite rule and size:
 // tile / live50 rules, no fragment cap, the depth key above the bin id.
-constexpr int kCutDilateMax = 4;  // bins (a 9x9 neighbourhood)
+#ifndef GS_CUT_DILATE_MAX  // A/B knobs of the dilation controller
+#define GS_CUT_DILATE_MAX 3
+#endif
+#ifndef GS_CUT_OPEN_TOL
+#define GS_CUT_OPEN_TOL 0
+#endif
+constexpr int kCutDilateMax = GS_CUT_DILATE_MAX;  // bins (3: a 7x7 neighbourhood)
 constexpr int kCutCalm = 8;       // frames with no open quadrant before the radius drops by one
+// open quadrants a frame may leave without widening the radius: a few cost the
+// fallback lists little (they run on the composite stream, off the next
+// frame's chain), a wider radius costs every bin's front list
+// (profiles/r05/ab_dilate_radius.txt)
+constexpr uint64_t kCutOpenTolerated = GS_CUT_OPEN_TOL;
 
 bool cut_rule(const gs_handle* h, const gs::FrameUniforms& U) {
     return h->opt.cap == 0 && (h->opt.mode == GS_MODE_TILE || h->opt.mode == GS_MODE_LIVE50) &&
@@ -802,6 +822,8 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
         GS_HIP(h->cutord.reserve((size_t)T * 4 * 4));
         GS_HIP(h->wcost.reserve((size_t)T * 2 * 4));
+        GS_HIP(h->cutdil.reserve((size_t)2 * T * 4));
+        h->dil_r[0] = h->dil_r[1] = 0;
         h->cut_bins = T;
         h->cut_valid[0] = h->cut_valid[1] = false;
     }
@@ -820,8 +842,10 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         const uint64_t opened = h->host_total ? h->host_total[6 + S] : ~0ull;
         if (h->host_total) h->host_total[6 + S] = ~0ull;  // (consumed; ~0: no new count since)
         if (opened != ~0ull) {
-            if (opened > 0) {
+            if (opened > kCutOpenTolerated) {
                 h->cut_r[S] = std::min(h->cut_r[S] + 1, kCutDilateMax);
+                h->cut_calm[S] = 0;
+            } else if (opened > 0) {
                 h->cut_calm[S] = 0;
             } else if (h->cut_r[S] > 0 && ++h->cut_calm[S] >= kCutCalm) {
                 --h->cut_r[S];
@@ -830,17 +854,19 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         }
         static const char* fixed_r = std::getenv("GS_CUT_DILATE");  // (A/B: a fixed radius)
         if (fixed_r) h->cut_r[S] = std::max(0, std::atoi(fixed_r));
-        if (h->cut_in && h->cut_r[S] > 0) {
-            if (h->cutdil.bytes < (size_t)2 * T * 4) {  // (a composite may still read the other set's table)
-                GS_HIP(hipStreamSynchronize(st));
-                GS_HIP(hipStreamSynchronize(sp));
-                GS_HIP(h->cutdil.reserve((size_t)2 * T * 4));
-            }
-            uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)S * T;
+        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)S * T;
+        if (h->cut_in && h->cut_r[S] > 0 && GS_CUT_DILATE_AHEAD && h->dil_r[S] >= h->cut_r[S]) {
+            // dilated ahead by the tail of the frame that wrote these cuts
+            // (a wider radius than the controller's now only moves pairs from
+            // the fallback lists to the front lists: the same image)
+            h->cut_in = d;
+            h->stats.cut_dilate = (uint32_t)h->dil_r[S];
+        } else if (h->cut_in && h->cut_r[S] > 0) {  // (the radius just grew: on the side stream, ahead of the lists)
             GS_HIP(gs::launch_cut_dilate(h->cut_in, d, (uint32_t)U.tiles_x, (uint32_t)U.tiles_y, h->cut_r[S], sp));
             h->cut_in = d;
             h->stats.cut_dilate = (uint32_t)h->cut_r[S];
         }
+        h->dil_r[S] = 0;  // (cutdil[S] is this frame's input now; the tail may dilate the next one)
     }
     // (the order tables are written by single-GPU frames only, and a change
     // of ownership invalidates the cuts, so a valid cut table has its order)
@@ -882,6 +908,19 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     // the set's next composite's longest-first bin order (single-GPU frames),
     // from what this frame's workgroups fetched
     if (ca.wcost && h->ord_out) GS_HIP(gs::launch_order_bins(ca.wcost, T, h->ord_out, sc));
+    // the set's next cuts, dilated here at the set's current radius while a
+    // moving camera keeps them dilated (setup_cuts then reads them without a
+    // kernel ahead of the projection).  cutdil[set] may be this frame's own
+    // input: its readers (the duplicate's marks, the pass-1 composite,
+    // cut_finalize) are all ordered before this point.  On the composite
+    // stream, which has slack while the side stream's projection and chain
+    // bound the frame (1080p); a stream of its own measured no better
+    // (profiles/r05/ab_dilate_radius.txt).
+    if (GS_CUT_DILATE_AHEAD && h->cut_out && h->cut_r[h->set] > 0 && h->cutdil.bytes >= (size_t)2 * T * 4) {
+        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)h->set * T;
+        GS_HIP(gs::launch_cut_dilate(h->cut_out, d, (uint32_t)U.tiles_x, (uint32_t)U.tiles_y, h->cut_r[h->set], sc));
+        h->dil_r[h->set] = h->cut_r[h->set];
+    }
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
 #ifdef GS_AB_NO_FALLBACK  // timing ablation build only: exact only while no quadrant is left open
     return GS_OK;
@@ -898,6 +937,9 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     // (a marked frame's pairs carry kBehindFlag above the depth key: the test
     // and the kept keys go without it)
     if (bits + gs::kDepthBits <= 31) flt.kmask = ~gs::kBehindFlag;
+    // (the table tested in LDS: every pair of the frame is tested against a
+    // few open bins; GS_FB_LDS=0: the global gather, A/B)
+    if (GS_FB_LDS && T <= gs::kDupCutBins) flt.lds_bins = T;
     // (usually no quadrant is open and the sort's input is empty: a fixed
     // grid that loops over the tiles then costs a few workgroups, not one
     // per tile of the frame's pairs)

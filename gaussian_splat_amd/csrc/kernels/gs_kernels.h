@@ -185,6 +185,10 @@ struct SortFilter {
     // frame's fallback lists; the pass stores kept keys masked with it)
     uint32_t flag = 0;
     uint32_t kmask = ~0u;
+    // lds_bins > 0 (<= kDupCutBins): the count and pass kernels copy the cut
+    // table into LDS as 16-bit words first and test against that copy (the
+    // fallback lists' filter: a few open bins, every pair of the frame tested)
+    uint32_t lds_bins = 0;
     __device__ __forceinline__ bool keep(uint32_t key) const {
         if (flag) return (key & kBehindFlag) == 0u;
         return (((key & kmask) >> dshift) <= cut[key & bmask]) != (behind != 0u);

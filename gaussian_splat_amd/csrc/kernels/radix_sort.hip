@@ -79,6 +79,16 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
+// SortFilter::keep against the LDS copy of the cut table (SortFilter::lds_bins)
+__device__ __forceinline__ bool keep_lds(const SortFilter& f, const uint16_t* tab, uint32_t key) {
+    return (((key & f.kmask) >> f.dshift) <= (uint32_t)tab[key & f.bmask]) != (f.behind != 0u);
+}
+// Copies the cut table into LDS (min(cut, 0xFFFF): depth keys are < 2^15).
+__device__ __forceinline__ void stage_filter_table(const SortFilter& f, uint16_t* tab) {
+    for (uint32_t i = threadIdx.x; i < f.lds_bins; i += blockDim.x) tab[i] = (uint16_t)min(f.cut[i], 0xFFFFu);
+    __syncthreads();
+}
+
 // FILT (the first pass of a depth-cut frame's bin sort, SortFilter): only
 // the items at or ahead of their bin's cut are counted and sorted.  Compiled
 // in only where it is used, so the other kernels keep their registers.
@@ -90,7 +100,9 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
     if (n_dev) n = *n_dev;  // tiles past it count zeros
     if (n == 0u) return;    // (nothing to sort: the scan and the pass return at once)
     __shared__ uint32_t h[kRsWaves][kSortBins];
+    extern __shared__ uint16_t ftab[];  // (FILT, flt.lds_bins words)
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    if (FILT && flt.lds_bins) stage_filter_table(flt, ftab);
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     for (int i = tid; i < kRsWaves * kSortBins; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
@@ -104,7 +116,7 @@ __global__ __launch_bounds__(512) void rts_count_kernel(const uint32_t* __restri
         for (int k = 0; k < K; ++k) kk[k] = keys[min(t0 + k * kRsThreads + tid, n - 1u)];
         bool keep[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) keep[k] = !FILT || flt.keep(kk[k]);
+        for (int k = 0; k < K; ++k) keep[k] = !FILT || (flt.lds_bins ? keep_lds(flt, ftab, kk[k]) : flt.keep(kk[k]));
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (t0 + k * kRsThreads + tid < n && keep[k])
@@ -205,6 +217,8 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    extern __shared__ uint16_t ftab[];  // (FILT, flt.lds_bins words)
+    if (FILT && flt.lds_bins) stage_filter_table(flt, ftab);
     for (uint32_t tile = blockIdx.x; tile * TILE < n; tile += gridDim.x) {
     for (uint32_t i = tid; i < kRsWaves * ND; i += kRsThreads) (&wh[0][0])[i] = 0;
     // Keys and all value arrays are loaded up front so their latency hides
@@ -282,7 +296,9 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
     if constexpr (FILT) {
         if (tile == 0 && tid == 0) *flt.kept = all;  // (the items every tile keeps)
 #pragma unroll
-        for (int k = 0; k < IPT; ++k) keep |= (base + k * 64 + lane < n && flt.keep(key[k])) ? 1u << k : 0u;
+        for (int k = 0; k < IPT; ++k)
+            keep |= (base + k * 64 + lane < n && (flt.lds_bins ? keep_lds(flt, ftab, key[k]) : flt.keep(key[k])))
+                        ? 1u << k : 0u;
     }
     // slot k of this lane holds an item to sort
     auto kept = [&](int k) -> bool {
@@ -414,16 +430,16 @@ size_t radix_sort_scratch_words(uint32_t n) {
 // rts_pass_kernel for a digit width (the ballot match unrolled per width);
 // STRIDE: `tiles` workgroups loop over all the tiles
 template <int NV, bool FILT, bool STRIDE = false, typename... A>
-static hipError_t launch_pass(int width, uint32_t tiles, hipStream_t st, A... args) {
+static hipError_t launch_pass(int width, uint32_t tiles, hipStream_t st, size_t lds, A... args) {
     switch (width) {
-    case 1: rts_pass_kernel<NV, 1, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 2: rts_pass_kernel<NV, 2, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 3: rts_pass_kernel<NV, 3, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 4: rts_pass_kernel<NV, 4, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 5: rts_pass_kernel<NV, 5, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 6: rts_pass_kernel<NV, 6, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 7: rts_pass_kernel<NV, 7, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
-    case 8: rts_pass_kernel<NV, 8, FILT, STRIDE><<<tiles, kRsThreads, 0, st>>>(args...); break;
+    case 1: rts_pass_kernel<NV, 1, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 2: rts_pass_kernel<NV, 2, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 3: rts_pass_kernel<NV, 3, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 4: rts_pass_kernel<NV, 4, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 5: rts_pass_kernel<NV, 5, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 6: rts_pass_kernel<NV, 6, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 7: rts_pass_kernel<NV, 7, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
+    case 8: rts_pass_kernel<NV, 8, FILT, STRIDE><<<tiles, kRsThreads, lds, st>>>(args...); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -437,6 +453,8 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
     // (first_counted with a filter: the producer counted only the kept items,
     // PassCounts::cut; not with the strided fallback grids)
     if (flt.cut && (NV != 1 || !flt.kept || (first_counted && flt.stride_grid))) return hipErrorInvalidValue;
+    if (flt.lds_bins > kDupCutBins || (flt.lds_bins && flt.flag)) return hipErrorInvalidValue;
+    const size_t flds = flt.lds_bins ? ((size_t)flt.lds_bins * 2 + 15) & ~(size_t)15 : 0;  // (dynamic LDS of the filtered kernels)
     *result_in_tmp = false;
     const SortPlan plan = make_sort_plan(bits, NV > 1);
     if (n == 0 || plan.passes == 0) return hipSuccess;
@@ -466,15 +484,15 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
             if (flt.cut && flt.stride_grid) {  // (every pass on a fixed grid looping over the tiles)
                 const uint32_t g = tiles < flt.stride_grid ? tiles : flt.stride_grid;
                 if (filt)
-                    rts_count_kernel<NV, true, true><<<g, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                    rts_count_kernel<NV, true, true><<<g, kRsThreads, flds, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
                                                                              tiles, n_dev, flt);
                 else
                     rts_count_kernel<NV, false, true><<<g, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p],
                                                                               C, tiles, n_dev, SortFilter{});
                 rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
-                e = filt ? launch_pass<NV, true, true>(plan.width[p], g, st, io, n, plan.shift[p], plan.mask[p], C,
+                e = filt ? launch_pass<NV, true, true>(plan.width[p], g, st, flds, io, n, plan.shift[p], plan.mask[p], C,
                                                        totals, tiles, rg, rmask, n_dev, flt)
-                         : launch_pass<NV, false, true>(plan.width[p], g, st, io, n, plan.shift[p], plan.mask[p], C,
+                         : launch_pass<NV, false, true>(plan.width[p], g, st, 0, io, n, plan.shift[p], plan.mask[p], C,
                                                         totals, tiles, rg, rmask, n_dev, SortFilter{});
                 if (e != hipSuccess) return e;
                 if (filt) n_dev = flt.kept;
@@ -485,10 +503,10 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
             }
             if (filt) {
                 if (!first_counted)
-                    rts_count_kernel<NV, true><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
+                    rts_count_kernel<NV, true><<<tiles, kRsThreads, flds, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
                                                                             tiles, n_dev, flt);
                 rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
-                e = launch_pass<NV, true>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+                e = launch_pass<NV, true>(plan.width[p], tiles, st, flds, io, n, plan.shift[p], plan.mask[p], C, totals,
                                           tiles, rg, rmask, n_dev, flt);
             }
         }
@@ -497,7 +515,7 @@ static hipError_t radix_sort_impl(const uint32_t* keys_in, const uint32_t* const
                 rts_count_kernel<NV, false><<<tiles, kRsThreads, 0, st>>>(io.kin, n, plan.shift[p], plan.mask[p], C,
                                                                          tiles, n_dev, SortFilter{});
             rts_scan_kernel<<<plan.mask[p] + 1, kRsScanThreads, 0, st>>>(C, tiles, totals, n_dev);
-            e = launch_pass<NV, false>(plan.width[p], tiles, st, io, n, plan.shift[p], plan.mask[p], C, totals,
+            e = launch_pass<NV, false>(plan.width[p], tiles, st, 0, io, n, plan.shift[p], plan.mask[p], C, totals,
                                        tiles, rg, rmask, n_dev, SortFilter{});
         }
         if (e != hipSuccess) return e;
