@@ -1,9 +1,7 @@
 #!/bin/bash
-# Session: the longest-first composite in two launches (GS_STRIP_SPLIT = 20 / 40 % of the bins in the
-# second launch, running into the next frame's chain) against one launch; 1080p 2 rounds, 4K 1 round;
-# then the depth-cut GPU tests on split20.
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-STEPS=ab ROUNDS=2 VARIANTS="base split20 split40" BENCH_ARGS="--orbit-probe 0" bash tools/gpu_r05.sh || exit 1
-STEPS=ab ROUNDS=1 VARIANTS="base split20 split40" BENCH_ARGS="--config 4k --steps 30 --settled-probe 0 --orbit-probe 0" bash tools/gpu_r05.sh || exit 1
-GSPLAT_LIB=$PWD/ab/split20.so timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread \
-  -k "depth or parity or oracle" > gpurun_out/pytest_split.log 2>&1; echo "split tests rc=$?"; tail -2 gpurun_out/pytest_split.log
+# Session: depth cuts on/off (GS_DEPTH_SPLIT) at the sparse configs: 1M @1080p SH0 and the heavy scene, 2 rounds.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
+for r in 1 2; do for cfg in "--config 1m" "--profile heavy"; do for ds in 1 0; do
+  GS_DEPTH_SPLIT=$ds timeout -k 10 300 python bench.py $cfg --steps 50 --cpu-baseline 0 --pmc 0 --orbit-probe 0 > gpurun_out/ds.json 2> gpurun_out/ds.err || { tail -3 gpurun_out/ds.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/ds.json'));c=d['config'];print('$cfg ds=$ds r$r', d['ms_per_step'], d['settled']['ms_per_step'], c['pairs'], c['pairs_sorted'], {k:round(v['ms'],4) for k,v in d['stages'].items()})"
+done; done; done
