@@ -493,6 +493,9 @@ __global__ __launch_bounds__(256, MODE == 3 ? 4 : 8) __attribute__((amdgpu_num_s
 #ifndef GS_COMPOSITE_LPT  // A/B knob: 0 = row-major bin order even when CompositeArgs::order is set
 #define GS_COMPOSITE_LPT 1
 #endif
+#ifndef GS_STRIP_PRIO_TOP  // the first batches' issue priority (then one lower every two batches)
+#define GS_STRIP_PRIO_TOP 3
+#endif
 #ifndef GS_STRIP_PRIO  // A/B knob: 1 = issue priority falls with the batches a workgroup has walked
 #define GS_STRIP_PRIO 1
 #endif
@@ -660,9 +663,9 @@ __global__ __launch_bounds__(256, GS_STRIP_WAVES) __attribute__((amdgpu_num_sgpr
         // starved behind older ones (age arbitration) into a long drain
         {
             const uint32_t nb = (b - rg.x) / kTileThreads;
-            if (nb == 0) __builtin_amdgcn_s_setprio(3);
-            else if (nb == 2) __builtin_amdgcn_s_setprio(2);
-            else if (nb == 4) __builtin_amdgcn_s_setprio(1);
+            if (nb == 0) __builtin_amdgcn_s_setprio(GS_STRIP_PRIO_TOP);
+            else if (nb == 2) __builtin_amdgcn_s_setprio(GS_STRIP_PRIO_TOP > 1 ? GS_STRIP_PRIO_TOP - 1 : 0);
+            else if (nb == 4) __builtin_amdgcn_s_setprio(GS_STRIP_PRIO_TOP > 2 ? GS_STRIP_PRIO_TOP - 2 : 0);
             else if (nb == 6) __builtin_amdgcn_s_setprio(0);
         }
 #endif

@@ -126,6 +126,10 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 #define GS_PRE_EARLY 0     // (one dependent round trip fewer, bytes for culled splats too)
 #endif
 
+#ifndef GS_PRE_PRIO  // A/B knob: issue priority (0..3) of the projection's waves
+#define GS_PRE_PRIO 0
+#endif
+
 #ifndef GS_PRE_FULLREC  // A/B knob: 1 = culled splats of a full frame write a zero record (whole-line record stores)
 #define GS_PRE_FULLREC 1
 #endif
@@ -146,6 +150,11 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
                                                          unsigned long long* __restrict__ zero8,
                                                          const PreFuse fuse, const ShardFuse shard) {
     uint32_t i = blockIdx.x * 256u + threadIdx.x;
+#if GS_PRE_PRIO
+    // (A/B) the projection bounds the pipelined frame (projection + chain):
+    // its waves ahead of the co-running composite's in issue arbitration
+    __builtin_amdgcn_s_setprio(GS_PRE_PRIO);
+#endif
     if (i < 2 && zero8) zero8[i] = 0ull;
     if constexpr (EPI == 0)
         if (i >= s.n) return;
