@@ -55,6 +55,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_FB_LDS  // A/B knob: 1 = the fallback lists' filter tests an LDS copy of its table
 #define GS_FB_LDS 1
 #endif
+#ifndef GS_HOST_SET_WAIT  // A/B knob: 1 = the host waits for a buffer set's last reader (no GPU wait packet)
+#define GS_HOST_SET_WAIT 1
+#endif
 #ifndef GS_BAND_LOCAL  // A/B knob: 1 = contiguous band frames bin without an owner table (gs_handle::band_local)
 #define GS_BAND_LOCAL 1
 #endif
@@ -1529,7 +1532,14 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     }
     // (a wait packet only when that composite may still run: each costs a
     // few us of stream bubble)
-    if (hipEventQuery(h->set_free[h->set]) != hipSuccess) GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
+    if (hipEventQuery(h->set_free[h->set]) != hipSuccess) {
+        // (GS_HOST_SET_WAIT, A/B) the host waits instead of a wait packet in
+        // the side stream: the set's last composite ends with the co-run, long
+        // before the side stream finishes the previous frame's chain, so the
+        // projection is still queued in time and its stream has no barrier
+        if (GS_HOST_SET_WAIT && pipe) GS_HIP(hipEventSynchronize(h->set_free[h->set]));
+        else GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
+    }
     if (pipe && !h->last_pipe) {  // the side stream starts after everything the caller's stream holds
         GS_HIP(hipEventRecord(h->sorted_ev, st));
         GS_HIP(hipStreamWaitEvent(sp, h->sorted_ev, 0));
