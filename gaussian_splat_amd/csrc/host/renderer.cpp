@@ -1820,7 +1820,8 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     if (!view || !proj || W <= 0 || H <= 0) return fail(GS_ERR_INVALID_ARG, "shard frame: bad arguments");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
     *U = make_uniforms(view, proj, W, H);
-    GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));  // a pipelined composite may still read the set
+    // a pipelined composite may still read the set (a wait packet only then)
+    if (hipEventQuery(h->set_free[h->set]) != hipSuccess) GS_HIP(hipStreamWaitEvent(st, h->set_free[h->set], 0));
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = true;
     h->slab_lists = false;
