@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -54,6 +55,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #endif
 #ifndef GS_FB_LDS  // A/B knob: 1 = the fallback lists' filter tests an LDS copy of its table
 #define GS_FB_LDS 1
+#endif
+#ifndef GS_HOST_POLL  // A/B knob: 1 = the host polls the pair count's sequence word instead of an event
+#define GS_HOST_POLL 0
 #endif
 #ifndef GS_HOST_SET_WAIT  // A/B knob: 1 = the host waits for a buffer set's last reader (no GPU wait packet)
 #define GS_HOST_SET_WAIT 1
@@ -140,6 +144,7 @@ struct gs_handle {
     int stats_set = -1;                 // buffer set of the frame in `stats` (its fetch counter)
     int64_t stats_fixed_bytes = 0;      // composite bytes besides the records: range words + output
     hipEvent_t totals_ev = nullptr;     // P is in host_total
+    unsigned long long totals_seq = 0;  // (GS_HOST_POLL) the last totals kernel's sequence number, host_total[5]
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
         int32_t w = 0, h = 0;
         int64_t n = -1;
@@ -638,6 +643,23 @@ bool pick_bin_first(gs_handle* h, const gs::FrameUniforms& U, uint32_t m, int nr
 // tail (optional): queues what reads the lists (per-bin sort, composite ...)
 // right behind them, before the host waits for P, so that the GPU never waits
 // for the host; called again, with the lists, if they are queued again.
+// Waits until the totals kernel has published sequence number `seq` in
+// host_total[5] (its release store follows total[0..4]).  The kernel is a few
+// microseconds behind the projection, so the host spins; past a second it
+// falls back to a stream sync (an error if the word still differs).
+hipError_t wait_totals(gs_handle* h, unsigned long long seq, hipStream_t st) {
+    volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(h->host_total) + 5;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (__atomic_load_n(reinterpret_cast<const unsigned long long*>(h->host_total) + 5, __ATOMIC_ACQUIRE) == seq)
+            return hipSuccess;
+        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) break;
+    }
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    return *w == seq ? hipSuccess : hipErrorUnknown;
+}
+
 using ListTail = std::function<gs_status(const uint32_t* sorted_vals)>;
 gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const uint32_t* rect_lo,
                           const uint32_t* rect_hi, const gs::FrameUniforms& U, const Ownership& own, bool timed,
@@ -677,17 +699,21 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         flt.flag = GS_DUP_FLAG && !order && !own.dev.owner && T <= gs::kDupCutBins &&
                    bits + gs::kDepthBits <= 31 ? 1u : 0u;
     }
+    // the host learns P by polling the totals kernel's sequence word in
+    // host-mapped memory (GS_HOST_POLL) or by an event in its dispatch packet
+    const unsigned long long seq = GS_HOST_POLL ? ++h->totals_seq : 0ull;
+    hipEvent_t tev = GS_HOST_POLL ? nullptr : h->totals_ev;
     if (fused) {
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
                                               h->partials.as<uint64_t>(), h->dev_total,
                                               h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
-                                              st, h->totals_ev));
+                                              st, tev, seq));
         h->ppart_dirty = false;
     } else {
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
                                             h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set,
                                             h->ranges.as<uint2>(), T, np, cap, pc.C,
-                                            pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, h->totals_ev));
+                                            pc.C ? (pc.mask + 1) * pc.ntiles : 0u, st, tev, seq));
     }
     if (timed) mark(h, 3, st);
     // pairs (bin, splat) in visiting order (bin-first: the depth key above the
@@ -730,7 +756,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     GS_HIP(enqueue_lists());
     gs_status ts = lists_done();
     if (ts != GS_OK) return ts;
-    GS_HIP(hipEventSynchronize(h->totals_ev));  // (the GPU goes on with the lists meanwhile)
+    if (seq) {  // (the GPU goes on with the lists meanwhile)
+        GS_HIP(wait_totals(h, seq, st));
+    } else {
+        GS_HIP(hipEventSynchronize(h->totals_ev));
+    }
     const uint64_t P = h->host_total[0], P_all = P;
     h->stats.visible = (int64_t)h->host_total[1];
     if (fused && P_all > 0) {  // the duplicate's wave-max work (PreFuse), for the binning-order model

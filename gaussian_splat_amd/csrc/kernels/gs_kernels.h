@@ -71,7 +71,8 @@ constexpr int kScanItems = 4096;  // per block
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr);
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done = nullptr,
+                                    unsigned long long seq = 0);
 // (done: recorded by the totals kernel's own dispatch packet, not a separate
 // marker packet, which would leave a ~6 us bubble in the stream.)
 // The scan half alone, after a preprocess with PreFuse: the block sums in
@@ -80,7 +81,10 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // frame.
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done = nullptr);
+                                      hipEvent_t done = nullptr, unsigned long long seq = 0);
+// (seq > 0: after total[0..4] the totals kernel stores seq into total[5] with
+// a system-scope release, for a host that polls host-mapped `total` instead
+// of waiting for `done`.)
 // The first LSD pass's digit counts of the pairs, C[digit][tile] with
 // `ntiles` columns, tiles of `tile` pairs, digit = bin & mask: the index-order
 // duplicate adds them up as it writes (C zeroed before), so the sort skips

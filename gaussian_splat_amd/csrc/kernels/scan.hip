@@ -108,7 +108,8 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
                                                                      uint32_t* __restrict__ npairs, uint64_t cap,
-                                                                     unsigned long long* __restrict__ src) {
+                                                                     unsigned long long* __restrict__ src,
+                                                                     unsigned long long seq) {
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
@@ -151,6 +152,9 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         total[1] = vt;
         total[4] = wt;
         if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
+        // (seq: the host polls total[5]; the totals are visible before it)
+        if (seq) __hip_atomic_store(reinterpret_cast<unsigned long long*>(total) + 5, seq, __ATOMIC_RELEASE,
+                                    __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -532,7 +536,8 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
 hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rect_hi, uint32_t n, RowOwnership own,
                                     bool masked, uint64_t* partials, uint64_t* total, uint32_t* seg_sample,
                                     uint2* ranges, uint32_t nranges, uint32_t* npairs, uint64_t cap,
-                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done) {
+                                    uint32_t* zero, uint32_t nzero, hipStream_t st, hipEvent_t done,
+                                    unsigned long long seq) {
     const CountSrc src{rect_lo, rect_hi, own, masked};
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) {
@@ -548,16 +553,16 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, nullptr);
+                          total, seg_sample, npairs, cap, nullptr, seq);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done) {
+                                      hipEvent_t done, unsigned long long seq) {
     if (!part) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, part);
+                          total, seg_sample, npairs, cap, part, seq);
     return hipGetLastError();
 }
 
