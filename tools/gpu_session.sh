@@ -1,8 +1,8 @@
 #!/bin/bash
-# Session: the host polls the pair count's sequence word in host-mapped memory (GS_HOST_POLL) instead of an
-# event in the totals kernel's dispatch packet: GPU tests on poll first, then A/B 3 rounds at 1080p, 4K 1 round.
+# Session: the GPU suite and smoke() on HEAD.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-GSPLAT_LIB=$PWD/ab/poll.so timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_poll.log 2>&1
-rc=$?; echo "poll tests rc=$rc"; tail -2 gpurun_out/pytest_poll.log; [ $rc -eq 0 ] || exit 1
-STEPS=ab ROUNDS=3 VARIANTS="base poll" bash tools/gpu_r05.sh || exit 1
-STEPS=ab ROUNDS=1 VARIANTS="base poll" BENCH_ARGS="--config 4k --steps 30 --settled-probe 0 --orbit-probe 0" bash tools/gpu_r05.sh || exit 1
+STEPS=tests bash tools/gpu_r05.sh || exit 1
+grep -q " passed" gpurun_out/pytest_gpu.log && ! grep -q "failed" gpurun_out/pytest_gpu.log || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_head.json 2> gpurun_out/bench_driver_head.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/bench_driver_head.json'));print(d['ms_per_step'], d['value'], d['settled']['ms_per_step'], d['orbit']['ms_per_step'])"
