@@ -12,29 +12,31 @@ does not exist offline):
   50m              BASELINE config 5: 50M-splat stress scene @3840x2160, SH 0
   1m               BASELINE config 2: 1M splats @1920x1080, SH 0
 
-Multi-GPU is STRONG scaling over one global scene: `--gpus N` (without
-torchrun) starts N rank processes itself (torch.distributed.run, one rank per
-GPU, 127.0.0.1) before anything touches a GPU; under torchrun WORLD_SIZE must
-equal --gpus.  value = global splats / frame time (max over ranks).  The
-exact multi-GPU schemes run by default (--scheme all), each timed on its own,
-and `value` is the faster of the two at this world size:
-  rows   rank r renders the splat-index shard [r*N/g, (r+1)*N/g) of the global
-         scene (generated chunk-wise, so a rank builds only its shard):
-         bin-row ownership + all_to_all of projected records + band gather
-  bands  SURVEY §8(e)'s fallback: every rank holds the whole scene and
-         renders its own bin rows (gs_band_render), then the band gather
-rows and bands are bit-identical to one GPU's frame.  Rows are link-bound at 2
-ranks (about half of every rank's records cross the one xGMI link between
-them) and bands need no exchange, so the headline scheme follows the world
-size; both are reported in `schemes` and the choice in `scheme_choice`.  Rows frames run one at
-a time unless --pipeline-rows 1 (frame k's exchange under frame k-1's render),
-which stays opt-in until a multi-GPU RCCL run of it is recorded.  `value` is the rows
-scheme's, the north star's splat-index sharding (a replicated
-scene must not become the headline of a splat-sharded config); bands are
-reported beside it in `schemes`.  The north star's depth slabs +
-transmittance all_gather + RGBA reduce (--scheme slabs / both) do NOT meet
-its 1e-4 tolerance (pixels at the 0.99 break) and are not
-part of the default run.
+Multi-GPU is STRONG scaling over one global scene; value = global splats /
+frame time (max over ranks).  Two launchers:
+  group  (`--gpus N` outside torchrun, the default there): ONE process drives
+         all N GPUs through the C-ABI group (gs_create_sharded_from_handle,
+         RCCL over xGMI: csrc/host/group.cpp)
+  ranks  (the driver's torchrun line, or --launcher ranks, which starts it):
+         one process per GPU, torch.distributed over RCCL (distributed.py);
+         WORLD_SIZE must equal --gpus
+Both time the two exact multi-GPU schemes (bit-identical to one GPU's frame)
+over the same K frames and report both in `schemes`:
+  rows   the north star's splat-index sharding: rank r holds the shard
+         [r*N/g, (r+1)*N/g) of the global scene (generated chunk-wise, so a
+         rank builds only its shard); 32-px bin-row ownership, all-to-all of
+         the projected records, band gather.  Two frames in flight by default
+         (--pipeline-rows 1): frame k's all-to-all under frame k-1's render
+  bands  SURVEY §8(e)'s fallback: the scene REPLICATED on every rank, each
+         renders its own bin rows, band gather; no exchange
+The headline rule (stated identically in DESIGN.md §6e and README): `value`
+is the rows scheme's whenever rows is at least as fast as bands at this world
+size; otherwise bands', named as the replicated scheme in
+`config.parallelism` and `scheme_choice`.  Rows are link-bound at 2 ranks
+(about half of every rank's records cross the one xGMI link between them).
+The north star's depth slabs + transmittance all_gather + RGBA reduce
+(--scheme slabs / both) do NOT meet its 1e-4 tolerance (pixels at the 0.99
+break) and are not part of the default run.
 
 At N=1 the line also carries
   roofline      the dominant kernel's algorithmic bytes / its standalone
@@ -117,11 +119,15 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="N=1: 2 = a frame's projection/sort overlaps the previous frame's composite")
     ap.add_argument("--scheme", default="all", choices=["rows", "slabs", "bands", "both", "all"],
-                    help="N>1: all = rows (exact; value) + bands (exact); slabs = depth slabs + RGBA reduce "
-                         "(approximate, outside the 1e-4 tolerance); both = rows + slabs")
-    ap.add_argument("--pipeline-rows", type=int, default=0,
-                    help="N>1: 1 = rows frames pipelined (frame k's exchange under frame k-1's render, a second "
-                         "communicator); opt-in until a multi-GPU RCCL run of it is recorded (ADVICE r4)")
+                    help="N>1: all = rows (splat-sharded) + bands (replicated), both exact; value = rows' when it is "
+                         "at least as fast as bands, else bands'; slabs = depth slabs + RGBA reduce (approximate, "
+                         "outside the 1e-4 tolerance); both = rows + slabs")
+    ap.add_argument("--pipeline-rows", type=int, default=1,
+                    help="N>1: 1 = rows frames pipelined (frame k's all-to-all under frame k-1's render, a second "
+                         "communicator set); 0 = one frame at a time")
+    ap.add_argument("--launcher", default="group", choices=["group", "ranks"],
+                    help="--gpus N outside torchrun: group = one process drives every GPU (gs_create_sharded, "
+                         "RCCL); ranks = one process per GPU (torch.distributed.run, the driver's launch line)")
     ap.add_argument("--orbit-probe", type=int, default=1,
                     help="N=1, fixed camera: after the settled probe, time the same K frames once more with an "
                          "orbiting camera (a new view every frame) and report them as 'orbit' (0 = skip)")
@@ -148,6 +154,27 @@ def spawn_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
     return subprocess.call(cmd)
+
+
+def headline(schemes, order):
+    """The headline scheme (README, this module's docstring):
+    rows, the north star's splat-index sharding, whenever it is at least as
+    fast as the replicated-scene bands at this world size; else bands."""
+    exact = [k for k in ("rows", "bands") if k in schemes]
+    if not exact:
+        return order[0], exact
+    if "rows" in exact and ("bands" not in exact or schemes["rows"]["ms"] <= schemes["bands"]["ms"]):
+        return "rows", exact
+    return "bands", exact
+
+
+def scheme_choice(head, exact, world):
+    if len(exact) < 2:
+        return head
+    return (f"{head}: rows (splat-sharded) is the headline whenever it is at least as fast as bands (the scene "
+            f"replicated on every rank); at world size {world} {head} was "
+            + ("(rows at most bands' time)" if head == "rows" else "faster (rows are link-bound at few ranks)")
+            + "; both timed over the same frames, reported in schemes, bit-identical to the 1-GPU frame")
 
 
 def stage_summary(stats_list):
@@ -245,12 +272,117 @@ def kernel_entry(ms, nbytes, pmc):
     return e
 
 
+def group_main(args):
+    """`--gpus N` outside torchrun: ONE process drives all N GPUs through the
+    C-ABI group (gs_create_sharded_from_handle / gs_create_replicated_from_
+    handle, csrc/host/group.cpp), collectives over RCCL (xGMI) when every rank
+    has its own device.  GS_BENCH_SAME_DEVICE=1 (a one-GPU rehearsal, never set
+    by the driver) puts every rank on device 0: peer copies, or the test RCCL
+    stub when GS_RCCL_LIB names it."""
+    import torch
+
+    from gaussian_splat_amd import scene as S
+    from gaussian_splat_amd.api import InstancedSplatRenderer, Options, ShardedGroup, default_camera
+
+    N, W, H, G = args.splats, args.width, args.height, args.gpus
+    same = os.environ.get("GS_BENCH_SAME_DEVICE") == "1"
+    devices = [0] * G if same else list(range(G))
+    if not same and torch.cuda.device_count() < G:
+        sys.exit(f"bench.py: --gpus {G} but {torch.cuda.device_count()} devices")
+    transport = ("rccl" if os.environ.get("GS_RCCL_LIB") else "copy") if same else "auto"
+    scene = S.activate(S.synthetic_raw(N, seed=args.seed, aspect=W / H, rest=args.sh > 0, profile=args.profile),
+                       args.sh)
+    cam = default_camera(W, H)
+    view, proj = cam.getViewMatrix(), cam.getProjectionMatrix()
+    src = InstancedSplatRenderer(scene, Options(mode=args.mode, sh_degree=args.sh, crop=False))
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0")
+    pipe = bool(args.pipeline_rows) and args.frames_in_flight >= 2
+
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    def timed(step, steps, warmup, drain=None):
+        for _ in range(args.settle + warmup):
+            step()
+        if drain is not None:
+            drain()
+        sync_all()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        if drain is not None:  # (pipelined rows: the last frame finishes inside the timed region)
+            drain()
+        sync_all()
+        return (time.perf_counter() - t0) * 1e3 / steps
+
+    schemes, groups = {}, {}
+    order = {"both": ["rows"], "all": ["bands", "rows"]}.get(args.scheme, [args.scheme])
+    for sch in order:
+        if sch == "slabs":
+            continue  # (the approximate scheme: torch.distributed launcher only)
+        g = ShardedGroup(src, G, replicated=(sch == "bands"))
+        g.initialize(devices, transport)
+        drain = None
+        if sch == "rows" and pipe:
+            g.set_frames_in_flight(2)
+            step = (lambda g_=g: g_.render_pipelined(view, proj, W, H, out=out))
+            drain = (lambda g_=g: g_.flush(W, H, out=out))
+        else:
+            step = (lambda g_=g: g_.render(view, proj, W, H, out=out))
+        schemes[sch] = {"ms": timed(step, args.steps, args.warmup, drain), "step": step, "drain": drain,
+                        "transport": g.transport}
+        groups[sch] = g
+    head, exact = headline(schemes, order)
+    ms = schemes[head]["ms"]
+    settled_line = None
+    if args.settled_probe > 0:
+        for _ in range(args.settled_probe):
+            schemes[head]["step"]()
+        settled_line = {"extra_frames": args.settled_probe,
+                        "ms_per_step": round(timed(schemes[head]["step"], args.steps, 0, schemes[head]["drain"]), 4),
+                        "note": "the same frames timed again after the value's run and these extra untimed frames"}
+    s0 = groups[head].last_stats(0)
+    tr = schemes[head]["transport"]
+    par = (f"rows: {G} GPUs from one process (gs_create_sharded), splat-index shards of one global scene, 32-px "
+           f"bin-row ownership, all-to-all of projected records + band gather ({tr}"
+           + ("; 2 frames in flight: a frame's all-to-all under the previous frame's render" if pipe else "") + ")"
+           if head == "rows" else
+           f"bands: {G} GPUs from one process (gs_create_replicated), the scene REPLICATED on every rank (not "
+           f"splat-sharded), each renders its 32-px bin rows, band gather ({tr})")
+    line = {
+        "metric": "Msplats/sec + achieved HBM GB/s (6M-splat scene @1080p, SH3, full frame)"
+        if args.config == "1080p" else f"Msplats/sec + achieved HBM GB/s ({args.label})",
+        "value": round(N / (ms * 1e-3) / 1e6, 2), "unit": "Msplats/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "settle": {"frames": args.settle, "note": "untimed frames before the warmup (--settle), per timed scheme"},
+        "settled": settled_line, "orbit": None, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic (seeded 3DGS-statistics scene, {args.profile} scales; no garden .ply offline)",
+        "hbm_gbs": None,
+        "config": {"workload": args.label, "global_splats": N, "width": W, "height": H, "sh_degree": args.sh,
+                   "parallelism": par, "launcher": "group (one process, csrc/host/group.cpp)",
+                   "devices": devices, "pairs": int(s0["pairs"]), "visible": int(s0["visible"])},
+        "comm": {"backend": tr, "ranks": G},
+        "schemes": {k: {"ms_per_step": round(v["ms"], 4), "value": round(N / (v["ms"] * 1e-3) / 1e6, 2),
+                        "transport": v["transport"]} for k, v in schemes.items()},
+        "scheme_choice": scheme_choice(head, exact, G),
+    }
+    if same:
+        line["rehearsal"] = ("every rank on device 0 (GS_BENCH_SAME_DEVICE): the protocol, not xGMI; "
+                             + ("RCCL entry points from GS_RCCL_LIB" if transport == "rccl" else "peer copies"))
+    print(json.dumps(line), flush=True)
+    for g in groups.values():
+        g.close()
+
+
 def main():
     args = parse()
     if args.camera == "orbit" and args.gpus > 1:
         sys.exit("bench.py: --camera orbit is a single-GPU workload")
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
+        if args.launcher == "group":
+            return group_main(args)
         sys.exit(spawn_ranks(args))
     world = int(world_env or "1")
     if world != args.gpus:
@@ -401,7 +533,9 @@ def main():
         from gaussian_splat_amd.distributed import (BandRenderer, HipBandBackend, HipShardBackend, HipSlabBackend,
                                                     ShardedRenderer, SlabRenderer)
 
-        order = {"both": ["rows", "slabs"], "all": ["rows", "bands"]}.get(args.scheme, [args.scheme])
+        # (bands first: no exchange; rows on process groups of their own, so
+        # the default group only times)
+        order = {"both": ["rows", "slabs"], "all": ["bands", "rows"]}.get(args.scheme, [args.scheme])
         for sch in order:
             if sch == "bands":  # the whole scene on every rank
                 full = S.activate(S.synthetic_raw(N, seed=args.seed, aspect=W / H, rest=args.sh > 0,
@@ -418,21 +552,14 @@ def main():
                 be = HipShardBackend(scene, rank, world, b, opts, local)
                 # two frames in flight: frame k's record exchange (its own
                 # communicator) overlaps frame k-1's render and gather
-                pipe = args.frames_in_flight >= 2 and args.pipeline_rows
-                sr = ShardedRenderer(be, rank, world, pipeline=pipe,
+                pipe = args.frames_in_flight >= 2 and bool(args.pipeline_rows)
+                sr = ShardedRenderer(be, rank, world, group=dist.new_group(backend=backend), pipeline=pipe,
                                      exchange_group=dist.new_group(backend=backend) if pipe else None)
             stp = (lambda s_=sr: s_.render(view, proj, W, H, gather=True))
             drn = getattr(sr, "flush", None) if getattr(sr, "pipeline", False) else None
             schemes[sch] = {"ms": timed(stp, args.steps, args.warmup, drain=drn), "handle": be.r, "step": stp,
                             "drain": drn}
-        # The headline is the faster of the exact schemes that ran (both timed
-        # over the same K frames, both reported in `schemes`): rows (splat-index
-        # shards + record exchange) are link-bound at 2 ranks, where one xGMI
-        # link carries about half of every rank's records, and the replicated
-        # scene's bands need no exchange.  `scheme_choice` names
-        # the rule; `config.parallelism` the scheme.
-        exact = [k for k in ("rows", "bands") if k in schemes]
-        head = min(exact, key=lambda k: schemes[k]["ms"]) if exact else order[0]
+        head, exact = headline(schemes, order)
         ms, rh, step = schemes[head]["ms"], schemes[head]["handle"], schemes[head]["step"]
         drain = schemes[head]["drain"]
         settled_line = settled_probe(step, args.steps, drain=drain)
@@ -498,8 +625,8 @@ def main():
                                         f"{world}" + ("; 2 frames in flight: a frame's exchange under the previous "
                                                       "frame's render" if drain is not None else "") + ")")
                                        if head == "rows" else
-                                       (f"bands: {world} ranks, the scene replicated on every rank, each renders its "
-                                        f"32-px bin rows, band gather ({backend}, world {world})")
+                                       (f"bands: {world} ranks, the scene REPLICATED on every rank (not splat-sharded), "
+                                        f"each renders its 32-px bin rows, band gather ({backend}, world {world})")
                                        if head == "bands" else
                                        (f"slabs: {world} ranks, splat-index shards, depth slabs + RGBA reduce "
                                         f"(approximate; {backend}, world {world})"))
@@ -519,9 +646,7 @@ def main():
             line["comm"] = {"backend": dist.get_backend(), "ranks": dist.get_world_size()}
             line["schemes"] = {k: {"ms_per_step": round(v["ms"], 4), "value": round(N / (v["ms"] * 1e-3) / 1e6, 2)}
                                for k, v in schemes.items()}
-            line["scheme_choice"] = (f"{head}: the faster exact scheme at world size {world} (rows and bands both "
-                                     "timed over the same frames and reported in schemes; both bit-identical to the "
-                                     "1-GPU frame)") if len(exact) > 1 else head
+            line["scheme_choice"] = scheme_choice(head, exact, world)
             if "slabs" in line["schemes"]:
                 line["schemes"]["slabs"]["note"] = ("depth slabs + transmittance all_gather + RGBA reduce "
                                                     "(approximate, outside the 1e-4 tolerance: reassociated transmittance product)")

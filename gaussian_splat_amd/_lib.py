@@ -41,7 +41,10 @@ class GsStats(C.Structure):
                 ("cut_dilate", C.c_uint32)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        # deprecated aliases of the ABI-10 renames (gsplat.h gs_stats), kept for one release
+        d["two_slab"], d["depth_cut"] = d["cut_frame"], d["cut_dilate"]
+        return d
 
 
 # name -> (restype, argtypes); every symbol include/gsplat.h declares.
@@ -92,6 +95,10 @@ SIGNATURES = {
     "gs_group_set_scheme": (C.c_int, [_P, C.c_int32]),
     "gs_group_set_timeout": (C.c_int, [_P, C.c_int32]),
     "gs_group_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P]),
+    "gs_group_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
+    "gs_group_render_pipelined": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int32, _P,
+                                            C.POINTER(C.c_int32)]),
+    "gs_group_flush": (C.c_int, [_P, _P, C.c_int32, _P, C.POINTER(C.c_int32)]),
     "gs_group_point_count": (C.c_int64, [_P]),
     "gs_group_size": (C.c_int32, [_P]),
     "gs_group_transport": (C.c_int32, [_P]),

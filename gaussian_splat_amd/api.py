@@ -458,6 +458,49 @@ class ShardedGroup:
                                     0, None), "gs_group_render")
         return out
 
+    def set_frames_in_flight(self, n: int):
+        """2: rows frames pipelined (gs_group_render_pipelined), one frame's
+        all-to-all under the previous frame's render and gather."""
+        check(lib().gs_group_set_frames_in_flight(self._g, int(n)), "gs_group_set_frames_in_flight")
+
+    def render_pipelined(self, view, proj, width: int, height: int, out=None, stream=None, host: bool = False):
+        """Projects this view's frame and returns the PREVIOUS call's frame
+        (None on the first call): a device tensor on the caller's stream, or
+        with host=True a numpy array.  flush() returns the last one."""
+        return self._pipelined(view, proj, width, height, out, stream, host)
+
+    def flush(self, width: int = 0, height: int = 0, out=None, stream=None, host: bool = False):
+        """The frame still in flight (None when there is none); its size is
+        the one it was projected at."""
+        return self._pipelined(None, None, width, height, out, stream, host)
+
+    def _pipelined(self, view, proj, width, height, out, stream, host):
+        import torch
+
+        produced = C.c_int32(0)
+        # (the frame that comes back is the one in flight: its size, not this view's)
+        prev = getattr(self, "_inflight", None)
+        self._inflight = (width, height) if view is not None else None
+        ow, oh = prev if prev is not None else (width, height)
+        if host:
+            buf = np.empty((oh, ow, 4), np.float32)
+            ptr, dev_out, st = buf.ctypes.data, 0, None
+        else:
+            if out is None:
+                out = torch.empty((oh, ow, 4), dtype=torch.float32, device=f"cuda:{self.device or 0}")
+            assert out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()
+            assert out.numel() >= ow * oh * 4, "out holds the frame in flight (the previous call's size)"
+            buf, ptr, dev_out = out, out.data_ptr(), 1
+            st = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        if view is None:
+            check(lib().gs_group_flush(self._g, C.c_void_p(ptr), dev_out, C.c_void_p(st), C.byref(produced)),
+                  "gs_group_flush")
+        else:
+            check(lib().gs_group_render_pipelined(self._g, _mat16(view), _mat16(proj), int(width), int(height),
+                                                  C.c_void_p(ptr), dev_out, C.c_void_p(st), C.byref(produced)),
+                  "gs_group_render_pipelined")
+        return buf if produced.value else None
+
     def last_stats(self, rank: int = 0) -> dict:
         s = GsStats()
         check(lib().gs_group_last_stats(self._g, int(rank), C.byref(s)), "gs_group_last_stats")

@@ -10,6 +10,12 @@
 //   rows  (default; the frame is bit-identical to one GPU's)
 //     gs_shard_project -> all-to-all of exchange records -> gs_shard_render
 //     -> each rank's band of bin rows into the frame on devices[0]
+//     With two frames in flight (gs_group_set_frames_in_flight 2,
+//     gs_group_render_pipelined) a call projects frame k and starts its
+//     all-to-all on the ranks' exchange streams (a communicator set of its
+//     own), then renders frame k-1, whose records arrived under frame k's
+//     projection, and gathers it on the ranks' gather streams: the link
+//     time of one frame hides under the other's compute.
 //   slabs (the north star's depth slabs + RGBA reduce)
 //     gs_slab_project -> all-reduce of the depth histogram -> gs_slab_pack
 //     -> all-to-all -> gs_slab_render -> all-gather of the transmittance
@@ -217,6 +223,16 @@ struct Rank {
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     DevMem send, recv, band, hist, tloc, tall, contrib, stage;
     std::vector<int64_t> counts;  // records to each rank
+    // two frames in flight (rows): compute, exchange and gather streams of the
+    // rank, the exchange buffers per frame slot, and the events between them:
+    // ev_proj (a frame's records are packed), ev_xdone[s] (slot s's all-to-all
+    // is done: its send buffer is free, its receive buffer full), ev_rdone[s]
+    // (slot s's records are rendered: its receive buffer is free), ev_gdone
+    // (the band's gather is done: the band is free)
+    hipStream_t cs = nullptr, xs = nullptr, gs = nullptr;
+    DevMem psend[2], precv[2];
+    std::vector<int64_t> pcounts[2];
+    hipEvent_t ev_proj = nullptr, ev_xdone[2] = {}, ev_rdone[2] = {}, ev_gdone = nullptr;
     gs_status status = GS_OK;
     std::string error;
 };
@@ -239,18 +255,37 @@ struct gs_group {
     int64_t timeout_ms = 60000;       // bound of every host wait (gs_group_set_timeout)
     bool timeout_set = false;         // set by gs_group_set_timeout (GS_COMM_TIMEOUT_MS then ignored)
     bool failed = false;              // communicators aborted: the group is unusable
+    // two frames in flight (rows scheme, gs_group_render_pipelined)
+    int frames_in_flight = 1;
+    bool pipe_ready = false;          // the ranks' pipeline streams and events exist
+    std::vector<ncclComm_t> xcomms;   // the all-to-all's own communicators (RCCL)
+    int pslot = 0;                    // exchange slot of the next projected frame
+    struct Pending {                  // the frame whose records are in flight
+        bool on = false;
+        int slot = 0, width = 0, height = 0;
+        std::vector<int64_t> nrec;
+    } pend;
     ~gs_group() {
         delete pool;
         for (auto& k : r) {
             if (k.dev >= 0) (void)hipSetDevice(k.dev);
-            for (DevMem* m : {&k.send, &k.recv, &k.band, &k.hist, &k.tloc, &k.tall, &k.contrib, &k.stage}) m->release();
+            for (hipStream_t q : {k.cs, k.xs, k.gs})
+                if (q) (void)hipStreamSynchronize(q);
+            for (DevMem* m : {&k.send, &k.recv, &k.band, &k.hist, &k.tloc, &k.tall, &k.contrib, &k.stage, &k.psend[0],
+                              &k.psend[1], &k.precv[0], &k.precv[1]})
+                m->release();
             if (k.own_stream && k.st) (void)hipStreamDestroy(k.st);
             if (k.ev_ready) (void)hipEventDestroy(k.ev_ready);
             if (k.ev_done) (void)hipEventDestroy(k.ev_done);
+            for (hipStream_t q : {k.cs, k.xs, k.gs})
+                if (q) (void)hipStreamDestroy(q);
+            for (hipEvent_t e : {k.ev_proj, k.ev_xdone[0], k.ev_xdone[1], k.ev_rdone[0], k.ev_rdone[1], k.ev_gdone})
+                if (e) (void)hipEventDestroy(e);
             gs_destroy(k.h);
         }
         // (a failure has aborted and cleared every handle already)
         gscomm::destroy_all(comms, [](ncclComm_t c) { return g_rccl.comm_destroy(c); });
+        gscomm::destroy_all(xcomms, [](ncclComm_t c) { return g_rccl.comm_destroy(c); });
         if (frame_done) (void)hipEventDestroy(frame_done);
         fb.release();
     }
@@ -292,8 +327,10 @@ gs_status run_ranks(gs_group* g, const std::function<gs_status(Rank&, int)>& f) 
 
 // Abort every communicator after a peer error or an expired wait.
 gs_status comm_failure(gs_group* g, const std::string& why) {
-    if (g->transport == GS_TRANSPORT_RCCL)
+    if (g->transport == GS_TRANSPORT_RCCL) {
         gscomm::abort_all(g->comms, [](ncclComm_t c) { return g_rccl.comm_abort(c); });
+        gscomm::abort_all(g->xcomms, [](ncclComm_t c) { return g_rccl.comm_abort(c); });
+    }
     g->failed = true;
     return gfail(GS_ERR_COMM, why);
 }
@@ -309,11 +346,12 @@ gs_status wait_bounded(gs_group* g, int dev, hipEvent_t ev, const char* what) {
         if (e == hipSuccess) return GS_OK;
         if (e != hipErrorNotReady) GG_HIP(e);
         if (g->transport == GS_TRANSPORT_RCCL)
-            for (ncclComm_t c : g->comms) {
-                ncclResult_t ae = ncclSuccess;
-                if (c && g_rccl.async_error(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
-                    return comm_failure(g, std::string(what) + ": RCCL peer error: " + g_rccl.error_string(ae));
-            }
+            for (const auto* set : {&g->comms, &g->xcomms})
+                for (ncclComm_t c : *set) {
+                    ncclResult_t ae = ncclSuccess;
+                    if (c && g_rccl.async_error(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+                        return comm_failure(g, std::string(what) + ": RCCL peer error: " + g_rccl.error_string(ae));
+                }
         const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
         if (ms > g->timeout_ms)
             return comm_failure(g, std::string(what) + ": no completion within " + std::to_string(g->timeout_ms) + " ms");
@@ -599,6 +637,219 @@ gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int 
     return GS_OK;
 }
 
+// ---- two frames in flight, rows scheme (gs_group_render_pipelined) ---------
+
+// The ranks' compute / exchange / gather streams and their events, and (RCCL)
+// a second communicator set for the all-to-all, so that frame k's exchange
+// and frame k-1's gather, issued on different streams, never share a
+// communicator.  Made at the first pipelined frame.
+gs_status ensure_pipeline(gs_group* g) {
+    if (g->pipe_ready) return GS_OK;
+    for (Rank& k : g->r) {
+        GG_HIP(hipSetDevice(k.dev));
+        for (hipStream_t* q : {&k.cs, &k.xs, &k.gs})
+            if (!*q) GG_HIP(hipStreamCreateWithFlags(q, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&k.ev_proj, &k.ev_xdone[0], &k.ev_xdone[1], &k.ev_rdone[0], &k.ev_rdone[1], &k.ev_gdone})
+            if (!*e) GG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        // (recorded once, so every first wait on them is satisfied at once)
+        for (hipEvent_t e : {k.ev_xdone[0], k.ev_xdone[1], k.ev_rdone[0], k.ev_rdone[1], k.ev_gdone})
+            GG_HIP(hipEventRecord(e, k.cs));
+    }
+    if (g->transport == GS_TRANSPORT_RCCL && g->xcomms.empty()) {
+        std::vector<int> dev;
+        for (const Rank& k : g->r) dev.push_back(k.dev);
+        g->xcomms.assign((size_t)g->world, nullptr);
+        const ncclResult_t rc = g_rccl.comm_init_all(g->xcomms.data(), g->world, dev.data());
+        if (rc != ncclSuccess) {
+            g->xcomms.clear();
+            return gfail(GS_ERR_COMM, std::string("ncclCommInitAll (exchange communicators): ") + g_rccl.error_string(rc));
+        }
+    }
+    g->pipe_ready = true;
+    return GS_OK;
+}
+
+// Frame k's all-to-all from slot s's send buffers into slot s's receive
+// buffers, on the exchange streams: each waits for its rank's projection of
+// frame k and for the render that last read its receive buffer (frame k-2).
+// The same transfer plan as exchange(), so the copy transport the one-GPU
+// tests run checks the offsets the RCCL path uses.
+gs_status exchange_pipelined(gs_group* g, int s, std::vector<int64_t>* nrec) {
+    const int W = g->world;
+    const int64_t xb = gs_exchange_record_bytes();
+    int32_t rb[GS_XREGIONS];
+    const int nreg = gs_exchange_regions(rb);
+    std::vector<std::vector<int64_t>> counts((size_t)W);
+    std::vector<int64_t> sent((size_t)W, 0);
+    nrec->assign((size_t)W, 0);
+    for (int q = 0; q < W; ++q) {
+        counts[(size_t)q] = g->r[(size_t)q].pcounts[s];
+        for (int d = 0; d < W; ++d) {
+            (*nrec)[(size_t)d] += counts[(size_t)q][(size_t)d];
+            sent[(size_t)q] += counts[(size_t)q][(size_t)d];
+        }
+    }
+    for (int d = 0; d < W; ++d) {
+        Rank& kd = g->r[(size_t)d];
+        GG_HIP(hipSetDevice(kd.dev));
+        const size_t want = (size_t)std::max<int64_t>((*nrec)[(size_t)d], 1) * xb;
+        if (want > kd.precv[s].bytes) GG_HIP(hipEventSynchronize(kd.ev_rdone[s]));  // (growth frees the buffer)
+        GG_HIP(kd.precv[s].reserve(kd.dev, want));
+        GG_HIP(hipStreamWaitEvent(kd.xs, kd.ev_rdone[s], 0));
+        for (const Rank& ks : g->r) GG_HIP(hipStreamWaitEvent(kd.xs, ks.ev_proj, 0));  // (every source's records)
+    }
+    const std::vector<Xfer> plan = exchange_plan(counts);
+    if (g->transport == GS_TRANSPORT_RCCL) GG_NCCL(g_rccl.group_start());
+    int64_t pre = 0;
+    for (int k = 0; k < nreg; pre += rb[k], ++k) {
+        const int64_t b = rb[k];
+        for (const Xfer& x : plan) {
+            Rank &ks = g->r[(size_t)x.src], &kd = g->r[(size_t)x.dst];
+            char* src = ks.psend[s].as<char>() + pre * sent[(size_t)x.src] + x.soff * b;
+            char* dst = kd.precv[s].as<char>() + pre * (*nrec)[(size_t)x.dst] + x.roff * b;
+            if (g->transport == GS_TRANSPORT_RCCL) {
+                GG_NCCL(g_rccl.send(src, (size_t)(x.n * b), ncclUint8, x.dst, g->xcomms[(size_t)x.src], ks.xs));
+                GG_NCCL(g_rccl.recv(dst, (size_t)(x.n * b), ncclUint8, x.src, g->xcomms[(size_t)x.dst], kd.xs));
+            } else {
+                GG_HIP(hipSetDevice(kd.dev));
+                GG_HIP(hipMemcpyPeerAsync(dst, kd.dev, src, ks.dev, (size_t)(x.n * b), kd.xs));
+            }
+        }
+    }
+    if (g->transport == GS_TRANSPORT_RCCL) GG_NCCL(g_rccl.group_end());
+    for (Rank& k : g->r) {
+        GG_HIP(hipSetDevice(k.dev));
+        GG_HIP(hipEventRecord(k.ev_xdone[s], k.xs));
+    }
+    return GS_OK;
+}
+
+// The rendered frame's bands into `out` on the gather streams (each waits for
+// its rank's render), then the caller's stream waits for the gather.
+gs_status gather_pipelined(gs_group* g, int Wd, int Ht, float* out, hipStream_t user) {
+    const int W = g->world;
+    Rank& r0 = g->r[0];
+    auto span = [&](int d, size_t* off, size_t* bytes) {
+        int row0, nrows;
+        owned_rows(Ht, W, d, &row0, &nrows);
+        const int y0 = row0 * gs::kBin, y1 = std::min(Ht, (row0 + nrows) * gs::kBin);
+        *off = (size_t)y0 * Wd * 4;
+        *bytes = y1 > y0 ? (size_t)(y1 - y0) * Wd * 16 : 0;
+    };
+    for (Rank& k : g->r) {
+        GG_HIP(hipSetDevice(k.dev));
+        GG_HIP(hipStreamWaitEvent(k.gs, k.ev_done, 0));
+    }
+    GG_HIP(hipSetDevice(r0.dev));
+    for (int d = 1; d < W; ++d) GG_HIP(hipStreamWaitEvent(r0.gs, g->r[(size_t)d].ev_done, 0));
+    if (g->transport == GS_TRANSPORT_RCCL) {
+        GG_NCCL(g_rccl.group_start());
+        for (int d = 1; d < W; ++d) {
+            size_t off, bytes;
+            span(d, &off, &bytes);
+            if (!bytes) continue;
+            GG_NCCL(g_rccl.send(g->r[(size_t)d].band.ptr, bytes, ncclUint8, 0, g->comms[(size_t)d], g->r[(size_t)d].gs));
+            GG_NCCL(g_rccl.recv(out + off, bytes, ncclUint8, d, g->comms[0], r0.gs));
+        }
+        GG_NCCL(g_rccl.group_end());
+    } else {
+        GG_HIP(hipSetDevice(r0.dev));
+        for (int d = 1; d < W; ++d) {
+            size_t off, bytes;
+            span(d, &off, &bytes);
+            if (bytes)
+                GG_HIP(hipMemcpyPeerAsync(out + off, r0.dev, g->r[(size_t)d].band.ptr, g->r[(size_t)d].dev, bytes, r0.gs));
+        }
+    }
+    size_t off, bytes;
+    span(0, &off, &bytes);
+    GG_HIP(hipSetDevice(r0.dev));
+    if (bytes) GG_HIP(hipMemcpyAsync(out + off, r0.band.ptr, bytes, hipMemcpyDeviceToDevice, r0.gs));
+    for (Rank& k : g->r) {  // (each band is free again once its transfer is done)
+        GG_HIP(hipSetDevice(k.dev));
+        GG_HIP(hipEventRecord(k.ev_gdone, k.gs));
+    }
+    GG_HIP(hipSetDevice(r0.dev));
+    GG_HIP(hipStreamWaitEvent(user, r0.ev_gdone, 0));
+    return GS_OK;
+}
+
+// One pipelined call: (project) frame k and its all-to-all; the frame in
+// flight (k-1) rendered and gathered into `out` (*produced = 1).  flush:
+// project = false.
+gs_status render_rows_pipelined(gs_group* g, const float* V, const float* P, int Wd, int Ht, float* out,
+                                hipStream_t user, bool project, bool* produced) {
+    *produced = false;
+    gs_status st = ensure_pipeline(g);
+    if (st != GS_OK) return st;
+    const int W = g->world;
+    const int s = g->pslot;
+    const int64_t xb = gs_exchange_record_bytes();
+    const gs_group::Pending prev = g->pend;
+    // (bounded host waits, SURVEY §5: frame k-2's all-to-all, whose send
+    // buffers this projection reuses; an RCCL peer error or a hang fails the
+    // call here instead of stalling a stream sync below)
+    for (Rank& k : g->r)
+        if ((st = wait_bounded(g, k.dev, k.ev_xdone[s], "pipelined all-to-all")) != GS_OK) return st;
+    // 1. per rank, on its compute stream: frame k's projection and packing
+    //    (the host reads its destination counts), then frame k-1's render
+    st = run_ranks(g, [&](Rank& k, int d) -> gs_status {
+        if (project) {
+            // (slot s's send buffers were last read by frame k-2's all-to-all)
+            for (const Rank& o : g->r) GG_HIP(hipStreamWaitEvent(k.cs, o.ev_xdone[s], 0));
+            const size_t cap = (size_t)std::max<int64_t>(gs_point_count(k.h), 1) * (size_t)W * (size_t)xb;
+            if (cap > k.psend[s].bytes) GG_HIP(hipStreamSynchronize(k.cs));
+            GG_HIP(k.psend[s].reserve(k.dev, cap));
+            k.pcounts[s].assign((size_t)W, 0);
+            gs_status r = gs_shard_project(k.h, V, P, Wd, Ht, k.psend[s].ptr, (int64_t)k.psend[s].bytes,
+                                           k.pcounts[s].data(), k.cs);
+            if (r != GS_OK) return r;
+            GG_HIP(hipEventRecord(k.ev_proj, k.cs));
+        }
+        if (prev.on) {
+            // the previous frame's records (its all-to-all) and a free band
+            // (the gather before it, possibly read by rank 0's gather stream)
+            GG_HIP(hipStreamWaitEvent(k.cs, k.ev_xdone[prev.slot], 0));
+            GG_HIP(hipStreamWaitEvent(k.cs, k.ev_gdone, 0));
+            GG_HIP(hipStreamWaitEvent(k.cs, g->r[0].ev_gdone, 0));
+            int row0, nrows;
+            owned_rows(prev.height, W, d, &row0, &nrows);
+            const size_t bb = (size_t)std::max(nrows, 1) * gs::kBin * prev.width * 16;
+            if (bb > k.band.bytes) {
+                GG_HIP(hipEventSynchronize(k.ev_gdone));
+                GG_HIP(hipEventSynchronize(g->r[0].ev_gdone));
+            }
+            GG_HIP(k.band.reserve(k.dev, bb));
+            gs_status r = gs_shard_render(k.h, k.precv[prev.slot].ptr, prev.nrec[(size_t)d], prev.width, prev.height,
+                                          k.band.as<float>(), k.cs);
+            if (r != GS_OK) return r;
+            GG_HIP(hipEventRecord(k.ev_rdone[prev.slot], k.cs));
+            GG_HIP(hipEventRecord(k.ev_done, k.cs));
+        }
+        return GS_OK;
+    });
+    if (st != GS_OK) return st;
+    // (frame k-2's gather, which frame k-1's render queued behind: bounded)
+    for (Rank& k : g->r)
+        if ((st = wait_bounded(g, k.dev, k.ev_gdone, "pipelined gather")) != GS_OK) return st;
+    // 2. frame k's all-to-all on the exchange streams, under frame k-1's render
+    g->pend.on = false;
+    if (project) {
+        if ((st = exchange_pipelined(g, s, &g->pend.nrec)) != GS_OK) return st;
+        g->pend.on = true;
+        g->pend.slot = s;
+        g->pend.width = Wd;
+        g->pend.height = Ht;
+        g->pslot = s ^ 1;
+    }
+    // 3. frame k-1's bands into the frame, on the gather streams
+    if (prev.on) {
+        if ((st = gather_pipelined(g, prev.width, prev.height, out, user)) != GS_OK) return st;
+        *produced = true;
+    }
+    return GS_OK;
+}
+
 gs_status make_group(gs_handle* scene, int32_t num_gpus, gs_group** out, bool replicated = false) {
     if (num_gpus < 1 || num_gpus > gs::kMaxWorld) return gfail(GS_ERR_INVALID_ARG, "num_gpus must be 1..32");
     gs_group* g = new gs_group();
@@ -784,10 +1035,72 @@ int64_t gs_group_point_count(const gs_group* g) { return g ? g->n : 0; }
 int32_t gs_group_size(const gs_group* g) { return g ? g->world : 0; }
 int32_t gs_group_transport(const gs_group* g) { return g && g->initialized ? g->transport : -1; }
 
+gs_status gs_group_set_frames_in_flight(gs_group* g, int32_t n) {
+    if (!g || n < 1 || n > 2) return gfail(GS_ERR_INVALID_ARG, "gs_group_set_frames_in_flight: 1 or 2");
+    if (g->pend.on) return gfail(GS_ERR_STATE, "a frame is in flight: gs_group_flush first");
+    g->frames_in_flight = n;
+    return GS_OK;
+}
+
+namespace {
+
+// gs_group_render_pipelined / gs_group_flush: one call of the pipeline.
+gs_status pipelined_call(gs_group* g, const float* view, const float* proj, int32_t width, int32_t height,
+                         float* out_rgba, int32_t out_is_device, void* hip_stream, int32_t* produced, bool project) {
+    if (!g || !g->initialized) return gfail(GS_ERR_STATE, "gs_group_initialize not called");
+    if (g->failed) return gfail(GS_ERR_COMM, "group unusable after a collective failure");
+    if (!produced || !out_rgba || (project && (!view || !proj || width <= 0 || height <= 0)))
+        return gfail(GS_ERR_INVALID_ARG, "gs_group_render_pipelined: bad arguments");
+    *produced = 0;
+    if (g->frames_in_flight < 2 || g->scheme != GS_SCHEME_ROWS || g->world < 2)
+        return gfail(GS_ERR_STATE, "pipelined frames: rows scheme, 2+ ranks, gs_group_set_frames_in_flight(2)");
+    Rank& r0 = g->r[0];
+    GG_HIP(hipSetDevice(r0.dev));
+    hipStream_t user = static_cast<hipStream_t>(hip_stream);
+    const int ow = g->pend.on ? g->pend.width : width, oh = g->pend.on ? g->pend.height : height;
+    const size_t bytes = (size_t)ow * oh * 16;
+    float* out = out_rgba;
+    if (!out_is_device) {
+        // (the staging frame may still be read by the last call's copy)
+        GG_HIP(hipStreamSynchronize(user));
+        GG_HIP(g->fb.reserve(r0.dev, bytes));
+        out = g->fb.as<float>();
+    }
+    bool made = false;
+    gs_status s = render_rows_pipelined(g, view, proj, width, height, out, user, project, &made);
+    if (s != GS_OK) return s;
+    *produced = made ? 1 : 0;
+    GG_HIP(hipSetDevice(r0.dev));
+    GG_HIP(hipEventRecord(g->frame_done, user));
+    if (made && !out_is_device) {
+        GG_HIP(hipMemcpyAsync(out_rgba, out, bytes, hipMemcpyDeviceToHost, user));
+        GG_HIP(hipEventRecord(g->frame_done, user));
+        return wait_bounded(g, r0.dev, g->frame_done, "frame");
+    }
+    return GS_OK;
+}
+
+}  // namespace
+
+gs_status gs_group_render_pipelined(gs_group* g, const float* view, const float* proj, int32_t width, int32_t height,
+                                    float* out_rgba, int32_t out_is_device, void* hip_stream, int32_t* produced) {
+    return pipelined_call(g, view, proj, width, height, out_rgba, out_is_device, hip_stream, produced, true);
+}
+
+gs_status gs_group_flush(gs_group* g, float* out_rgba, int32_t out_is_device, void* hip_stream, int32_t* produced) {
+    if (g && !g->pend.on) {  // nothing in flight
+        if (!produced) return gfail(GS_ERR_INVALID_ARG, "gs_group_flush: null produced");
+        *produced = 0;
+        return GS_OK;
+    }
+    return pipelined_call(g, nullptr, nullptr, 0, 0, out_rgba, out_is_device, hip_stream, produced, false);
+}
+
 gs_status gs_group_render(gs_group* g, const float* view, const float* proj, int32_t width, int32_t height,
                           float* out_rgba, int32_t out_is_device, void* hip_stream) {
     if (!g || !g->initialized) return gfail(GS_ERR_STATE, "gs_group_initialize not called");
     if (g->failed) return gfail(GS_ERR_COMM, "group unusable after a collective failure");
+    if (g->pend.on) return gfail(GS_ERR_STATE, "a pipelined frame is in flight: gs_group_flush first");
     if (!view || !proj || !out_rgba || width <= 0 || height <= 0)
         return gfail(GS_ERR_INVALID_ARG, "gs_group_render: bad arguments");
     Rank& r0 = g->r[0];

@@ -65,6 +65,12 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_BAND_LOCAL  // A/B knob: 1 = contiguous band frames bin without an owner table (gs_handle::band_local)
 #define GS_BAND_LOCAL 1
 #endif
+#ifndef GS_DUP_FRONT  // A/B knob: 1 = a bin-first depth-cut frame emits only its front pairs (launch_front_count)
+#define GS_DUP_FRONT 1
+#endif
+#ifndef GS_DUP_FRONT_COUNT  // A/B knob: 1 = the front-only duplicate counts the first sort pass's digits
+#define GS_DUP_FRONT_COUNT 1
+#endif
 
 struct DevBuf {
     void* ptr = nullptr;
@@ -94,6 +100,8 @@ using gsio::sh_coeffs;
 
 // (gs_internal.h) the calling thread's gs_last_error() text
 void gs_set_last_error(const std::string& msg) { g_last_error = msg; }
+
+
 
 struct gs_handle {
     gs_options opt{};
@@ -158,9 +166,13 @@ struct gs_handle {
     // pairs into ppart (PreFuse), prepared by render_frame (prepare_lists)
     struct ListPrep {
         bool ok = false;
+        bool front = false;  // the frame emits only its front pairs (launch_front_count; depth cuts)
         uint32_t cap = 0;
         gs::PassCounts pc;
     } fused_prep;
+    bool front_last = false;   // the frame in `stats` emitted only its front pairs (its fallback regenerates)
+    uint64_t pairs_emitted = 0;  // pairs the frame's duplicate wrote (= stats.pairs unless front_last)
+    DevBuf fbpart, fbtot;      // front_last frames' fallback pair scan (2 rows per block; totals)
     DevBuf ppart;
     size_t ppart_words = 0;
     bool ppart_dirty = false;  // a fused preprocess ran without its scan (error path): clear first
@@ -207,6 +219,8 @@ struct gs_handle {
     int cut_r[2] = {0, 0};
     int cut_calm[2] = {0, 0};
     int dil_r[2] = {0, 0};
+    int dil_slot[2] = {0, 0};    // per set: cutdil slot the set's next frame reads
+    int dil_wslot[2] = {1, 1};   // per set: slot the current frame's tail dilates ahead into
     uint32_t cut_bins = 0;       // bins per table in cutbuf
     int32_t cut_w = 0, cut_h = 0, cut_mode = -1;
     int cut_phase[2] = {0, 0};   // per set: which table the next frame reads
@@ -249,7 +263,8 @@ struct gs_handle {
                           &dtl, &dth, &xmask, &xcounts, &xtotal, &owner_dev, &rows_dev, &alt_rec,
                           &alt_dkey, &alt_keys, &alt_vals, &alt_tkeys, &alt_tvals, &alt_ranges, &alt_thr, &alt_rlo,
                           &alt_rhi, &alt_qrec, &alt_fkeys, &alt_fvals, &seg_sample, &npairs, &fetch, &qrec, &cutbuf,
-                          &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart, &cutord, &cutdil, &wcost})
+                          &cstate, &fkeys, &fvals, &fbtab, &fbn, &scratch2, &kept, &ppart, &cutord, &cutdil, &wcost,
+                          &fbpart, &fbtot})
             b->release();
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
@@ -444,7 +459,7 @@ gs_status ensure_frame_scratch(gs_handle* h) {
     GS_HIP(h->rhi.reserve(n * 4));
     GS_HIP(h->partials.reserve(((n + gs::kScanItems - 1) / gs::kScanItems + 1) * 24));  // (3 rows: depth-cut front lists)
     if (!h->host_total) {  // written by the scan kernel itself, read after the stream sync
-        GS_HIP(hipHostMalloc((void**)&h->host_total, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        GS_HIP(hipHostMalloc((void**)&h->host_total, 128, hipHostMallocMapped | hipHostMallocCoherent));
         GS_HIP(hipHostGetDevicePointer((void**)&h->dev_total, h->host_total, 0));
         h->host_total[6] = h->host_total[7] = ~0ull;  // (the sets' open-quadrant counts: none yet)
     }
@@ -682,6 +697,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     gs::PassCounts pc = lp.pc;
     uint32_t* const np = h->npairs.as<uint32_t>() + h->set;  // P on the device (this set's)
     const bool cut_frame = h->cut_pending && h->cut_in && carry_dkey;
+    // (front-only emission: decided with the fused preprocess, render_frame)
+    const bool front = fused && lp.front && cut_frame;
     gs::SortFilter flt;  // front lists: the pairs at or ahead of their bin's cut
     if (cut_frame) {
         GS_HIP(h->kept.reserve(16));
@@ -698,16 +715,24 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         // gathering cut[bin] per pair (index order, every bin row owned)
         flt.flag = GS_DUP_FLAG && !order && !own.dev.owner && T <= gs::kDupCutBins &&
                    bits + gs::kDepthBits <= 31 ? 1u : 0u;
+        // (front-only frames count the first pass's digits in the duplicate:
+        // its pairs are few and nearly all kept)
+        if (front) flt.flag = 1u;
+        if (front && GS_DUP_FRONT_COUNT) pc = lp.pc;
     }
+    h->front_last = front;
     // the host learns P by polling the totals kernel's sequence word in
     // host-mapped memory (GS_HOST_POLL) or by an event in its dispatch packet
     const unsigned long long seq = GS_HOST_POLL ? ++h->totals_seq : 0ull;
     hipEvent_t tev = GS_HOST_POLL ? nullptr : h->totals_ev;
     if (fused) {
-        GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), (m + gs::kScanItems - 1) / gs::kScanItems,
-                                              h->partials.as<uint64_t>(), h->dev_total,
-                                              h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
-                                              st, tev, seq));
+        const uint32_t nb = (m + gs::kScanItems - 1) / gs::kScanItems;
+        if (front)  // the front pairs' block sums into ppart's fourth row
+            GS_HIP(gs::launch_front_count(rect_lo, rect_hi, carry_dkey, m, U.cell_mask != 0, (uint32_t)U.tiles_x,
+                                          h->cut_in, T, h->ppart.as<unsigned long long>() + (size_t)3 * nb, st));
+        GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), nb, h->partials.as<uint64_t>(),
+                                              h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
+                                              st, tev, seq, front));
         h->ppart_dirty = false;
     } else {
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
@@ -725,7 +750,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
                                                  np, st, h->offsets.as<uint32_t>(), pc,
-                                                 flt.flag ? h->cut_in : nullptr, flt.flag ? T : 0u);
+                                                 flt.flag ? h->cut_in : nullptr, flt.flag ? T : 0u, front);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         // (depth-cut frames: sorted into fkeys/fvals, so keys/vals keep every
@@ -761,7 +786,10 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     } else {
         GS_HIP(hipEventSynchronize(h->totals_ev));
     }
-    const uint64_t P = h->host_total[0], P_all = P;
+    // P: the pairs the duplicate writes; P_all: every pair of the frame (the
+    // same unless front-only; the pair buffers hold P_all, so that the
+    // fallback lists always fit)
+    const uint64_t P = h->host_total[0], P_all = h->host_total[8];
     h->stats.visible = (int64_t)h->host_total[1];
     if (fused && P_all > 0) {  // the duplicate's wave-max work (PreFuse), for the binning-order model
         h->order.wmax = h->host_total[4];
@@ -780,13 +808,17 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         // into the counters cleared below, so it drains first too.
         GS_HIP(hipStreamSynchronize(st));
         if (tail && tail_st && tail_st != st) GS_HIP(hipStreamSynchronize(tail_st));
+        // (the no-op tail's cut_finalize published an open-quadrant count of
+        // a composite that never ran: discard it, the re-queued tail writes
+        // the real one for the dilation controller)
+        if (tail && h->host_total) h->host_total[6 + h->set] = ~0ull;
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
         const uint32_t p32 = (uint32_t)P;
         GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
         pc = pass_counts(h, m, order == nullptr, plan, cap, P);
         if (cut_frame) pc.cut = h->cut_in;
 #if !GS_DUP_FILTER_COUNT
-        if (cut_frame) pc = gs::PassCounts{};
+        if (cut_frame && !(front && GS_DUP_FRONT_COUNT)) pc = gs::PassCounts{};
 #endif
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         if (tail) GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));  // (the no-op frame's composite counted into these)
@@ -795,7 +827,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     }
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
-    *pairs = P;
+    h->pairs_emitted = P;
+    *pairs = P_all;
     return GS_OK;
 }
 
@@ -855,7 +888,7 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         GS_HIP(h->cutbuf.reserve((size_t)T * 4 * 4));
         GS_HIP(h->cutord.reserve((size_t)T * 4 * 4));
         GS_HIP(h->wcost.reserve((size_t)T * 2 * 4));
-        GS_HIP(h->cutdil.reserve((size_t)2 * T * 4));
+        GS_HIP(h->cutdil.reserve((size_t)4 * T * 4));  // (two slots per set, see dil_slot)
         h->dil_r[0] = h->dil_r[1] = 0;
         h->cut_bins = T;
         h->cut_valid[0] = h->cut_valid[1] = false;
@@ -887,7 +920,13 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
         }
         static const char* fixed_r = std::getenv("GS_CUT_DILATE");  // (A/B: a fixed radius)
         if (fixed_r) h->cut_r[S] = std::max(0, std::atoi(fixed_r));
-        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)S * T;
+        // two dilated tables per set: the one this frame reads (dil_slot[S],
+        // made ahead by the tail of the frame that wrote its cuts, or here)
+        // and the one this frame's tail dilates ahead into, which therefore
+        // never is this frame's input, even when the tail is queued twice
+        // (build_bin_lists' pair-buffer regrowth)
+        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)(2 * S + h->dil_slot[S]) * T;
+        h->dil_wslot[S] = h->dil_slot[S] ^ 1;
         if (h->cut_in && h->cut_r[S] > 0 && GS_CUT_DILATE_AHEAD && h->dil_r[S] >= h->cut_r[S]) {
             // dilated ahead by the tail of the frame that wrote these cuts
             // (a wider radius than the controller's now only moves pairs from
@@ -920,8 +959,12 @@ gs_status setup_cuts(gs_handle* h, const gs::FrameUniforms& U, bool cut_frame, h
 // quadrant open, cut_finalize leaves a pair count of 0 and every kernel here
 // returns at once (the usual case).  The front lists' buffers are free by
 // then (same stream).
+// Front-only frames (h->front_last) wrote no pair behind a cut: their
+// fallback lists' pairs are emitted here from the splats' rects (m items,
+// rect_lo / rect_hi / dkey), the bins with an open quadrant only.
 gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs ca, const uint32_t* dkey,
-                   const gs::RowOwnership& own, hipStream_t sc) {
+                   const gs::RowOwnership& own, hipStream_t sc, uint32_t m, const uint32_t* rect_lo,
+                   const uint32_t* rect_hi) {
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);
     gs::CutFallback fb;
     if (h->cut_in) {
@@ -943,16 +986,18 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     if (ca.wcost && h->ord_out) GS_HIP(gs::launch_order_bins(ca.wcost, T, h->ord_out, sc));
     // the set's next cuts, dilated here at the set's current radius while a
     // moving camera keeps them dilated (setup_cuts then reads them without a
-    // kernel ahead of the projection).  cutdil[set] may be this frame's own
-    // input: its readers (the duplicate's marks, the pass-1 composite,
-    // cut_finalize) are all ordered before this point.  On the composite
-    // stream, which has slack while the side stream's projection and chain
-    // bound the frame (1080p); a stream of its own measured no better
-    // (profiles/r05/ab_dilate_radius.txt).
-    if (GS_CUT_DILATE_AHEAD && h->cut_out && h->cut_r[h->set] > 0 && h->cutdil.bytes >= (size_t)2 * T * 4) {
-        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)h->set * T;
-        GS_HIP(gs::launch_cut_dilate(h->cut_out, d, (uint32_t)U.tiles_x, (uint32_t)U.tiles_y, h->cut_r[h->set], sc));
-        h->dil_r[h->set] = h->cut_r[h->set];
+    // kernel ahead of the projection), into the set's other dilated table
+    // (dil_wslot: never this frame's input, so a tail queued twice, as after a
+    // pair-buffer regrowth, cannot change what the frame's lists read).  On
+    // the composite stream, which has slack while the side stream's
+    // projection and chain bound the frame (1080p); a stream of its own
+    // measured no better (profiles/r05/ab_dilate_radius.txt).
+    if (GS_CUT_DILATE_AHEAD && h->cut_out && h->cut_r[h->set] > 0 && h->cutdil.bytes >= (size_t)4 * T * 4) {
+        const int S = h->set;
+        uint32_t* d = h->cutdil.as<uint32_t>() + (size_t)(2 * S + h->dil_wslot[S]) * T;
+        GS_HIP(gs::launch_cut_dilate(h->cut_out, d, (uint32_t)U.tiles_x, (uint32_t)U.tiles_y, h->cut_r[S], sc));
+        h->dil_r[S] = h->cut_r[S];
+        h->dil_slot[S] = h->dil_wslot[S];  // (the set's next frame reads it; idempotent when queued twice)
     }
     if (!h->cut_in) return GS_OK;  // (whole lists: no quadrant can be left open)
 #ifdef GS_AB_NO_FALLBACK  // timing ablation build only: exact only while no quadrant is left open
@@ -973,6 +1018,22 @@ gs_status cut_tail(gs_handle* h, const gs::FrameUniforms& U, gs::CompositeArgs c
     // (the table tested in LDS: every pair of the frame is tested against a
     // few open bins; GS_FB_LDS=0: the global gather, A/B)
     if (GS_FB_LDS && T <= gs::kDupCutBins) flt.lds_bins = T;
+    if (h->front_last) {
+        // the fallback pairs regenerated into keys/vals (free: the front lists
+        // were sorted out of them on the side stream before this composite
+        // ran), counted and scanned on the device; the sort keeps them all
+        // (no pair carries the behind mark) on the same looping grid
+        const uint32_t nb = (m + gs::kScanItems - 1) / gs::kScanItems;
+        GS_HIP(reserve_after(h->fbpart, (size_t)std::max<uint32_t>(nb, 1) * 16, sc));
+        GS_HIP(reserve_after(h->fbtot, 16 * 8, sc));
+        GS_HIP(gs::launch_fallback_pairs(rect_lo, rect_hi, dkey, m, U.cell_mask != 0, (uint32_t)U.tiles_x, bits, fb.table,
+                                         T, fb.open, h->fbpart.as<uint64_t>(), h->fbtot.as<uint64_t>(), fb.n, fb.kept,
+                                         cap, h->keys.as<uint32_t>(), h->vals.as<uint32_t>(), sc));
+        flt.behind = 0;
+        flt.flag = 1u;
+        flt.kmask = ~0u;
+        flt.lds_bins = 0;
+    }
     // (usually no quadrant is open and the sort's input is empty: a fixed
     // grid that loops over the tiles then costs a few workgroups, not one
     // per tile of the frame's pairs)
@@ -1122,7 +1183,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             }
             // the next cuts of this set, then the fallback lists
             if (cutf) {
-                gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc);
+                gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc, m, rect_lo, rect_hi);
                 if (fs_ != GS_OK) return fs_;
             }
             mark(h, 7, sc);
@@ -1185,7 +1246,7 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             mark(h, 6, st);
             GS_HIP(handoff());
             GS_HIP(gs::launch_composite(c, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));
-            gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc);
+            gs_status fs_ = cut_tail(h, U, c, dkey, own.dev, sc, m, slo, shi);
             if (fs_ != GS_OK) return fs_;
             mark(h, 7, sc);
             return GS_OK;
@@ -1241,7 +1302,11 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.bytes_scan = N * 8 + T * 8;  // (+ the empty bin ranges, filled on the way)
     if (h->fused_last)  // the block sums came from the preprocess: the scan reads them
         s.bytes_scan = (N + gs::kScanItems - 1) / gs::kScanItems * 16 + T * 8;
-    s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pi * 8;
+    // (front-only frames write only their front pairs, counted first by
+    // launch_front_count: another read of the rects and depth keys)
+    const int64_t Pe = h->front_last ? (int64_t)h->pairs_emitted : Pi;
+    if (h->front_last) s.bytes_scan += N * 12;
+    s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pe * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
         // per-bin depth sort: keys read, vals gathered and written back (12 B
@@ -1596,18 +1661,28 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         if (bf) {
             if ((s = prepare_lists(h, (uint32_t)h->n, true, U, &h->fused_prep)) != GS_OK) return s;
             const uint32_t nb = (uint32_t)((h->n + gs::kScanItems - 1) / gs::kScanItems);
-            GS_HIP(h->ppart.reserve((size_t)nb * 24));
-            if (h->ppart_words != (size_t)nb * 3 || h->ppart_dirty) {
-                GS_HIP(hipMemsetAsync(h->ppart.ptr, 0, (size_t)nb * 24, sp));  // (then kept clear by the scan)
-                h->ppart_words = (size_t)nb * 3;
+            // (four rows: the three atomic sums of PreFuse, and the front
+            // pairs' block sums a front-only frame stores, launch_front_count)
+            GS_HIP(h->ppart.reserve((size_t)nb * 32));
+            if (h->ppart_words != (size_t)nb * 4 || h->ppart_dirty) {
+                GS_HIP(hipMemsetAsync(h->ppart.ptr, 0, (size_t)nb * 32, sp));  // (then kept clear by the scan)
+                h->ppart_words = (size_t)nb * 4;
             }
             fuse.part = h->ppart.as<unsigned long long>();
             fuse.nb = nb;
             fuse.fill = h->ranges.as<uint2>();
             fuse.nfill = T;
+            // Front-only emission (a frame with cuts, the duplicate's table in
+            // LDS, the behind mark above the depth key): the duplicate writes
+            // the front lists' pairs alone, so neither it nor the sort's first
+            // pass moves the pairs behind the cuts (most of a frame's: 86 % at
+            // 50M @4K); the fallback lists regenerate theirs when a quadrant
+            // is left open (cut_tail).
+            h->fused_prep.front = GS_DUP_FRONT && h->cut_in && T <= gs::kDupCutBins &&
+                                  list_key_bits(U) + gs::kDepthBits <= 31;
             h->fused_prep.pc.cut = h->cut_in;  // (with cuts: the duplicate counts only the pairs the filter keeps)
 #if !GS_DUP_FILTER_COUNT
-            if (h->cut_in) h->fused_prep.pc = gs::PassCounts{};
+            if (h->cut_in && !(h->fused_prep.front && GS_DUP_FRONT_COUNT)) h->fused_prep.pc = gs::PassCounts{};
 #endif
             fuse.zero = h->fused_prep.pc.C;
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
@@ -1675,7 +1750,9 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
             if (h->cut_lists) {
                 uint32_t k1 = 0;
                 GS_HIP(hipMemcpy(&k1, h->kept.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
-                const int64_t P = s.pairs, P1 = (int64_t)k1;
+                // (the first pass reads the emitted pairs: every pair, or the
+                // front pairs of a front-only frame)
+                const int64_t P = h->front_last ? (int64_t)h->pairs_emitted : s.pairs, P1 = (int64_t)k1;
                 s.pairs_sorted = P1;
                 s.bytes_sort = P * 12 + P1 * 8 + P1 * 20 * (int64_t)(s.sort_passes - 1);
                 if (h->bin_first_frame) s.bytes_depth_sort = P1 * 12;  // (depth-first: the global depth sort, unchanged)
@@ -1687,7 +1764,12 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
             if (open) GS_HIP(hipMemcpy(&P2, h->kept.as<uint32_t>() + 2 + h->stats_set, 4, hipMemcpyDeviceToHost));
             s.open_tiles = (int64_t)open;
             s.pairs_sorted += (int64_t)P2;
-            if (open) {  // the fallback sort's first pass reads every pair again
+            if (open && h->front_last) {  // the fallback pairs regenerated from the rects, then sorted
+                s.bytes_duplicate += s.splats * 24 + (int64_t)P2 * 8;
+                s.bytes_sort += (int64_t)P2 * 20 * (int64_t)s.sort_passes;
+                s.bytes_depth_sort += (int64_t)P2 * 12;
+                s.bytes_composite += (int64_t)open * 64 * 32;
+            } else if (open) {  // the fallback sort's first pass reads every pair again
                 s.bytes_sort += s.pairs * 12 + (int64_t)P2 * 8 + (int64_t)P2 * 20 * (int64_t)(s.sort_passes - 1);
                 s.bytes_depth_sort += (int64_t)P2 * 12;
                 s.bytes_composite += (int64_t)open * 64 * 32;  // (8x8 quadrants)
@@ -1855,6 +1937,7 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     std::memset(&h->stats, 0, sizeof h->stats);
     h->shard_frame = true;
     h->slab_lists = false;
+    h->band_local = false;  // (a shard frame bins with its owner table; an earlier band frame may have set it)
     begin_frame(h, st);
     gs::ShardFuse sf;
     if (owner) {
@@ -1923,6 +2006,9 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !(out_rgba || slab_t) || W <= 0 || H <= 0)
         return fail(GS_ERR_INVALID_ARG, "shard render: bad arguments");
     if ((s = ensure_frame_scratch(h)) != GS_OK) return s;
+    // received records bin with the owner table (band_local is a gs_band_render
+    // frame's, whose rects were clipped to the band: not these)
+    h->band_local = false;
     const float I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     const gs::FrameUniforms U = make_uniforms(I, I, W, H);
     const uint32_t T = (uint32_t)(U.tiles_x * U.tiles_y);

@@ -968,6 +968,7 @@ __global__ __launch_bounds__(1024) void order_bins_kernel(const uint32_t* __rest
     constexpr int kB = 128;
     __shared__ uint32_t cnt[kB];
     __shared__ uint8_t bk[kOrderMaxBins];  // each bin's bucket, between the two phases
+    static_assert(kOrderMaxBins + kB * 4 <= kLdsBytes, "order_bins_kernel's LDS exceeds a gfx950 workgroup's");
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     if (tid < kB) cnt[tid] = 0u;
     __syncthreads();

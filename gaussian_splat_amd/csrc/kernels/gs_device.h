@@ -9,8 +9,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// The kernels size their LDS for gfx950 (160 KB per CU, up to 160 KB per
+// workgroup: order_bins_kernel and the duplicate's cut table use more than
+// the 64 KB of earlier CDNA parts), so the device code builds for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libgsplat's kernels are written for gfx950 (MI355X): build with --offload-arch=gfx950"
+#endif
+
 namespace gs {
 
+constexpr int kLdsBytes = 160 * 1024;     // LDS per CU (and per workgroup) on gfx950
 constexpr int kTile = 16;                 // 16x16-pixel tiles (gaussian_splat_types.h:9 budget)
 constexpr int kTileThreads = kTile * kTile;
 // Binning granularity: 32x32-pixel bins of 2x2 tiles.  Splats are binned per

@@ -79,9 +79,33 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // part (2 x nb words: pairs, visible splats) are scanned into partials (as
 // launch_tile_count_totals leaves them) and part is cleared for the next
 // frame.
+// front (a depth-cut frame's front-only emission, launch_front_count): the
+// offsets are scanned from the front pairs' block sums (part row 3, nb words
+// after the three atomic rows), total[0] = the front pairs; total[8] = every
+// pair of the frame (row 0) either way, and npairs is 0 when the pair buffers
+// cannot hold them all (the fallback lists may need them).
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done = nullptr, unsigned long long seq = 0);
+                                      hipEvent_t done = nullptr, unsigned long long seq = 0, bool front = false);
+// Front-only emission of a depth-cut frame (index order, every
+// bin row owned): per 4096-splat block, the pairs the front duplicate emits
+// (launch_scan_duplicate front): a splat whose rect lies within 4x4 bins
+// emits the bins with dkey <= cut[bin]; a larger one every bin (marked behind
+// its cut, kBehindFlag, as kDupMark frames mark every pair).  out[b] = the
+// block's sum (plain stores; nbins <= kDupCutBins, the table staged in LDS).
+hipError_t launch_front_count(const uint32_t* rect_lo, const uint32_t* rect_hi, const uint32_t* dkey, uint32_t n,
+                              bool masked, uint32_t tiles_x, const uint32_t* cut, uint32_t nbins,
+                              unsigned long long* out, hipStream_t st);
+// The fallback lists' pairs of a front-only frame (which never wrote the
+// pairs behind the cuts): with *open != 0, every (splat, bin) pair with
+// dkey > table[bin] (the open bins' cuts, ~0 elsewhere), in index order,
+// key = dkey << bin_bits | bin, into keys/vals; *npairs = *kept = their
+// number (<= cap).  part (2 * nblocks words) and total (>= 9 words): scratch.
+// Nothing runs while *open == 0 (npairs keeps cut_finalize's 0).
+hipError_t launch_fallback_pairs(const uint32_t* rect_lo, const uint32_t* rect_hi, const uint32_t* dkey, uint32_t n,
+                                 bool masked, uint32_t tiles_x, int bin_bits, const uint32_t* table, uint32_t nbins,
+                                 const unsigned long long* open, uint64_t* part, uint64_t* total, uint32_t* npairs,
+                                 uint32_t* kept, uint64_t cap, uint32_t* keys, uint32_t* vals, hipStream_t st);
 // (seq > 0: after total[0..4] the totals kernel stores seq into total[5] with
 // a system-scope release, for a host that polls host-mapped `total` instead
 // of waiting for `done`.)
@@ -114,12 +138,14 @@ constexpr uint32_t kDupCountTiles = 8;  // sort tiles a duplicate block counts i
 // instead of gathering cut[bin] per pair.
 constexpr uint32_t kDupCutBins = 16384;
 constexpr uint32_t kBehindFlag = 0x80000000u;
+// front (with fcut): only the pairs launch_front_count counted, at offsets
+// scanned from its sums (launch_scan_partials_fused front).
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
                                  uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
-                                 const uint32_t* fcut = nullptr, uint32_t nbins = 0);
+                                 const uint32_t* fcut = nullptr, uint32_t nbins = 0, bool front = false);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)

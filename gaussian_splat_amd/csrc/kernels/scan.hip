@@ -104,12 +104,21 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 // src (may be null): the block sums come from there instead (the fused
 // preprocess's, PreFuse: 3 x nb words) and are cleared after reading; the
 // third row's sum (the duplicate's wave-max work) goes to total[4].
+// prow (src only): the row whose sums are scanned into the offsets, 0 (every
+// pair) or 3 (the front pairs a depth-cut frame emits, launch_front_count);
+// row 0's sum is total[8] either way (the frame's every pair: the pair buffers
+// must hold them all, so npairs is 0 when they do not).  guard (may be null):
+// nothing is done while *guard == 0 (the fallback lists' regeneration).
+// kept (may be null): also receives the pair count.
 __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
                                                                      uint64_t* __restrict__ total,
                                                                      uint32_t* __restrict__ seg_sample,
                                                                      uint32_t* __restrict__ npairs, uint64_t cap,
                                                                      unsigned long long* __restrict__ src,
-                                                                     unsigned long long seq) {
+                                                                     unsigned long long seq, uint32_t prow,
+                                                                     const unsigned long long* __restrict__ guard,
+                                                                     uint32_t* __restrict__ kept) {
+    if (guard && *guard == 0ull) return;
     if (seg_sample && threadIdx.x == 0) {
         total[2] = seg_sample[0];
         total[3] = seg_sample[1];
@@ -118,16 +127,18 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
     }
     __shared__ uint64_t tmp[kPartThreads / 64];
     constexpr uint32_t CH = kPartThreads * kPartIpt;
-    uint64_t carry = 0, vis = 0, wmax = 0;
+    uint64_t carry = 0, vis = 0, wmax = 0, all = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += CH) {
         const uint32_t i0 = b0 + threadIdx.x * kPartIpt;
         uint64_t v[kPartIpt], s = 0;
 #pragma unroll
         for (int k = 0; k < kPartIpt; ++k) {
             if (src) {
-                v[k] = i0 + k < nb ? (uint64_t)src[i0 + k] : 0u;
+                v[k] = i0 + k < nb ? (uint64_t)src[(size_t)prow * nb + i0 + k] : 0u;
+                all += i0 + k < nb ? (uint64_t)src[i0 + k] : 0u;
                 vis += i0 + k < nb ? (uint64_t)src[nb + i0 + k] : 0u;
                 wmax += i0 + k < nb ? (uint64_t)src[2u * nb + i0 + k] : 0u;
+                // (rows 0-2 are atomic sums: cleared for the next frame; row 3 is stored whole by every front frame)
                 if (i0 + k < nb) src[i0 + k] = src[nb + i0 + k] = src[2u * nb + i0 + k] = 0ull;  // (read by this lane only)
             } else {
                 v[k] = i0 + k < nb ? partials[i0 + k] : 0u;
@@ -144,14 +155,17 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         }
         carry += t;
     }
-    uint64_t vt, wt = 0;
+    uint64_t vt, wt = 0, at = carry;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
     if (src) block1024_exclusive_scan<uint64_t>(wmax, tmp, &wt);
+    if (src && prow) block1024_exclusive_scan<uint64_t>(all, tmp, &at);
     if (threadIdx.x == 0) {
         total[0] = carry;
         total[1] = vt;
         total[4] = wt;
-        if (npairs) *npairs = carry <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
+        total[8] = at;
+        if (npairs) *npairs = at <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
+        if (kept) *kept = (uint32_t)carry;
         // (seq: the host polls total[5]; the totals are visible before it)
         if (seq) __hip_atomic_store(reinterpret_cast<unsigned long long*>(total) + 5, seq, __ATOMIC_RELEASE,
                                     __HIP_MEMORY_SCOPE_SYSTEM);
@@ -180,6 +194,123 @@ __device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
     return b + (i >= (m & 1u) ? 1u : 0u);
 }
 
+// ---- filtered emission (depth-cut frames) ---------------------
+// A 16-bit table in LDS (a cut table, min(cut, 0xFFFF); depth keys are < 2^15)
+// decides per (splat, bin) whether a pair is emitted: front (FM 2), dk <=
+// tab[bin], the pairs a depth-cut frame's front lists hold; behind (FM 3), dk
+// > tab[bin], the fallback lists' pairs of the bins whose table entry is the
+// cut of a bin with an open quadrant (0xFFFF elsewhere: none).
+enum : int { kDupPlain = 0, kDupMark = 1, kDupFront = 2, kDupBehind = 3 };
+
+// A rect within 4x4 bins (the only ones with excluded bins).
+__device__ __forceinline__ bool small_rect(const BinRect& r) { return r.bx1 - r.bx0 < 4u && r.by1 - r.by0 < 4u; }
+
+// Its bins as a 16-bit mask (bit dy * 4 + dx), minus the excluded ones.
+__device__ __forceinline__ uint32_t rect_inc16(const BinRect& r) {
+    const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u, rm = (1u << cols) - 1u;
+    uint32_t inc = 0u;
+#pragma unroll
+    for (uint32_t dy = 0; dy < 4u; ++dy)
+        if (dy < rows) inc |= rm << (4u * dy);
+    return inc & ~r.excl;
+}
+
+template <bool BEHIND>
+__device__ __forceinline__ bool tab_keep(const uint16_t* tab, uint32_t bin, uint32_t dk) {
+    const uint32_t t = tab[bin];
+    return BEHIND ? dk > t : dk <= t;
+}
+
+// The bins of inc16 (a small rect's) that the table keeps.
+template <bool BEHIND>
+__device__ __forceinline__ uint32_t filter_inc16(uint32_t inc, const BinRect& r, uint32_t tiles_x, const uint16_t* tab,
+                                                 uint32_t dk) {
+    uint32_t out = 0u, m = inc;
+    while (m) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        if (tab_keep<BEHIND>(tab, (r.by0 + (b >> 2)) * tiles_x + r.bx0 + (b & 3u), dk)) out |= 1u << b;
+    }
+    return out;
+}
+
+// Pairs an item emits under filter mode FM (every bin row owned).  Front: a
+// small rect its kept bins; a larger one every bin (they are emitted whole
+// and marked, kBehindFlag, so the sort's first pass still drops their behind
+// pairs; such splats are few).  Behind: every kept bin (a loop: the fallback
+// runs only when quadrants are open).
+template <int FM>
+__device__ __forceinline__ uint32_t filtered_count(uint32_t lo, uint32_t hi, bool masked, uint32_t dk, uint32_t tiles_x,
+                                                   const uint16_t* tab) {
+    const BinRect r = bin_rect(lo, hi, masked);
+    if (r.empty) return 0u;
+    if constexpr (FM == kDupFront) {
+        if (small_rect(r)) return (uint32_t)__builtin_popcount(filter_inc16<false>(rect_inc16(r), r, tiles_x, tab, dk));
+        return rect_tile_count(lo, hi, RowOwnership{nullptr, 0u}, masked);
+    } else {
+        uint32_t c = 0u;
+        for (uint32_t by = r.by0; by <= r.by1; ++by)
+            for (uint32_t bx = r.bx0; bx <= r.bx1; ++bx)
+                c += !bin_excluded(r, by, bx) && tab_keep<true>(tab, by * tiles_x + bx, dk) ? 1u : 0u;
+        return c;
+    }
+}
+
+// Stages the table (nbins words, min(t, 0xFFFF)) in LDS.
+__device__ __forceinline__ void stage_tab16(const uint32_t* __restrict__ t, uint32_t nbins, uint16_t* tab) {
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) tab[i] = (uint16_t)min(t[i], 0xFFFFu);
+}
+
+// Per 4096-item block (the scan's and the duplicate's blocking): the pairs the
+// block's items emit under FM into out[b] and, when vis is set, the items
+// that emit any into vis[b] (plain stores: one workgroup per block).  guard
+// (may be null): nothing while *guard == 0.
+template <int FM>
+__global__ __launch_bounds__(1024) void filtered_count_kernel(const uint32_t* __restrict__ rect_lo,
+                                                              const uint32_t* __restrict__ rect_hi,
+                                                              const uint32_t* __restrict__ dkey, uint32_t n, bool masked,
+                                                              uint32_t tiles_x, const uint32_t* __restrict__ table,
+                                                              uint32_t nbins, unsigned long long* __restrict__ out,
+                                                              unsigned long long* __restrict__ vis,
+                                                              const unsigned long long* __restrict__ guard) {
+    if (guard && *guard == 0ull) return;
+    extern __shared__ uint16_t tab[];
+    __shared__ uint2 wsum[16];
+    constexpr int IPT = kScanItems / 1024;
+    const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    uint32_t lo[IPT], hi[IPT], dk[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {  // (every load first, clamped)
+        const uint32_t j = min(blk + k * 1024 + tid, n - 1u);
+        lo[k] = rect_lo[j];
+        hi[k] = rect_hi[j];
+        dk[k] = dkey[j];
+    }
+    stage_tab16(table, nbins, tab);
+    __syncthreads();
+    uint32_t c = 0u, v = 0u;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const uint32_t x = blk + k * 1024 + tid < n ? filtered_count<FM>(lo[k], hi[k], masked, dk[k], tiles_x, tab) : 0u;
+        c += x;
+        v += x > 0u;
+    }
+    c = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c), 63);
+    v = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
+    if ((tid & 63u) == 0) wsum[tid >> 6] = make_uint2(c, v);
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t sc = 0, sv = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            sc += wsum[w].x;
+            sv += wsum[w].y;
+        }
+        out[blockIdx.x] = sc;
+        if (vis) vis[blockIdx.x] = sv;
+    }
+}
+
 // Wave-cooperative emission of 64 consecutive items' pairs (every bin row
 // owned): the items own the contiguous pair range [off0, off0 + T); lane q of
 // a 64-pair chunk writes pair off0 + q0 + q (coalesced).  Its item: the last
@@ -194,21 +325,16 @@ __device__ __forceinline__ uint32_t nth_bit16(uint32_t m, uint32_t i) {
 #ifndef GS_DUP_TAG  // A/B knob
 #define GS_DUP_TAG 0
 #endif
+// inc: the item's emitted bins of a rect within 4x4 bins (bit dy*4 + dx; the
+// included ones with excluded bins, or the kept ones of a filtered emission),
+// or 0: every bin of the rect in row-major order (minus none).
 template <typename F>
-__device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t c, uint32_t start,
-                                          uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
+__device__ __forceinline__ void coop_emit(uint32_t* mk, uint32_t lane, const BinRect& r, uint32_t inc, uint32_t c,
+                                          uint32_t start, uint32_t off0, uint32_t val, uint32_t khi, uint32_t tiles_x,
                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t& gen,
                                           F&& on_pair) {
     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<true>(c > 0u ? start + c : 0u), 63);
-    const uint32_t cols = r.bx1 - r.bx0 + 1u, rows = r.by1 - r.by0 + 1u;
-    uint32_t inc = 0;  // with excluded bins (rect <= 4x4 bins): the included ones, bit dy*4 + dx
-    if (r.excl) {
-        const uint32_t rm = (1u << cols) - 1u;
-#pragma unroll
-        for (uint32_t dy = 0; dy < 4u; ++dy)
-            if (dy < rows) inc |= rm << (4u * dy);
-        inc &= ~r.excl;
-    }
+    const uint32_t cols = r.bx1 - r.bx0 + 1u;
     const uint32_t pa = r.bx0 | (r.by0 << 16), pb = (cols & 0xFFFFu) | (inc << 16);
     uint32_t carry = 0;
     for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
@@ -290,6 +416,12 @@ __device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_
     return base + inc - v;
 }
 
+// FM (filter mode): kDupPlain every pair; kDupMark every pair, those behind
+// their bin's cut (ftab, the cut table) marked with kBehindFlag; kDupFront the
+// front pairs (filtered_count; the block's offsets are then scanned from
+// launch_front_count's sums); kDupBehind the fallback lists' pairs (ftab: the
+// open bins' cuts, one splat per lane).
+template <int FM>
 __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
                                                                      const uint64_t* __restrict__ partials,
                                                                      const uint32_t* __restrict__ order,
@@ -304,7 +436,9 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     __shared__ uint32_t mk[kDupThreads / 64][64];        // coop_emit's start marks, per wave
-    extern __shared__ uint16_t scut[];                   // (fcut, dynamic: nbins words) the cut table, min(cut, 0xFFFF)
+    extern __shared__ uint16_t scut[];                   // (fcut, dynamic: nbins words) the table, min(t, 0xFFFF)
+    static_assert(sizeof tmp + sizeof st + sizeof lh + sizeof mk + kDupCutBins * 2 <= kLdsBytes,
+                  "scan_duplicate_kernel's LDS (static + the largest cut table) exceeds a gfx950 workgroup's");
     const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
@@ -323,10 +457,10 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         dk[k] = dsrc[j];
         ord[k] = osrc[j];
     }
-    if (fcut)  // (a depth key is < 2^15: min(cut, 0xFFFF) keeps every comparison)
-        for (uint32_t i = tid; i < nbins; i += kDupThreads) scut[i] = (uint16_t)min(fcut[i], 0xFFFFu);
+    if (FM != kDupPlain) stage_tab16(fcut, nbins, scut);  // (a depth key is < 2^15: min(t, 0xFFFF) keeps every comparison)
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
+    if (FM >= kDupFront) block_lds_sync();  // (the counts below read the table)
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid;
@@ -334,7 +468,8 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        st[pad32(i)] = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        st[pad32(i)] = FM >= kDupFront ? filtered_count<FM>(rlo[k], rhi[k], src.masked, dk[k], tiles_x, scut)
+                                       : rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
     }
     block_lds_sync();
     uint32_t v[kDupIpt];
@@ -359,12 +494,12 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     // without its key re-read): the block's pairs are contiguous from its
     // partial, so its first kDupCountTiles tiles count in LDS
     const uint32_t t_lo = pc.C ? (uint32_t)(part / pc.tile) : 0u;
-    // (fcut) the behind-the-cut mark, from the LDS table
+    // (kDupMark, kDupFront) the behind-the-cut mark, from the LDS table
     auto mark = [&](uint32_t bin, uint32_t key) -> uint32_t {
         return (key >> bin_bits) > (uint32_t)scut[bin] ? key | kBehindFlag : key;
     };
     auto count = [&](uint32_t g, uint32_t bin, uint32_t key) -> uint32_t {  // (pc.C) the pair's digit into its tile's counts
-        if (fcut) {
+        if (FM == kDupMark || FM == kDupFront) {
             key = mark(bin, key);
             if (key & kBehindFlag) return key;  // (the filter drops it)
         } else if (pc.cut && (key >> bin_bits) > pc.cut[bin]) {
@@ -375,7 +510,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         else atomicAdd(&pc.C[(size_t)d * pc.ntiles + t], 1u);
         return key;
     };
-    if (GS_DUP_COOP && !src.own.owner) {
+    if (FM != kDupBehind && GS_DUP_COOP && !src.own.owner) {
         // wave-cooperative emission (every bin row owned): each wave's 64
         // consecutive items of a round own one contiguous pair run, written
         // 64 pairs per step by all lanes, so a large splat does not hold its
@@ -388,16 +523,23 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         for (int k = 0; k < kDupIpt; ++k) {
             const uint32_t i = k * kDupThreads + tid, j = blk + i;
             const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);  // (items past n: the empty rect)
-            const uint32_t c = j < n && !r.empty ? rect_tile_count(rlo[k], rhi[k], src.own, src.masked) : 0u;
+            uint32_t inc, c;
+            if (FM == kDupFront && small_rect(r)) {  // (its kept bins; a larger rect emits every bin, marked)
+                inc = j < n && !r.empty ? filter_inc16<false>(rect_inc16(r), r, tiles_x, scut, dk[k]) : 0u;
+                c = (uint32_t)__builtin_popcount(inc);
+            } else {
+                inc = r.excl ? rect_inc16(r) : 0u;
+                c = j < n && !r.empty ? rect_tile_count(rlo[k], rhi[k], src.own, src.masked) : 0u;
+            }
             const uint32_t off = st[pad32(i)];
             const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
             const uint32_t khi = dkey ? dk[k] << bin_bits : 0u;
             const uint32_t val = order ? ord[k] : j;
-            if (pc.C) coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen, count);
-            else if (fcut)
-                coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
+            if (pc.C) coop_emit(mk[wave], lane, r, inc, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen, count);
+            else if (FM == kDupMark || FM == kDupFront)
+                coop_emit(mk[wave], lane, r, inc, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
                           [&](uint32_t, uint32_t bin, uint32_t key) { return mark(bin, key); });
-            else coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
+            else coop_emit(mk[wave], lane, r, inc, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
                            [](uint32_t, uint32_t, uint32_t key) { return key; });
         }
     } else
@@ -409,6 +551,12 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         const uint32_t off = st[pad32(i)];
         const uint32_t key_hi = dkey ? dk[k] << bin_bits : 0u;  // depth key above the bin id
         const uint32_t val = order ? ord[k] : j;
+        if constexpr (FM == kDupBehind) {  // (the fallback lists: the kept bins, filtered_count's)
+            const uint32_t d = dk[k];
+            emit_bin_pairs_if(r, tiles_x, src.own, key_hi, val, off, keys, vals,
+                              [&](uint32_t bin) { return tab_keep<true>(scut, bin, d); }, [](uint32_t, uint32_t) {});
+            continue;
+        }
         auto keep = [](uint32_t) { return true; };
         if (pc.C) {
             uint32_t t = off / pc.tile, next = (t + 1u) * pc.tile;  // pair offsets rise by one
@@ -529,7 +677,7 @@ __global__ __launch_bounds__(256) void duplicate_coop_kernel(CountSrc src, uint3
     const uint32_t off0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);  // lane 0 is valid
     uint32_t gen = 0;
     mk[wave][lane] = ~0u;  // (no chunk's tag)
-    coop_emit(mk[wave], lane, r, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
+    coop_emit(mk[wave], lane, r, r.excl ? rect_inc16(r) : 0u, c, off - off0, off0, val, khi, tiles_x, keys, vals, gen,
               [](uint32_t, uint32_t, uint32_t key) { return key; });
 }
 
@@ -553,16 +701,51 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
         scan_reduce_kernel<<<nb, 256, 0, st>>>(src, n, partials, ranges, nranges, zero, nzero);
     }
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, nullptr, seq);
+                          total, seg_sample, npairs, cap, nullptr, seq, 0u, nullptr, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done, unsigned long long seq) {
+                                      hipEvent_t done, unsigned long long seq, bool front) {
     if (!part) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, part, seq);
+                          total, seg_sample, npairs, cap, part, seq, front ? 3u : 0u, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+// (dynamic LDS of a staged table of nbins 16-bit words)
+static size_t tab_lds(uint32_t nbins) { return ((size_t)nbins * 2 + 15) & ~(size_t)15; }
+
+hipError_t launch_front_count(const uint32_t* rect_lo, const uint32_t* rect_hi, const uint32_t* dkey, uint32_t n,
+                              bool masked, uint32_t tiles_x, const uint32_t* cut, uint32_t nbins,
+                              unsigned long long* out, hipStream_t st) {
+    const uint32_t nb = (n + kScanItems - 1) / kScanItems;
+    if (nb == 0) return hipSuccess;
+    if (!cut || !out || nbins > kDupCutBins) return hipErrorInvalidValue;
+    filtered_count_kernel<kDupFront><<<nb, 1024, tab_lds(nbins), st>>>(rect_lo, rect_hi, dkey, n, masked, tiles_x, cut,
+                                                                       nbins, out, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_fallback_pairs(const uint32_t* rect_lo, const uint32_t* rect_hi, const uint32_t* dkey, uint32_t n,
+                                 bool masked, uint32_t tiles_x, int bin_bits, const uint32_t* table, uint32_t nbins,
+                                 const unsigned long long* open, uint64_t* part, uint64_t* total, uint32_t* npairs,
+                                 uint32_t* kept, uint64_t cap, uint32_t* keys, uint32_t* vals, hipStream_t st) {
+    const uint32_t nb = (n + kScanItems - 1) / kScanItems;
+    if (nb == 0) return hipSuccess;
+    if (!table || !open || !part || !total || !npairs || nbins > kDupCutBins || bin_bits + kDepthBits > 31)
+        return hipErrorInvalidValue;
+    // per-block pair counts and items with pairs (the scan's two rows), their
+    // scan into npairs / kept (only with an open quadrant), then the pairs
+    filtered_count_kernel<kDupBehind><<<nb, 1024, tab_lds(nbins), st>>>(
+        rect_lo, rect_hi, dkey, n, masked, tiles_x, table, nbins, reinterpret_cast<unsigned long long*>(part),
+        reinterpret_cast<unsigned long long*>(part) + nb, open);
+    scan_partials_kernel<<<1, kPartThreads, 0, st>>>(part, nb, total, nullptr, npairs, cap, nullptr, 0ull, 0u, open,
+                                                     kept);
+    const CountSrc src{rect_lo, rect_hi, RowOwnership{nullptr, 0u}, masked};
+    scan_duplicate_kernel<kDupBehind><<<nb, kDupThreads, tab_lds(nbins), st>>>(
+        src, n, part, nullptr, dkey, bin_bits, tiles_x, keys, vals, npairs, PassCounts{}, table, nbins);
     return hipGetLastError();
 }
 
@@ -570,14 +753,15 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
-                                 const uint32_t* fcut, uint32_t nbins) {
+                                 const uint32_t* fcut, uint32_t nbins, bool front) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     // (order: dkey holds the items' depth keys in that order)
     if (dkey && bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked};
     // (the marks: index order, the cooperative emission, the flag above the depth key)
-    if (fcut && (order || own.owner || !GS_DUP_COOP || !dkey || nbins > kDupCutBins || bin_bits + kDepthBits > 31))
+    if ((fcut || front) &&
+        (!fcut || order || own.owner || !GS_DUP_COOP || !dkey || nbins > kDupCutBins || bin_bits + kDepthBits > 31))
         return hipErrorInvalidValue;
     if (order) {  // depth order: per-item offsets, then one splat per lane
         if (!offsets) return hipErrorInvalidValue;
@@ -594,9 +778,16 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     }
     // (the cut table sized to the frame: a block that fits beside the previous
     // composite's workgroups starts sooner)
-    const size_t lds = fcut ? ((size_t)nbins * 2 + 15) & ~(size_t)15 : 0;
-    scan_duplicate_kernel<<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals,
-                                                        npairs, pc, fcut, nbins);
+    const size_t lds = fcut ? tab_lds(nbins) : 0;
+    if (front)
+        scan_duplicate_kernel<kDupFront><<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
+                                                                       keys, vals, npairs, pc, fcut, nbins);
+    else if (fcut)
+        scan_duplicate_kernel<kDupMark><<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
+                                                                      keys, vals, npairs, pc, fcut, nbins);
+    else
+        scan_duplicate_kernel<kDupPlain><<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
+                                                                       keys, vals, npairs, pc, fcut, nbins);
     return hipGetLastError();
 }
 

@@ -135,11 +135,20 @@ typedef struct gs_stats {
        cut_frame = 1 for a depth-cut frame.  Read with records_fetched.
        cut_dilate: the radius in 32-px bins over which the frame's cuts were
        dilated (0 unless the buffer set's recent frames left quadrants open:
-       a moving camera). */
+       a moving camera).
+       Renamed in ABI 10 (same offsets and types): cut_frame was two_slab and
+       cut_dilate was depth_cut; the old names stay as deprecated aliases of
+       the same storage for one release (README "Changes"). */
     int64_t pairs_sorted;
     int64_t open_tiles;
-    int32_t cut_frame;
-    uint32_t cut_dilate;
+    union {
+        int32_t cut_frame;
+        int32_t two_slab; /* deprecated alias of cut_frame */
+    };
+    union {
+        uint32_t cut_dilate;
+        uint32_t depth_cut; /* deprecated alias of cut_dilate */
+    };
 } gs_stats;
 
 typedef struct gs_handle gs_handle;
@@ -327,6 +336,22 @@ gs_status gs_group_set_timeout(gs_group *g, int32_t timeout_ms);
  * hip_stream (a stream of devices[0]); 0 = host memory, the call syncs. */
 gs_status gs_group_render(gs_group *g, const float view[16], const float proj[16], int32_t width, int32_t height,
                           float *out_rgba, int32_t out_is_device, void *hip_stream);
+/* Two frames in flight, rows scheme: n = 2 lets
+ * gs_group_render_pipelined overlap one frame's record all-to-all (on a
+ * communicator set of its own) with the previous frame's render and gather.
+ * n = 1 (default): gs_group_render only.  Not while a frame is in flight. */
+gs_status gs_group_set_frames_in_flight(gs_group *g, int32_t n);
+/* Projects this view's frame and starts its all-to-all, then renders and
+ * gathers the PREVIOUS call's frame into out_rgba (same conventions as
+ * gs_group_render; out_rgba must hold that frame: the previous call's width
+ * x height): *produced = 1 when out_rgba holds that frame (0 on the first
+ * call).  Every frame is bit-identical to gs_group_render's of the same
+ * view.  gs_group_flush finishes the frame still in flight (*produced = 0 when
+ * none); gs_group_render fails with GS_ERR_STATE while one is. */
+gs_status gs_group_render_pipelined(gs_group *g, const float view[16], const float proj[16], int32_t width,
+                                    int32_t height, float *out_rgba, int32_t out_is_device, void *hip_stream,
+                                    int32_t *produced);
+gs_status gs_group_flush(gs_group *g, float *out_rgba, int32_t out_is_device, void *hip_stream, int32_t *produced);
 int64_t gs_group_point_count(const gs_group *g);
 int32_t gs_group_size(const gs_group *g);
 int32_t gs_group_transport(const gs_group *g); /* the transport in use, -1 before initialize */

@@ -233,3 +233,107 @@ def test_group_replicated_bands_bitexact(built, world, mode, sh):
     from gaussian_splat_amd import GsError
     with pytest.raises(GsError):
         g.set_scheme("rows")  # a replicated group renders bands only
+
+
+def _pipelined_frames(g, views, W, H, host):
+    """Pipelined group frames over a camera path: frame i comes back from call
+    i + 1 (the last from flush)."""
+    got = [g.render_pipelined(V, P, W, H, host=host) for V, P in views]
+    assert got[0] is None, "the first pipelined call has no frame to return"
+    got = got[1:] + [g.flush(W, H, host=host)]
+    assert g.flush(W, H, host=host) is None  # (nothing left in flight)
+    if not host:
+        import torch
+        torch.cuda.synchronize()
+        got = [x.cpu().numpy() for x in got]
+    return got
+
+
+@pytest.mark.parametrize("world,mode,sh,host", [(2, "tile", 3, False), (3, "live50", 0, True), (4, "tile", 3, False)])
+def test_group_rows_pipelined_bitexact(built, world, mode, sh, host):
+    """Two frames in flight (gs_group_render_pipelined): frame k's record
+    all-to-all on the ranks' exchange streams under frame k-1's render and
+    gather; every frame comes back one call late, bit for bit the 1-GPU frame
+    of its view, over a camera path with a resolution change in it."""
+    from gaussian_splat_amd import GsError, InstancedSplatRenderer, Options
+    W, H = 960, 540
+    sc = _scene(120000, 141 + world, sh, W / H)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    g = _group(r, world)
+    g.set_frames_in_flight(2)
+    views = orbit_views(W, H, 4)
+    frames = _pipelined_frames(g, views, W, H, host)
+    for (V, P), got in zip(views, frames):
+        ref = r.render_host(V, P, W, H)
+        assert int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))) == 0
+    # a resolution change between two frames in flight
+    W2, H2 = 640, 400
+    (V1, P1), (V2, P2) = orbit_views(W, H, 1)[0], orbit_views(W2, H2, 2)[1]
+    assert g.render_pipelined(V1, P1, W, H, host=True) is None
+    a = g.render_pipelined(V2, P2, W2, H2, host=True)
+    with pytest.raises(GsError):
+        g.render_host(V1, P1, W, H)  # (a frame is in flight)
+    b = g.flush(W2, H2, host=True)
+    np.testing.assert_array_equal(a.view(np.uint32), r.render_host(V1, P1, W, H).view(np.uint32))
+    np.testing.assert_array_equal(b.view(np.uint32), r.render_host(V2, P2, W2, H2).view(np.uint32))
+    # back to one frame at a time
+    g.set_frames_in_flight(1)
+    np.testing.assert_array_equal(g.render_host(V1, P1, W, H).view(np.uint32), r.render_host(V1, P1, W, H).view(np.uint32))
+
+
+_STUB_PIPE_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import orbit_views
+from gaussian_splat_amd import InstancedSplatRenderer, Options, ShardedGroup
+from gaussian_splat_amd import scene as S
+
+def run(world, mode, sh, W, H, n, seed):
+    sc = S.activate(S.synthetic_raw(n, seed=seed, aspect=W / H, rest=sh > 0), sh)
+    r = InstancedSplatRenderer(sc, Options(mode=mode, sh_degree=sh, crop=False))
+    r.initialize(0)
+    views = orbit_views(W, H, 4)
+    frames = {}
+    for tr in ("rccl", "copy"):
+        g = ShardedGroup(r, world)
+        g.initialize([0] * world, tr)
+        assert g.transport == tr, (g.transport, tr)
+        g.set_frames_in_flight(2)
+        got = [g.render_pipelined(V, P, W, H, host=True) for V, P in views]
+        assert got[0] is None
+        frames[tr] = got[1:] + [g.flush(W, H, host=True)]
+        g.close()
+    for (V, P), a, b in zip(views, frames["rccl"], frames["copy"]):
+        ref = r.render_host(V, P, W, H)
+        for tr, x in (("rccl", a), ("copy", b)):
+            nd = int(np.count_nonzero(x.view(np.uint32) != ref.view(np.uint32)))
+            assert nd == 0, (world, tr, "pipelined vs 1 GPU", nd)
+    print("ok", world, mode, sh)
+
+run(2, "tile", 3, 640, 400, 60000, 121)
+run(3, "live50", 0, 960, 540, 80000, 122)
+"""
+
+
+def test_group_rccl_stub_pipelined_bitexact(built):
+    """The pipelined rows scheme's RCCL branches (the exchange communicator
+    set's grouped ncclSend/ncclRecv on the exchange streams, the band gather
+    on the gather streams) on a one-GPU box through the test stub (as
+    test_group_rccl_stub_bitexact): over a camera path every frame equals
+    the 1-GPU frame bit for bit, for the RCCL and the copy transport."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from gaussian_splat_amd.build import RCCL_STUB
+    root = Path(__file__).resolve().parents[1]
+    assert RCCL_STUB.exists(), "build() makes tests/cpp/librccl_stub.so"
+    env = dict(os.environ, GS_RCCL_LIB=str(RCCL_STUB))
+    p = subprocess.run([sys.executable, "-c", _STUB_PIPE_SCRIPT, str(root)], env=env, capture_output=True, text=True,
+                       timeout=170)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert p.stdout.count("ok ") == 2, p.stdout

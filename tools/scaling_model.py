@@ -5,15 +5,18 @@ the per-rank compute they measure, plus their xGMI link models.  NOT a
 measured curve: the driver's 8-GPU run measures that.
 
 For every world size it lists the two exact schemes as bench.py runs them:
-  rows        splat-index shards, unpipelined (bench.py's default): per rank
-              project + largest per-peer exchange over one link + render +
-              its band to rank 0 (rows_probe link_model_ms)
-  rows_pipe   the same with two frames in flight (--pipeline-rows 1):
-              max(compute, busiest link) (rows_probe pipelined_model_ms)
+  rows        splat-index shards with two frames in flight (bench.py's
+              default, --pipeline-rows 1; gs_group_render_pipelined):
+              max(project + render, busiest link) per rank
+              (rows_probe pipelined_model_ms)
+  rows_unpipelined  one frame at a time (--pipeline-rows 0): project +
+              largest per-peer exchange over one link + render + its band to
+              rank 0 (rows_probe link_model_ms)
   bands       the replicated scene, each rank its own bin rows:
               max(slowest rank, largest band over one link)
-and `chosen` = the faster of rows and bands (bench.py's headline rule),
-with `monotone` = every chosen period at or below the previous world size's.
+and `chosen` by bench.py's headline rule: rows (the splat-sharded scheme)
+whenever its period is at most bands', else bands; `monotone` = every chosen
+period at or below the previous world size's.
 
   python tools/scaling_model.py rows_1080p.json bands_1080p.json [more pairs ...] > model.json
 """
@@ -34,10 +37,10 @@ def model(rows: dict, bands: dict) -> dict:
             continue
         r = rw.get(str(g)) or rw[g]
         b = bw.get(str(g)) or bw.get(g)
-        e = {"rows": r["link_model_ms"], "rows_pipe": r["pipelined_model_ms"]}
+        e = {"rows": r["pipelined_model_ms"], "rows_unpipelined": r["link_model_ms"]}
         if b:
             e["bands"] = b["period_model_ms"]
-        choice = min((k for k in ("rows", "bands") if k in e), key=lambda k: e[k])
+        choice = "rows" if "bands" not in e or e["rows"] <= e["bands"] else "bands"
         e["chosen"] = choice
         e["chosen_ms"] = e[choice]
         e["speedup_vs_1"] = round(base / e[choice], 3)
