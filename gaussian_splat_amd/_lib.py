@@ -36,7 +36,7 @@ class GsStats(C.Structure):
                 ("bytes_preprocess", C.c_int64), ("bytes_scan", C.c_int64), ("bytes_duplicate", C.c_int64),
                 ("bytes_sort", C.c_int64), ("bytes_ranges", C.c_int64), ("bytes_composite", C.c_int64),
                 ("ms_depth_sort", C.c_float), ("ms_exchange", C.c_float), ("bytes_depth_sort", C.c_int64),
-                ("binning", C.c_int32), ("reserved_stats", C.c_int32), ("records_fetched", C.c_int64),
+                ("binning", C.c_int32), ("front_only", C.c_int32), ("records_fetched", C.c_int64),
                 ("pairs_sorted", C.c_int64), ("open_tiles", C.c_int64), ("cut_frame", C.c_int32),
                 ("cut_dilate", C.c_uint32)]
 

@@ -68,6 +68,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_DUP_FRONT  // A/B knob: 1 = a bin-first depth-cut frame emits only its front pairs (launch_front_count)
 #define GS_DUP_FRONT 1
 #endif
+#ifndef GS_DUP_LOOKBACK  // A/B knob: 1 = the front-only duplicate finds its offsets by look-back (no count kernel)
+#define GS_DUP_LOOKBACK 1
+#endif
 #ifndef GS_DUP_FRONT_COUNT  // A/B knob: 1 = the front-only duplicate counts the first sort pass's digits
 #define GS_DUP_FRONT_COUNT 1
 #endif
@@ -172,6 +175,7 @@ struct gs_handle {
     } fused_prep;
     bool front_last = false;   // the frame in `stats` emitted only its front pairs (its fallback regenerates)
     uint64_t pairs_emitted = 0;  // pairs the frame's duplicate wrote (= stats.pairs unless front_last)
+    static constexpr uint64_t kEmittedOnDevice = ~0ull;  // (look-back: in npairs[set], read by gs_last_stats)
     DevBuf fbpart, fbtot;      // front_last frames' fallback pair scan (2 rows per block; totals)
     DevBuf ppart;
     size_t ppart_words = 0;
@@ -721,18 +725,21 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (front && GS_DUP_FRONT_COUNT) pc = lp.pc;
     }
     h->front_last = front;
+    // (front-only, GS_DUP_LOOKBACK: no count kernel; the duplicate's blocks
+    // count their front pairs and find their offsets by look-back)
+    const bool lookb = front && GS_DUP_LOOKBACK;
     // the host learns P by polling the totals kernel's sequence word in
     // host-mapped memory (GS_HOST_POLL) or by an event in its dispatch packet
     const unsigned long long seq = GS_HOST_POLL ? ++h->totals_seq : 0ull;
     hipEvent_t tev = GS_HOST_POLL ? nullptr : h->totals_ev;
     if (fused) {
         const uint32_t nb = (m + gs::kScanItems - 1) / gs::kScanItems;
-        if (front)  // the front pairs' block sums into ppart's fourth row
+        if (front && !lookb)  // the front pairs' block sums into ppart's fourth row
             GS_HIP(gs::launch_front_count(rect_lo, rect_hi, carry_dkey, m, U.cell_mask != 0, (uint32_t)U.tiles_x,
                                           h->cut_in, T, h->ppart.as<unsigned long long>() + (size_t)3 * nb, st));
         GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), nb, h->partials.as<uint64_t>(),
                                               h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
-                                              st, tev, seq, front));
+                                              st, tev, seq, front, lookb));
         h->ppart_dirty = false;
     } else {
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
@@ -750,7 +757,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
                                                  (uint32_t)U.tiles_x, own.dev, U.cell_mask != 0, carry_dkey, bits,
                                                  h->keys.as<uint32_t>(), h->vals.as<uint32_t>(),
                                                  np, st, h->offsets.as<uint32_t>(), pc,
-                                                 flt.flag ? h->cut_in : nullptr, flt.flag ? T : 0u, front);
+                                                 flt.flag ? h->cut_in : nullptr, flt.flag ? T : 0u, front,
+                                                 lookb ? np : nullptr, cap);
         if (e != hipSuccess) return e;
         if (timed) mark(h, 4, st);
         // (depth-cut frames: sorted into fkeys/fvals, so keys/vals keep every
@@ -813,9 +821,14 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         // the real one for the dilation controller)
         if (tail && h->host_total) h->host_total[6 + h->set] = ~0ull;
         if (!(cap = reserve_pairs(h, P_all))) return fail(GS_ERR_OOM, "pair buffers");
-        const uint32_t p32 = (uint32_t)P;
+        // (look-back: 1 lets the duplicate run, its last block stores the
+        // count; the statuses and the ticket cleared again)
+        const uint32_t p32 = lookb ? 1u : (uint32_t)P;
         GS_HIP(hipMemcpy(np, &p32, 4, hipMemcpyHostToDevice));
-        pc = pass_counts(h, m, order == nullptr, plan, cap, P);
+        if (lookb)
+            GS_HIP(hipMemsetAsync(h->partials.as<uint64_t>(), 0,
+                                  ((size_t)(m + gs::kScanItems - 1) / gs::kScanItems + 1) * 8, st));
+        pc = pass_counts(h, m, order == nullptr, plan, cap, lookb ? P_all : P);
         if (cut_frame) pc.cut = h->cut_in;
 #if !GS_DUP_FILTER_COUNT
         if (cut_frame && !(front && GS_DUP_FRONT_COUNT)) pc = gs::PassCounts{};
@@ -827,7 +840,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     }
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
-    h->pairs_emitted = P;
+    h->pairs_emitted = lookb ? gs_handle::kEmittedOnDevice : P;
     *pairs = P_all;
     return GS_OK;
 }
@@ -1153,8 +1166,10 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             ca.open_q_count = open_counter(h);
             ca.state = h->cstate.as<float4>();
             ca.cut_in = h->cut_in;
-            ca.order = own.dev.owner ? nullptr : h->ord_in;
-            ca.wcost = own.dev.owner ? nullptr : h->wcost.as<uint32_t>();
+            // (the longest-first order: whole frames on the strip kernel)
+            const bool ordered = !own.dev.owner && gs::composite_strip((uint32_t)(U.tiles_x * U.tiles_y));
+            ca.order = ordered ? h->ord_in : nullptr;
+            ca.wcost = ordered ? h->wcost.as<uint32_t>() : nullptr;
         }
         // everything that reads the lists, queued before the host waits for P
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
@@ -1237,8 +1252,9 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
         ca.open_q_count = open_counter(h);
         ca.state = h->cstate.as<float4>();
         ca.cut_in = h->cut_in;
-        ca.order = own.dev.owner ? nullptr : h->ord_in;
-        ca.wcost = own.dev.owner ? nullptr : h->wcost.as<uint32_t>();
+        const bool ordered = !own.dev.owner && gs::composite_strip((uint32_t)(U.tiles_x * U.tiles_y));
+        ca.order = ordered ? h->ord_in : nullptr;
+        ca.wcost = ordered ? h->wcost.as<uint32_t>() : nullptr;
         const ListTail tail = [&](const uint32_t* sv) -> gs_status {
             gs::CompositeArgs c = ca;
             c.vals = sv;
@@ -1304,8 +1320,11 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
         s.bytes_scan = (N + gs::kScanItems - 1) / gs::kScanItems * 16 + T * 8;
     // (front-only frames write only their front pairs, counted first by
     // launch_front_count: another read of the rects and depth keys)
-    const int64_t Pe = h->front_last ? (int64_t)h->pairs_emitted : Pi;
-    if (h->front_last) s.bytes_scan += N * 12;
+    // (look-back: the emitted count is on the device; P until gs_last_stats
+    // reads it, and no separate count kernel)
+    const bool pe_dev = h->front_last && h->pairs_emitted == gs_handle::kEmittedOnDevice;
+    const int64_t Pe = h->front_last && !pe_dev ? (int64_t)h->pairs_emitted : Pi;
+    if (h->front_last && !pe_dev) s.bytes_scan += N * 12;
     s.bytes_duplicate = (h->bin_first_frame ? N * 12 : N * 28) + Pe * 8;
     s.binning = h->bin_first_frame ? GS_BINNING_BIN_FIRST : GS_BINNING_DEPTH_FIRST;
     if (h->bin_first_frame) {
@@ -1323,6 +1342,7 @@ void fill_stats(gs_handle* h, uint64_t P, const gs::FrameUniforms& U) {
     s.records_fetched = -1;
     s.pairs_sorted = Pi;
     s.cut_frame = h->cut_frame ? 1 : 0;
+    s.front_only = h->front_last ? 1 : 0;
     h->cut_lists = h->cut_frame && h->cut_in;
     // (depth-cut frames with cuts: the first sort pass reads every pair, keeps
     // the front lists' P1; the rest runs on P1 -- set by gs_last_stats)
@@ -1678,7 +1698,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             // pass moves the pairs behind the cuts (most of a frame's: 86 % at
             // 50M @4K); the fallback lists regenerate theirs when a quadrant
             // is left open (cut_tail).
-            h->fused_prep.front = GS_DUP_FRONT && h->cut_in && T <= gs::kDupCutBins &&
+            // (not while the set's cuts are dilated: a moving camera leaves
+            // quadrants open, and regenerating their fallback pairs from every
+            // splat's rect costs more than the whole pairs' sort pass it saves)
+            h->fused_prep.front = GS_DUP_FRONT && h->cut_in && h->cut_r[h->set] == 0 && T <= gs::kDupCutBins &&
                                   list_key_bits(U) + gs::kDepthBits <= 31;
             h->fused_prep.pc.cut = h->cut_in;  // (with cuts: the duplicate counts only the pairs the filter keeps)
 #if !GS_DUP_FILTER_COUNT
@@ -1747,6 +1770,12 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
             // per-bin sorted; each open tile's 256 pixel states written and
             // read back)
             gs_stats& s = h->stats;
+            if (h->front_last && h->pairs_emitted == gs_handle::kEmittedOnDevice) {
+                uint32_t pe = 0;  // (look-back: the duplicate's last block stored it)
+                GS_HIP(hipMemcpy(&pe, h->npairs.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));
+                s.bytes_duplicate += ((int64_t)pe - s.pairs) * 8;
+                h->pairs_emitted = pe;
+            }
             if (h->cut_lists) {
                 uint32_t k1 = 0;
                 GS_HIP(hipMemcpy(&k1, h->kept.as<uint32_t>() + h->stats_set, 4, hipMemcpyDeviceToHost));

@@ -862,11 +862,17 @@ __global__ __launch_bounds__(256, GS_STRIP_WAVES) __attribute__((amdgpu_num_sgpr
 #define GS_COMPOSITE_STRIP 1
 #endif
 
+bool composite_strip(uint32_t bins) { return GS_COMPOSITE_STRIP && bins > kStripMinBins; }
+
 template <int MODE, bool CAP, int SLAB = 0, int PASS = 0>
 static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t t0 = nullptr,
                               hipEvent_t t1 = nullptr) {
     if (a.nrows < 0 || a.nrows > a.tiles_y || (!a.rows && a.nrows != a.tiles_y)) return hipErrorInvalidValue;
-    constexpr bool kStrip = GS_COMPOSITE_STRIP && (MODE == 0 || MODE == 1) && !CAP && SLAB == 0;
+    // (the strip kernel for launches of many bins; a small one -- a rank's band
+    // at 8 ranks, a small frame -- on the tile kernel: there the slowest
+    // workgroup bounds the launch, and a tile's walks one pixel per lane)
+    constexpr bool kStripOk = (MODE == 0 || MODE == 1) && !CAP && SLAB == 0;
+    const bool kStrip = kStripOk && composite_strip((uint32_t)(a.tiles_x * a.nrows));
     const uint32_t nwg = (uint32_t)((kStrip ? 2 : 4) * a.tiles_x * a.nrows);
     if (nwg == 0) {  // no owned tiles: the timing events still mark the (empty) stage
         if (t0 && hipEventRecord(t0, st) != hipSuccess) return hipGetLastError();
@@ -874,10 +880,12 @@ static hipError_t launch_mode(const CompositeArgs& a, hipStream_t st, hipEvent_t
         return hipSuccess;
     }
     // t0/t1 (optional) are recorded by the dispatch packet itself
-    if constexpr (kStrip) {
-        hipExtLaunchKernelGGL(composite_strip_kernel<MODE < 2 ? MODE : 0, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0,
-                              t1, 0, a, nwg);
-        return hipGetLastError();
+    if constexpr (kStripOk) {
+        if (kStrip) {
+            hipExtLaunchKernelGGL(composite_strip_kernel<MODE < 2 ? MODE : 0, PASS>, dim3(nwg), dim3(kTileThreads), 0, st,
+                                  t0, t1, 0, a, nwg);
+            return hipGetLastError();
+        }
     }
     hipExtLaunchKernelGGL(composite_kernel<MODE, CAP, SLAB, PASS>, dim3(nwg), dim3(kTileThreads), 0, st, t0, t1, 0, a,
                           nwg);

@@ -73,6 +73,20 @@ __device__ __forceinline__ uint32_t rect_with_mask(uint32_t w, uint32_t m4lo, ui
     return w | (m4lo << 12) | (m4hi << 28);
 }
 
+// A window [base, base + span) of a u32 array of n items, read through a raw
+// buffer resource (uniform: scalar registers): one 32-bit offset per load
+// instead of a 64-bit address, and reads past n return 0 (no clamping, so no
+// load waits inside a branch).  Dword 3 of a gfx9 raw buffer descriptor.
+struct BufU32 {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ BufU32(const uint32_t* p, uint32_t base, uint32_t n, uint32_t span)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p) + base, (short)0,
+                                              (int)((base < n ? min(n - base, span) : 0u) * 4u), 0x00020000)) {}
+    __device__ __forceinline__ uint32_t operator[](uint32_t i) const {  // (i: within the window)
+        return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 0);
+    }
+};
+
 // Scene SoA resident in HBM: coalesced 16-B loads per lane.
 struct SceneDev {
     const float4* p0;   // x, y, z, opacity

@@ -84,9 +84,13 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // after the three atomic rows), total[0] = the front pairs; total[8] = every
 // pair of the frame (row 0) either way, and npairs is 0 when the pair buffers
 // cannot hold them all (the fallback lists may need them).
+// lookback (with front): no front sums; partials[0..nb] (nb + 1 words) are
+// cleared for the duplicate's look-back, total[0] = 0 and npairs = 1 (the
+// duplicate stores the front pairs' count there), or 0 as above.
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done = nullptr, unsigned long long seq = 0, bool front = false);
+                                      hipEvent_t done = nullptr, unsigned long long seq = 0, bool front = false,
+                                      bool lookback = false);
 // Front-only emission of a depth-cut frame (index order, every
 // bin row owned): per 4096-splat block, the pairs the front duplicate emits
 // (launch_scan_duplicate front): a splat whose rect lies within 4x4 bins
@@ -139,13 +143,18 @@ constexpr uint32_t kDupCountTiles = 8;  // sort tiles a duplicate block counts i
 constexpr uint32_t kDupCutBins = 16384;
 constexpr uint32_t kBehindFlag = 0x80000000u;
 // front (with fcut): only the pairs launch_front_count counted, at offsets
-// scanned from its sums (launch_scan_partials_fused front).
+// scanned from its sums (launch_scan_partials_fused front).  np_out (with
+// front): each block counts its own front pairs and finds its offset by a
+// decoupled look-back over partials (nb + 1 words cleared by
+// launch_scan_partials_fused lookback; launch_front_count is not needed); the
+// front pairs' count goes to *np_out; pairs past cap are never written.
 hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo, const uint32_t* rect_hi,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st,
                                  uint32_t* offsets = nullptr, PassCounts pc = PassCounts{},
-                                 const uint32_t* fcut = nullptr, uint32_t nbins = 0, bool front = false);
+                                 const uint32_t* fcut = nullptr, uint32_t nbins = 0, bool front = false,
+                                 uint32_t* np_out = nullptr, uint32_t cap = 0);
 
 // ---- bin_depth_sort.hip ------------------------------------------------------
 // Per bin b with list [start, end) = decode_range(ranges[b]) of (key, val)
@@ -300,6 +309,17 @@ struct CompositeArgs {
 // id <= thr[pixel] are composited.
 hipError_t launch_composite(const CompositeArgs& a, int mode, hipStream_t st, hipEvent_t t0 = nullptr,
                             hipEvent_t t1 = nullptr);
+// Tile and live-50 frames of more than kStripMinBins composited bins run the
+// strip kernel (two 16x16 tiles per workgroup, two pixels per lane, the
+// longest-first bin order: CompositeArgs::order / wcost); fewer bins (a rank's
+// band at 8 ranks, small frames) run one workgroup per tile: with less than a
+// round of workgroups the slowest one bounds the launch, and a tile walks its
+// bin's list one pixel per lane.  Same pixels either way.
+#ifndef GS_STRIP_MIN_BINS  // A/B knob
+#define GS_STRIP_MIN_BINS 512
+#endif
+constexpr uint32_t kStripMinBins = GS_STRIP_MIN_BINS;
+bool composite_strip(uint32_t bins);
 // Depth cuts: the next cut of every bin from the largest of its 16 quadrants'
 // cut positions (CompositeArgs::qrec): ~0 -> 0xFFFF (every pair), 0 -> 0,
 // else the depth key of the list record before it plus `margin`, at most

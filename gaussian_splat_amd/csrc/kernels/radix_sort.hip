@@ -46,6 +46,9 @@ struct SortIO {
 #define GS_RS_PASS_WAVES 1
 #endif
 constexpr int ipt_for(int nv) { return nv == 1 ? GS_RS_IPT1 : 8; }
+#ifndef GS_RS_PAIR_STAGE  // A/B knob: 1 = one-array passes stage (key, value) pairs through LDS together
+#define GS_RS_PAIR_STAGE 0
+#endif
 constexpr uint32_t tile_items(int nv) { return (uint32_t)kRsThreads * ipt_for(nv); }
 
 // Exclusive scan over the kRsThreads-lane workgroup (LDS-only barriers).
@@ -211,7 +214,10 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
     __shared__ uint32_t wh[kRsWaves][ND];  // wave-private running counts -> wave offsets
     __shared__ uint32_t blk_start[ND];     // tile-local start of each digit
     __shared__ uint32_t gbase[ND];         // global start of this tile's digit run
-    __shared__ uint32_t stage[TILE];
+    // (one array: keys and values staged together as (key, value) pairs, one
+    // scatter and one gather through LDS instead of one per array)
+    constexpr bool kPair = NV == 1 && GS_RS_PAIR_STAGE;
+    __shared__ uint32_t stage[kPair ? 2 * TILE : TILE];
     __shared__ uint32_t tmp[kRsWaves];
     __shared__ uint32_t rflag[ND];         // (ranges, shift > 0: run-end merges this tile skips)
 
@@ -345,20 +351,33 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
     // keys: stage in tile-local sorted order, write out; each slot's global
     // destination (from its staged key's digit) stays in registers for the
     // value arrays
+    uint2* const stage2 = reinterpret_cast<uint2*>(stage);
 #pragma unroll
     for (int k = 0; k < IPT; ++k)
-        if (kept(k)) stage[pos[k]] = FILT ? key[k] & flt.kmask : key[k];
+        if (kept(k)) {
+            const uint32_t sk = FILT ? key[k] & flt.kmask : key[k];
+            if constexpr (kPair) stage2[pos[k]] = make_uint2(sk, io.vin[0] ? val[0][k] : base + k * 64 + lane);
+            else stage[pos[k]] = sk;
+        }
     block_lds_sync();
     uint32_t gdst[IPT];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
         const uint32_t j = tid + k * kRsThreads;
         if (j < cnt) {
-            const uint32_t key = stage[j];
+            uint32_t key, v = 0u;
+            if constexpr (kPair) {
+                const uint2 kv = stage2[j];
+                key = kv.x;
+                v = kv.y;
+            } else {
+                key = stage[j];
+            }
             const uint32_t d = (key >> shift) & mask;
             const uint32_t g = gbase[d] + (j - blk_start[d]);
             gdst[k] = g;
             io.kout[g] = key;
+            if constexpr (kPair) io.vout[0][g] = v;
 #ifdef GS_RS_ABL_NORANGES  // ablation (timing only): no run ends
             if (false) {
 #else
@@ -367,8 +386,10 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
                 // run ends of this key inside the tile (the tile's output is a
                 // contiguous, fully sorted slice of the final order per digit)
                 const uint32_t rk = key & rmask;
-                const bool s0 = j == 0 || (stage[j - 1] & rmask) != rk;
-                const bool s1 = j + 1 == cnt || (stage[j + 1] & rmask) != rk;
+                const uint32_t kprev = j == 0 ? 0u : (kPair ? stage2[j - 1].x : stage[j - 1]);
+                const uint32_t knext = j + 1 == cnt ? 0u : (kPair ? stage2[j + 1].x : stage[j + 1]);
+                const bool s0 = j == 0 || (kprev & rmask) != rk;
+                const bool s1 = j + 1 == cnt || (knext & rmask) != rk;
                 if (s0 || s1) {
                     const uint32_t lo = key & lm;
                     const uint32_t fl = rskip ? rflag[d] : 0u;
@@ -378,9 +399,9 @@ __global__ __launch_bounds__(512, GS_RS_PASS_WAVES) GS_RS_PASS_ATTR void rts_pas
             }
         }
     }
-    // values: same permutation
+    // values: same permutation (already written with the keys when staged as pairs)
 #pragma unroll
-    for (int a = 0; a < NV; ++a) {
+    for (int a = 0; a < (kPair ? 0 : NV); ++a) {
         block_lds_sync();
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {

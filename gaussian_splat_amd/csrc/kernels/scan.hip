@@ -20,6 +20,9 @@
 namespace gs {
 
 constexpr int kScanIpt = kScanItems / 256;  // 16 consecutive items per lane
+#ifndef GS_BUF_LOADS  // A/B knob: 1 = the count and duplicate kernels read through raw buffer resources (BufU32)
+#define GS_BUF_LOADS 0
+#endif
 
 struct CountSrc {
     const uint32_t* lo;
@@ -80,6 +83,7 @@ __global__ __launch_bounds__(256) void scan_reduce_kernel(CountSrc src, uint32_t
 // registers, one block-wide scan joins them (a single pass for nb <= 4096;
 // larger grids loop).
 constexpr int kPartThreads = 1024;
+constexpr uint32_t kPartLookback = 4;  // (scan_partials_kernel prow)
 constexpr int kPartIpt = 4;
 
 template <typename T>
@@ -106,6 +110,8 @@ __device__ __forceinline__ T block1024_exclusive_scan(T v, T* tmp, T* total) {
 // third row's sum (the duplicate's wave-max work) goes to total[4].
 // prow (src only): the row whose sums are scanned into the offsets, 0 (every
 // pair) or 3 (the front pairs a depth-cut frame emits, launch_front_count);
+// kPartLookback: none (the front duplicate finds its blocks' offsets by
+// look-back): partials[0..nb] are cleared for it and total[0] is 0;
 // row 0's sum is total[8] either way (the frame's every pair: the pair buffers
 // must hold them all, so npairs is 0 when they do not).  guard (may be null):
 // nothing is done while *guard == 0 (the fallback lists' regeneration).
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
 #pragma unroll
         for (int k = 0; k < kPartIpt; ++k) {
             if (src) {
-                v[k] = i0 + k < nb ? (uint64_t)src[(size_t)prow * nb + i0 + k] : 0u;
+                v[k] = i0 + k < nb && prow != kPartLookback ? (uint64_t)src[(size_t)prow * nb + i0 + k] : 0u;
                 all += i0 + k < nb ? (uint64_t)src[i0 + k] : 0u;
                 vis += i0 + k < nb ? (uint64_t)src[nb + i0 + k] : 0u;
                 wmax += i0 + k < nb ? (uint64_t)src[2u * nb + i0 + k] : 0u;
@@ -150,11 +156,12 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         uint64_t run = carry + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
 #pragma unroll
         for (int k = 0; k < kPartIpt; ++k) {
-            if (i0 + k < nb) partials[i0 + k] = run;
+            if (i0 + k < nb) partials[i0 + k] = run;  // (look-back: 0, every block's status cleared)
             run += v[k];
         }
         carry += t;
     }
+    if (prow == kPartLookback && threadIdx.x == 0) partials[nb] = 0u;  // (the duplicate's block ticket)
     uint64_t vt, wt = 0, at = carry;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
     if (src) block1024_exclusive_scan<uint64_t>(wmax, tmp, &wt);
@@ -164,7 +171,9 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         total[1] = vt;
         total[4] = wt;
         total[8] = at;
-        if (npairs) *npairs = at <= cap ? (uint32_t)carry : 0u;  // 0: the pair buffers are too small
+        // (0: the pair buffers are too small; look-back: the duplicate's last
+        // block stores the front pairs' count over the 1 that lets it run)
+        if (npairs) *npairs = at <= cap ? (prow == kPartLookback ? (at > 0u ? 1u : 0u) : (uint32_t)carry) : 0u;
         if (kept) *kept = (uint32_t)carry;
         // (seq: the host polls total[5]; the totals are visible before it)
         if (seq) __hip_atomic_store(reinterpret_cast<unsigned long long*>(total) + 5, seq, __ATOMIC_RELEASE,
@@ -221,15 +230,37 @@ __device__ __forceinline__ bool tab_keep(const uint16_t* tab, uint32_t bin, uint
     return BEHIND ? dk > t : dk <= t;
 }
 
-// The bins of inc16 (a small rect's) that the table keeps.
+// The bins of inc16 (a small rect's) that the table keeps.  The first four
+// bins' table words are read together (independent LDS reads, one wait:
+// nearly every rect has at most four bins; an unused slot reads the rect's
+// first bin, in the frame), the rest one by one.  (Measured and not kept, the
+// count at 50M: a 2x2 fast path with a loop for every other rect, 0.34 ->
+// 0.41 ms, since a wave pays the loop's serial reads whenever any of its
+// rects is three bins wide or tall; row bases selected instead of multiplied,
+// 0.34 -> 0.39 ms.)
 template <bool BEHIND>
 __device__ __forceinline__ uint32_t filter_inc16(uint32_t inc, const BinRect& r, uint32_t tiles_x, const uint16_t* tab,
                                                  uint32_t dk) {
-    uint32_t out = 0u, m = inc;
-    while (m) {
+    const uint32_t b00 = r.by0 * tiles_x + r.bx0;
+    auto bin_of = [&](uint32_t b) { return b00 + (b >> 2) * tiles_x + (b & 3u); };
+    uint32_t m = inc, bit[4], t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t b = m ? (uint32_t)__builtin_ctz(m) : 0u;
+        bit[j] = m ? 1u << b : 0u;
+        m &= m - 1u;
+        t[j] = tab[bin_of(b)];
+    }
+    uint32_t out = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool keep = BEHIND ? dk > t[j] : dk <= t[j];
+        out |= keep ? bit[j] : 0u;
+    }
+    while (m) {  // (rects of more than four bins)
         const uint32_t b = (uint32_t)__builtin_ctz(m);
         m &= m - 1u;
-        if (tab_keep<BEHIND>(tab, (r.by0 + (b >> 2)) * tiles_x + r.bx0 + (b & 3u), dk)) out |= 1u << b;
+        if (tab_keep<BEHIND>(tab, bin_of(b), dk)) out |= 1u << b;
     }
     return out;
 }
@@ -241,12 +272,13 @@ __device__ __forceinline__ uint32_t filter_inc16(uint32_t inc, const BinRect& r,
 // runs only when quadrants are open).
 template <int FM>
 __device__ __forceinline__ uint32_t filtered_count(uint32_t lo, uint32_t hi, bool masked, uint32_t dk, uint32_t tiles_x,
-                                                   const uint16_t* tab) {
+                                                   uint32_t nbins, const uint16_t* tab) {
     const BinRect r = bin_rect(lo, hi, masked);
     if (r.empty) return 0u;
     if constexpr (FM == kDupFront) {
-        if (small_rect(r)) return (uint32_t)__builtin_popcount(filter_inc16<false>(rect_inc16(r), r, tiles_x, tab, dk));
-        return rect_tile_count(lo, hi, RowOwnership{nullptr, 0u}, masked);
+        if (small_rect(r))
+            return (uint32_t)__builtin_popcount(filter_inc16<false>(rect_inc16(r), r, tiles_x, tab, dk));
+        return (r.bx1 - r.bx0 + 1u) * (r.by1 - r.by0 + 1u);  // (a larger rect has no excluded bins)
     } else {
         uint32_t c = 0u;
         for (uint32_t by = r.by0; by <= r.by1; ++by)
@@ -256,15 +288,28 @@ __device__ __forceinline__ uint32_t filtered_count(uint32_t lo, uint32_t hi, boo
     }
 }
 
-// Stages the table (nbins words, min(t, 0xFFFF)) in LDS.
+// Stages the table (nbins words, min(t, 0xFFFF)) in LDS: four loads per lane
+// issued together (clamped, so none waits inside a branch), then the stores.
 __device__ __forceinline__ void stage_tab16(const uint32_t* __restrict__ t, uint32_t nbins, uint16_t* tab) {
-    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) tab[i] = (uint16_t)min(t[i], 0xFFFFu);
+    for (uint32_t i0 = threadIdx.x; i0 < nbins; i0 += 4u * blockDim.x) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = t[min(i0 + k * blockDim.x, nbins - 1u)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k * blockDim.x < nbins) tab[i0 + k * blockDim.x] = (uint16_t)min(v[k], 0xFFFFu);
+    }
 }
 
 // Per 4096-item block (the scan's and the duplicate's blocking): the pairs the
 // block's items emit under FM into out[b] and, when vis is set, the items
-// that emit any into vis[b] (plain stores: one workgroup per block).  guard
-// (may be null): nothing while *guard == 0.
+// that emit any into vis[b] (plain stores).  Persistent: a workgroup stages
+// the table in LDS once and then walks blocks blockIdx.x, + gridDim.x, ...,
+// loading the next block's rects and keys while it counts the current one
+// (one table copy per workgroup instead of per block: at 50M splats @4K,
+// 12k blocks would read 16 KB each).  guard (may be null): nothing while
+// *guard == 0.
+constexpr int kCountGrid = 512;  // 2 workgroups of 1024 lanes per CU
 template <int FM>
 __global__ __launch_bounds__(1024) void filtered_count_kernel(const uint32_t* __restrict__ rect_lo,
                                                               const uint32_t* __restrict__ rect_hi,
@@ -275,39 +320,65 @@ __global__ __launch_bounds__(1024) void filtered_count_kernel(const uint32_t* __
                                                               const unsigned long long* __restrict__ guard) {
     if (guard && *guard == 0ull) return;
     extern __shared__ uint16_t tab[];
-    __shared__ uint2 wsum[16];
+    __shared__ uint2 wsum[2][16];  // (double-buffered: one barrier per block)
     constexpr int IPT = kScanItems / 1024;
-    const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, nblocks = (n + kScanItems - 1) / kScanItems;
     uint32_t lo[IPT], hi[IPT], dk[IPT];
+    auto load = [&](uint32_t b, uint32_t* l, uint32_t* h, uint32_t* d) {
+#if GS_BUF_LOADS  // (A/B: raw buffer loads, reads past n return 0)
+        const uint32_t base = b < nblocks ? b * kScanItems : n;
+        const BufU32 blo(rect_lo, base, n, kScanItems), bhi(rect_hi, base, n, kScanItems), bdk(dkey, base, n, kScanItems);
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {  // (every load first, clamped)
-        const uint32_t j = min(blk + k * 1024 + tid, n - 1u);
-        lo[k] = rect_lo[j];
-        hi[k] = rect_hi[j];
-        dk[k] = dkey[j];
-    }
+        for (int k = 0; k < IPT; ++k) {
+            l[k] = blo[k * 1024 + tid];
+            h[k] = bhi[k * 1024 + tid];
+            d[k] = bdk[k * 1024 + tid];
+        }
+#else  // (clamped: none waits in a branch; past n counted as nothing below)
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t j = min(b * kScanItems + k * 1024 + tid, n - 1u);
+            l[k] = rect_lo[j];
+            h[k] = rect_hi[j];
+            d[k] = dkey[j];
+        }
+#endif
+    };
+    uint32_t b = blockIdx.x;
+    load(b, lo, hi, dk);
     stage_tab16(table, nbins, tab);
     __syncthreads();
-    uint32_t c = 0u, v = 0u;
+    for (int par = 0; b < nblocks; b += gridDim.x, par ^= 1) {
+        uint32_t nlo[IPT], nhi[IPT], ndk[IPT];
+        load(b + gridDim.x, nlo, nhi, ndk);  // (the next block's, in flight while this one counts)
+        uint32_t c = 0u, v = 0u;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        const uint32_t x = blk + k * 1024 + tid < n ? filtered_count<FM>(lo[k], hi[k], masked, dk[k], tiles_x, tab) : 0u;
-        c += x;
-        v += x > 0u;
-    }
-    c = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c), 63);
-    v = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
-    if ((tid & 63u) == 0) wsum[tid >> 6] = make_uint2(c, v);
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t sc = 0, sv = 0;
-#pragma unroll
-        for (int w = 0; w < 16; ++w) {
-            sc += wsum[w].x;
-            sv += wsum[w].y;
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t x =
+                b * kScanItems + k * 1024 + tid < n ? filtered_count<FM>(lo[k], hi[k], masked, dk[k], tiles_x, nbins, tab) : 0u;
+            c += x;
+            v += x > 0u;
         }
-        out[blockIdx.x] = sc;
-        if (vis) vis[blockIdx.x] = sv;
+        c = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(c), 63);
+        v = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(v), 63);
+        if ((tid & 63u) == 0) wsum[par][tid >> 6] = make_uint2(c, v);
+        block_lds_sync();
+        if (tid == 0) {
+            uint64_t sc = 0, sv = 0;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) {
+                sc += wsum[par][w].x;
+                sv += wsum[par][w].y;
+            }
+            out[b] = sc;
+            if (vis) vis[b] = sv;
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            lo[k] = nlo[k];
+            hi[k] = nhi[k];
+            dk[k] = ndk[k];
+        }
     }
 }
 
@@ -416,12 +487,56 @@ __device__ __forceinline__ uint32_t block_dup_exclusive_scan(uint32_t v, uint32_
     return base + inc - v;
 }
 
+// Decoupled look-back (the front duplicate, GS_DUP_LOOKBACK): block b's
+// status word lb[b] is 0 (not yet), kLbAgg | its pair count, or kLbIncl | the
+// pairs of blocks 0..b.  Called by wave 0 with the block's count; returns the
+// pairs of blocks 0..b-1 in every lane.  Each step reads the 64 statuses below
+// a window at once (per-lane addresses: vector loads at agent scope, which
+// see other XCDs' stores); it is complete when every status up to the
+// nearest inclusive one is published.  Blocks are numbered by a ticket
+// (lb[nb]) taken at start, so every predecessor a block waits for is already
+// running.  The spin is bounded (kLbSpinMax sleeps): a block that gives up
+// sums what it saw, and its pair run is then dropped by the capacity test,
+// never written out of bounds.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62;
+constexpr uint32_t kLbSpinMax = 1u << 20;
+__device__ __forceinline__ uint32_t lookback_prefix(uint64_t* lb, uint32_t b, uint32_t count) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane == 0)
+        __hip_atomic_store(lb + b, (b ? kLbAgg : kLbIncl) | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (b == 0) return 0u;
+    uint32_t excl = 0;
+    for (int64_t w = b;; w -= 64) {
+        const int64_t idx = w - 1 - (int64_t)lane;
+        uint64_t v = kLbIncl, incl, below;
+        uint32_t first;
+        for (uint32_t spin = 0;; ++spin) {
+            v = idx >= 0 ? __hip_atomic_load(lb + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+            incl = __ballot((v >> 62) == 2u);
+            first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+            below = first >= 63u ? ~0ull : (2ull << first) - 1ull;  // (lanes 0..first)
+            if ((__ballot((v >> 62) == 0u) & below) == 0ull || spin >= kLbSpinMax) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t mine = lane <= first ? (uint32_t)v : 0u;
+        excl += (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp<false>(mine), 63);
+        if (first < 64u) break;
+    }
+    if (lane == 0)
+        __hip_atomic_store(lb + b, kLbIncl | (uint64_t)(excl + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 // FM (filter mode): kDupPlain every pair; kDupMark every pair, those behind
 // their bin's cut (ftab, the cut table) marked with kBehindFlag; kDupFront the
 // front pairs (filtered_count; the block's offsets are then scanned from
 // launch_front_count's sums); kDupBehind the fallback lists' pairs (ftab: the
 // open bins' cuts, one splat per lane).
-template <int FM>
+// LB (kDupFront): the block's offset by look-back (lookback_prefix; lb: nb
+// status words and the ticket), no scan of counts before; the block numbered
+// last stores the front pairs' count into np_out; a block whose pairs would
+// pass cap writes none.
+template <int FM, bool LB = false>
 __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc src, uint32_t n,
                                                                      const uint64_t* __restrict__ partials,
                                                                      const uint32_t* __restrict__ order,
@@ -430,25 +545,49 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                                                      uint32_t* __restrict__ vals,
                                                                      const uint32_t* __restrict__ npairs,
                                                                      PassCounts pc, const uint32_t* __restrict__ fcut,
-                                                                     uint32_t nbins) {
+                                                                     uint32_t nbins, uint64_t* __restrict__ lb = nullptr,
+                                                                     uint32_t* np_out = nullptr,  // (may be npairs)
+                                                                     uint32_t cap = 0u) {
     if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
     __shared__ uint32_t tmp[kDupThreads / 64];
+    __shared__ uint32_t lbs[2];  // (LB) the block's ticket, then its offset
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
     __shared__ uint32_t lh[kDupCountTiles][kSortBins];  // digit counts of the block's first sort tiles
     __shared__ uint32_t mk[kDupThreads / 64][64];        // coop_emit's start marks, per wave
     extern __shared__ uint16_t scut[];                   // (fcut, dynamic: nbins words) the table, min(t, 0xFFFF)
     static_assert(sizeof tmp + sizeof st + sizeof lh + sizeof mk + kDupCutBins * 2 <= kLdsBytes,
                   "scan_duplicate_kernel's LDS (static + the largest cut table) exceeds a gfx950 workgroup's");
-    const uint32_t blk = blockIdx.x * kScanItems, tid = threadIdx.x;
+    const uint32_t nblocks = (n + kScanItems - 1) / kScanItems;
+    uint32_t bid = blockIdx.x;
+    if constexpr (LB) {
+        if (threadIdx.x == 0)
+            lbs[0] = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lb + nblocks), 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        block_lds_sync();
+        bid = lbs[0];
+    }
+    const uint32_t blk = bid * kScanItems, tid = threadIdx.x;
     // every global load of the block up front (clamped, branch-free), before
     // the first pair store: vmcnt counts loads and stores together, so a load
     // issued between stores would wait for them
     // (absent arrays read a stand-in, so no load sits in a branch, where its
     // value would be waited for at once)
-    const uint64_t part = partials[blockIdx.x];
+    uint64_t part = LB ? 0ull : partials[bid];
+    uint32_t rlo[kDupIpt], rhi[kDupIpt], dk[kDupIpt], ord[kDupIpt];
+#if GS_BUF_LOADS  // (A/B: raw buffer loads, reads past n return 0; those items get the empty rect below)
+    const BufU32 blo(src.lo, blk, n, kScanItems), bhi(src.hi, blk, n, kScanItems),
+        bdk(dkey ? dkey : src.lo, blk, n, kScanItems), bord(order ? order : src.lo, blk, n, kScanItems);
+#pragma unroll
+    for (int k = 0; k < kDupIpt; ++k) {
+        const uint32_t i = k * kDupThreads + tid;
+        rlo[k] = blo[i];
+        rhi[k] = bhi[i];
+        dk[k] = bdk[i];
+        ord[k] = bord[i];
+    }
+#else
     const uint32_t* dsrc = dkey ? dkey : src.lo;
     const uint32_t* osrc = order ? order : src.lo;
-    uint32_t rlo[kDupIpt], rhi[kDupIpt], dk[kDupIpt], ord[kDupIpt];
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t j = min(blk + k * kDupThreads + tid, n - 1u);
@@ -457,10 +596,12 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
         dk[k] = dsrc[j];
         ord[k] = osrc[j];
     }
+#endif
     if (FM != kDupPlain) stage_tab16(fcut, nbins, scut);  // (a depth key is < 2^15: min(t, 0xFFFF) keeps every comparison)
     if (pc.C)
         for (uint32_t i = tid; i < kDupCountTiles * kSortBins; i += kDupThreads) (&lh[0][0])[i] = 0u;
     if (FM >= kDupFront) block_lds_sync();  // (the counts below read the table)
+    uint32_t finc[kDupIpt];  // (kDupFront) a small rect's kept bins, reused by the emission
 #pragma unroll
     for (int k = 0; k < kDupIpt; ++k) {
         const uint32_t i = k * kDupThreads + tid;
@@ -468,8 +609,24 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             rlo[k] = kEmptyRectLo;
             rhi[k] = 0u;
         }
-        st[pad32(i)] = FM >= kDupFront ? filtered_count<FM>(rlo[k], rhi[k], src.masked, dk[k], tiles_x, scut)
-                                       : rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        finc[k] = 0u;
+        uint32_t c;
+        if constexpr (FM == kDupFront) {
+            const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);
+            if (r.empty) {
+                c = 0u;
+            } else if (small_rect(r)) {
+                finc[k] = filter_inc16<false>(rect_inc16(r), r, tiles_x, scut, dk[k]);
+                c = (uint32_t)__builtin_popcount(finc[k]);
+            } else {
+                c = (r.bx1 - r.bx0 + 1u) * (r.by1 - r.by0 + 1u);  // (no excluded bins)
+            }
+        } else if constexpr (FM == kDupBehind) {
+            c = filtered_count<FM>(rlo[k], rhi[k], src.masked, dk[k], tiles_x, nbins, scut);
+        } else {
+            c = rect_tile_count(rlo[k], rhi[k], src.own, src.masked);
+        }
+        st[pad32(i)] = c;
     }
     block_lds_sync();
     uint32_t v[kDupIpt];
@@ -481,6 +638,18 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
     }
     uint32_t t;
     const uint32_t ex = block_dup_exclusive_scan(s, tmp, &t);  // (ends with a barrier)
+    if constexpr (LB) {
+        if (tid < 64u) {
+            const uint32_t e = lookback_prefix(lb, bid, t);
+            if (tid == 0) {
+                lbs[1] = e;
+                if (bid == nblocks - 1u) *np_out = e + t;  // (every block has read *npairs before its status)
+            }
+        }
+        block_lds_sync();
+        part = lbs[1];
+        if (part + t > cap) return;  // (only after a spin gave up: the frame's count then differs from P)
+    }
     {
         uint32_t run = (uint32_t)part + ex;
 #pragma unroll
@@ -525,7 +694,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             const BinRect r = bin_rect(rlo[k], rhi[k], src.masked);  // (items past n: the empty rect)
             uint32_t inc, c;
             if (FM == kDupFront && small_rect(r)) {  // (its kept bins; a larger rect emits every bin, marked)
-                inc = j < n && !r.empty ? filter_inc16<false>(rect_inc16(r), r, tiles_x, scut, dk[k]) : 0u;
+                inc = finc[k];
                 c = (uint32_t)__builtin_popcount(inc);
             } else {
                 inc = r.excl ? rect_inc16(r) : 0u;
@@ -707,10 +876,11 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
-                                      hipEvent_t done, unsigned long long seq, bool front) {
-    if (!part) return hipErrorInvalidValue;
+                                      hipEvent_t done, unsigned long long seq, bool front, bool lookback) {
+    if (!part || (lookback && !front)) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
-                          total, seg_sample, npairs, cap, part, seq, front ? 3u : 0u, nullptr, nullptr);
+                          total, seg_sample, npairs, cap, part, seq, lookback ? kPartLookback : front ? 3u : 0u,
+                          nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -723,8 +893,8 @@ hipError_t launch_front_count(const uint32_t* rect_lo, const uint32_t* rect_hi, 
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     if (!cut || !out || nbins > kDupCutBins) return hipErrorInvalidValue;
-    filtered_count_kernel<kDupFront><<<nb, 1024, tab_lds(nbins), st>>>(rect_lo, rect_hi, dkey, n, masked, tiles_x, cut,
-                                                                       nbins, out, nullptr, nullptr);
+    filtered_count_kernel<kDupFront><<<min(nb, (uint32_t)kCountGrid), 1024, tab_lds(nbins), st>>>(
+        rect_lo, rect_hi, dkey, n, masked, tiles_x, cut, nbins, out, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -738,7 +908,7 @@ hipError_t launch_fallback_pairs(const uint32_t* rect_lo, const uint32_t* rect_h
         return hipErrorInvalidValue;
     // per-block pair counts and items with pairs (the scan's two rows), their
     // scan into npairs / kept (only with an open quadrant), then the pairs
-    filtered_count_kernel<kDupBehind><<<nb, 1024, tab_lds(nbins), st>>>(
+    filtered_count_kernel<kDupBehind><<<min(nb, (uint32_t)kCountGrid), 1024, tab_lds(nbins), st>>>(
         rect_lo, rect_hi, dkey, n, masked, tiles_x, table, nbins, reinterpret_cast<unsigned long long*>(part),
         reinterpret_cast<unsigned long long*>(part) + nb, open);
     scan_partials_kernel<<<1, kPartThreads, 0, st>>>(part, nb, total, nullptr, npairs, cap, nullptr, 0ull, 0u, open,
@@ -753,7 +923,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
                                  const uint64_t* partials, uint32_t n, uint32_t tiles_x, RowOwnership own, bool masked,
                                  const uint32_t* dkey, int bin_bits, uint32_t* keys, uint32_t* vals,
                                  const uint32_t* npairs, hipStream_t st, uint32_t* offsets, PassCounts pc,
-                                 const uint32_t* fcut, uint32_t nbins, bool front) {
+                                 const uint32_t* fcut, uint32_t nbins, bool front, uint32_t* np_out, uint32_t cap) {
     const uint32_t nb = (n + kScanItems - 1) / kScanItems;
     if (nb == 0) return hipSuccess;
     // (order: dkey holds the items' depth keys in that order)
@@ -779,7 +949,12 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     // (the cut table sized to the frame: a block that fits beside the previous
     // composite's workgroups starts sooner)
     const size_t lds = fcut ? tab_lds(nbins) : 0;
-    if (front)
+    if (np_out && !front) return hipErrorInvalidValue;
+    if (front && np_out)  // (offsets by look-back: partials holds nb + 1 cleared words)
+        scan_duplicate_kernel<kDupFront, true><<<nb, kDupThreads, lds, st>>>(
+            src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals, npairs, pc, fcut, nbins,
+            const_cast<uint64_t*>(partials), np_out, cap);
+    else if (front)
         scan_duplicate_kernel<kDupFront><<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
                                                                        keys, vals, npairs, pc, fcut, nbins);
     else if (fcut)

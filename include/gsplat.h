@@ -121,7 +121,9 @@ typedef struct gs_stats {
     int32_t binning;       /* order the last frame's bin lists were built in: GS_BINNING_DEPTH_FIRST
                               (ms_depth_sort = global depth sort) or GS_BINNING_BIN_FIRST
                               (ms_depth_sort = per-bin depth sort after the bin sort) */
-    int32_t reserved_stats;
+    int32_t front_only;    /* 1: a depth-cut frame whose duplicate wrote only its front pairs (the
+                              pairs at or ahead of their bin's cut; the fallback lists' pairs were
+                              regenerated from the splats when a quadrant stayed open), DESIGN.md §4 */
     /* records the composite's workgroups fetched (each of a 32-px bin's four
        16x16 tiles reads the bin's list itself; a tile stops fetching once its
        pixels saturate): the basis of bytes_composite = 8 B per workgroup +

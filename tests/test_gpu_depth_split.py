@@ -118,6 +118,8 @@ def test_depth_cuts_still_camera_saves_pairs(built, binning):
     st = cut.last_stats()
     assert st["pairs_sorted"] < 0.6 * st["pairs"], st
     assert st["open_tiles"] == 0, st
+    # bin-first frames with cuts write only their front pairs
+    assert st["front_only"] == (1 if binning == "bin_first" else 0), st
 
 
 @pytest.mark.parametrize("binning", ["bin_first", "depth_first"])
@@ -135,12 +137,18 @@ def test_depth_cuts_jump_opens_tiles(built, binning):
     near = default_camera(W, H)
     near.setDistance(2.0)
     near.orbit(0.4, 0.1)
-    opened = 0
+    opened = front_opened = 0
     for cam in (far, far, far, near, near, far, near):
         V, P = cam.getViewMatrix(), cam.getProjectionMatrix()
         assert _bits(cut.render_host(V, P, W, H), whole.render_host(V, P, W, H)) == 0
-        opened += cut.last_stats()["open_tiles"]
+        st = cut.last_stats()
+        opened += st["open_tiles"]
+        # (a front-only frame that leaves tiles open: the fallback pairs were
+        # regenerated from the splats' rects, launch_fallback_pairs)
+        front_opened += st["open_tiles"] if st["front_only"] else 0
     assert opened > 0
+    if binning == "bin_first":
+        assert front_opened > 0
 
 
 def test_depth_cuts_bgra8_and_resolution_change(built):

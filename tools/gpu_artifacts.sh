@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/art; mkdir -p $O
 step() { name=$1; shift; echo "== $name"; "$@"; rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-for s in ${STEPS:-tests driver bench prof pmc configs heavy orbit ranks timeline}; do case $s in
+for s in ${STEPS:-tests driver bench prof pmc configs heavy orbit ranks timeline scaling}; do case $s in
 driver) step driver bash -c "timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_command.json 2> $O/bench_driver_command.err"
        python -c "import json;d=json.load(open('$O/bench_driver_command.json'));print('driver', d['ms_per_step'], d['settled']['ms_per_step'], d['orbit']['ms_per_step'], d['roofline']['frac'], d['roofline']['kernels']['composite']['ms'])" ;;
 tests) step tests bash -c "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
@@ -45,6 +45,12 @@ rows50m) step rows50m bash -c "timeout -k 10 900 python tools/rows_probe.py --sp
        tail -5 $O/rows_probe_50m.err ;;
 rows4k) step rows4k bash -c "timeout -k 10 600 python tools/rows_probe.py --splats 6000000 --width 3840 --height 2160 --sh 3 > $O/rows_probe_virtual_ranks_4k.json 2> $O/rows_probe_4k.err"
        tail -5 $O/rows_probe_4k.err ;;
-ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
-       cat $O/rehearsal_2rank_gloo.json ;;
+ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --launcher ranks --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
+       cat $O/rehearsal_2rank_gloo.json
+       # the one-process launcher (bench.py's default outside torchrun) through the group's RCCL
+       # branches, on device 0 with the test stub of the RCCL entry points
+       step group bash -c "GS_BENCH_SAME_DEVICE=1 GS_RCCL_LIB=$PWD/tests/cpp/librccl_stub.so timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 3 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_group_stub.json 2> $O/rehearsal_2rank_group_stub.err"
+       cat $O/rehearsal_2rank_group_stub.json ;;
+scaling) step scaling bash tools/gpu_scaling.sh
+       mkdir -p $O/scaling && cp gpurun_out/scaling/* $O/scaling/ ;;
 esac; done
