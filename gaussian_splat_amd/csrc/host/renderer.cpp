@@ -68,6 +68,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_DUP_FRONT  // A/B knob: 1 = a bin-first depth-cut frame emits only its front pairs (launch_front_count)
 #define GS_DUP_FRONT 1
 #endif
+#ifndef GS_DUP_FRONT_DILATED  // A/B knob: 1 = front-only emission also while the set's cuts are dilated (moving camera)
+#define GS_DUP_FRONT_DILATED 0
+#endif
 #ifndef GS_DUP_LOOKBACK  // A/B knob: 1 = the front-only duplicate finds its offsets by look-back (no count kernel)
 #define GS_DUP_LOOKBACK 1
 #endif
@@ -1701,7 +1704,8 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             // (not while the set's cuts are dilated: a moving camera leaves
             // quadrants open, and regenerating their fallback pairs from every
             // splat's rect costs more than the whole pairs' sort pass it saves)
-            h->fused_prep.front = GS_DUP_FRONT && h->cut_in && h->cut_r[h->set] == 0 && T <= gs::kDupCutBins &&
+            h->fused_prep.front = GS_DUP_FRONT && h->cut_in && (GS_DUP_FRONT_DILATED || h->cut_r[h->set] == 0) &&
+                                  T <= gs::kDupCutBins &&
                                   list_key_bits(U) + gs::kDepthBits <= 31;
             h->fused_prep.pc.cut = h->cut_in;  // (with cuts: the duplicate counts only the pairs the filter keeps)
 #if !GS_DUP_FILTER_COUNT
