@@ -29,9 +29,9 @@ over the same K frames and report both in `schemes`:
          (--pipeline-rows 1): frame k's all-to-all under frame k-1's render
   bands  SURVEY §8(e)'s fallback: the scene REPLICATED on every rank, each
          renders its own bin rows, band gather; no exchange
-The headline rule (stated identically in DESIGN.md §6e and README): `value`
-is the rows scheme's whenever rows is at least as fast as bands at this world
-size; otherwise bands', named as the replicated scheme in
+The headline rule (stated identically in DESIGN.md §6 and README):
+`value` is the rows scheme's whenever rows is at least as fast as bands at
+that world size; otherwise it is bands', named as the replicated scheme in
 `config.parallelism` and `scheme_choice`.  Rows are link-bound at 2 ranks
 (about half of every rank's records cross the one xGMI link between them).
 The north star's depth slabs + transmittance all_gather + RGBA reduce
@@ -157,7 +157,7 @@ def spawn_ranks(args) -> int:
 
 
 def headline(schemes, order):
-    """The headline scheme (DESIGN.md §6e, README, this module's docstring):
+    """The headline scheme (DESIGN.md §6, README, this module's docstring):
     rows, the north star's splat-index sharding, whenever it is at least as
     fast as the replicated-scene bands at this world size; else bands."""
     exact = [k for k in ("rows", "bands") if k in schemes]
