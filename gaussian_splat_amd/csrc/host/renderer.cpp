@@ -71,6 +71,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_DUP_FRONT_DILATED  // A/B knob: 1 = front-only emission also while the set's cuts are dilated (moving camera)
 #define GS_DUP_FRONT_DILATED 0
 #endif
+#ifndef GS_AUX_TOTALS  // A/B knob: 1 = a look-back frame's totals kernel runs on a stream of its own, beside the duplicate
+#define GS_AUX_TOTALS 1
+#endif
 #ifndef GS_DUP_LOOKBACK  // A/B knob: 1 = the front-only duplicate finds its offsets by look-back (no count kernel)
 #define GS_DUP_LOOKBACK 1
 #endif
@@ -158,6 +161,8 @@ struct gs_handle {
     int stats_set = -1;                 // buffer set of the frame in `stats` (its fetch counter)
     int64_t stats_fixed_bytes = 0;      // composite bytes besides the records: range words + output
     hipEvent_t totals_ev = nullptr;     // P is in host_total
+    hipStream_t aux = nullptr;          // (GS_AUX_TOTALS) a look-back frame's totals kernel
+    hipEvent_t pre_ev = nullptr;        // recorded by that frame's preprocess dispatch
     unsigned long long totals_seq = 0;  // (GS_HOST_POLL) the last totals kernel's sequence number, host_total[5]
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
         int32_t w = 0, h = 0;
@@ -173,6 +178,7 @@ struct gs_handle {
     struct ListPrep {
         bool ok = false;
         bool front = false;  // the frame emits only its front pairs (launch_front_count; depth cuts)
+        bool aux = false;    // (look-back) its totals kernel on the aux stream, after the preprocess's pre_ev
         uint32_t cap = 0;
         gs::PassCounts pc;
     } fused_prep;
@@ -276,6 +282,8 @@ struct gs_handle {
         if (side) (void)hipStreamDestroy(side);
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
         if (totals_ev) (void)hipEventDestroy(totals_ev);
+        if (pre_ev) (void)hipEventDestroy(pre_ev);
+        if (aux) (void)hipStreamDestroy(aux);
         for (auto& e : set_free)
             if (e) (void)hipEventDestroy(e);
         if (host_total) (void)hipHostFree(host_total);
@@ -740,9 +748,19 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         if (front && !lookb)  // the front pairs' block sums into ppart's fourth row
             GS_HIP(gs::launch_front_count(rect_lo, rect_hi, carry_dkey, m, U.cell_mask != 0, (uint32_t)U.tiles_x,
                                           h->cut_in, T, h->ppart.as<unsigned long long>() + (size_t)3 * nb, st));
-        GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), nb, h->partials.as<uint64_t>(),
-                                              h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
-                                              st, tev, seq, front, lookb));
+        if (lookb && lp.aux) {
+            // the totals alone, for the host, on the aux stream beside the
+            // duplicate (which needs none of them: the preprocess cleared its
+            // statuses); the host waits for them before the next frame's
+            // preprocess is queued, which adds into ppart again
+            GS_HIP(hipStreamWaitEvent(h->aux, h->pre_ev, 0));
+            GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), nb, nullptr, h->dev_total,
+                                                  nullptr, nullptr, cap, h->aux, tev, seq, front, lookb));
+        } else {
+            GS_HIP(gs::launch_scan_partials_fused(h->ppart.as<unsigned long long>(), nb, h->partials.as<uint64_t>(),
+                                                  h->dev_total, h->seg_sample.as<uint32_t>() + 2 * h->set, np, cap,
+                                                  st, tev, seq, front, lookb));
+        }
         h->ppart_dirty = false;
     } else {
         GS_HIP(gs::launch_tile_count_totals(rect_lo, rect_hi, m, own.dev, U.cell_mask != 0, h->partials.as<uint64_t>(),
@@ -819,6 +837,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
         // into the counters cleared below, so it drains first too.
         GS_HIP(hipStreamSynchronize(st));
         if (tail && tail_st && tail_st != st) GS_HIP(hipStreamSynchronize(tail_st));
+        if (lp.aux) GS_HIP(hipStreamSynchronize(h->aux));
         // (the no-op tail's cut_finalize published an open-quadrant count of
         // a composite that never ran: discard it, the re-queued tail writes
         // the real one for the dilation controller)
@@ -1546,6 +1565,8 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
     const char* sp_env = std::getenv("GS_SIDE_PRIORITY");
     const bool high = !(sp_env && sp_env[0] == '0');
     GS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, high ? greatest : 0));
+    GS_HIP(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, high ? greatest : 0));
+    GS_HIP(hipEventCreateWithFlags(&h->pre_ev, hipEventDisableTiming));
     GS_HIP(hipEventCreateWithFlags(&h->sorted_ev, hipEventDisableTiming));
     for (auto& e : h->set_free) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->initialized = true;
@@ -1713,6 +1734,14 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
 #endif
             fuse.zero = h->fused_prep.pc.C;
             fuse.nzero = h->fused_prep.pc.C ? (h->fused_prep.pc.mask + 1) * h->fused_prep.pc.ntiles : 0u;
+            // (look-back frames: the preprocess clears the duplicate's statuses
+            // and ticket, so its totals kernel can run beside the duplicate;
+            // not while the preprocess's dispatch carries timing events)
+            h->fused_prep.aux = GS_AUX_TOTALS && GS_DUP_LOOKBACK && h->fused_prep.front && !kernel_event(h, 1);
+            if (h->fused_prep.aux) {
+                fuse.zero64 = reinterpret_cast<unsigned long long*>(h->partials.as<uint64_t>());
+                fuse.nzero64 = nb + 1;
+            }
             h->fused_prep.ok = true;
             h->ppart_dirty = true;  // (until its scan is queued)
         }
@@ -1720,7 +1749,7 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
     if (!cut_frame && (s = setup_cuts(h, U, false, st, sp)) != GS_OK) return s;
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), sp, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h), fuse));
+                                 h->fused_prep.aux ? h->pre_ev : kernel_event(h, 1), fetch_counter(h), fuse));
     mark(h, 1, sp);
     if ((s = bin_sort_composite(h, (uint32_t)h->n, h->dkey.as<uint32_t>(), h->rlo.as<uint32_t>(),
                                 h->rhi.as<uint32_t>(), h->rec.as<float4>(), gs::kRecFloat4, U, compact,

@@ -35,6 +35,8 @@ struct PreFuse {
     uint32_t nfill = 0;
     uint32_t* zero = nullptr;
     uint32_t nzero = 0;
+    unsigned long long* zero64 = nullptr;  // (look-back statuses, launch_scan_duplicate np_out)
+    uint32_t nzero64 = 0;
 };
 // Row-scheme projections (gs_shard_project): the preprocess also writes each
 // splat's destination mask (the ranks owning a bin row its rect touches) and
@@ -86,7 +88,10 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // cannot hold them all (the fallback lists may need them).
 // lookback (with front): no front sums; partials[0..nb] (nb + 1 words) are
 // cleared for the duplicate's look-back, total[0] = 0 and npairs = 1 (the
-// duplicate stores the front pairs' count there), or 0 as above.
+// duplicate stores the front pairs' count there), or 0 as above.  partials
+// and npairs may then be null (the totals alone, on a stream of their own
+// beside the duplicate: the preprocess cleared the statuses, PreFuse::zero64;
+// seg_sample null too: total[2..3] = 0, no sample).
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
                                       hipEvent_t done = nullptr, unsigned long long seq = 0, bool front = false,

@@ -391,6 +391,7 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
         const uint32_t g = blockIdx.x * 256u + threadIdx.x;
         for (uint32_t z = g; z < fuse.nfill; z += gridDim.x * 256u) fuse.fill[z] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
         for (uint32_t z = g; z < fuse.nzero; z += gridDim.x * 256u) fuse.zero[z] = 0u;
+        for (uint32_t z = g; z < fuse.nzero64; z += gridDim.x * 256u) fuse.zero64[z] = 0ull;
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t b = blockIdx.x / (uint32_t)(kScanItems / 256);
@@ -412,6 +413,8 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
         if (fuse.nfill && hipMemsetAsync(fuse.fill, 0xFF, (size_t)fuse.nfill * sizeof(uint2), st) != hipSuccess)
             return hipGetLastError();
         if (fuse.nzero && hipMemsetAsync(fuse.zero, 0, (size_t)fuse.nzero * 4, st) != hipSuccess)
+            return hipGetLastError();
+        if (fuse.nzero64 && hipMemsetAsync(fuse.zero64, 0, (size_t)fuse.nzero64 * 8, st) != hipSuccess)
             return hipGetLastError();
     }
     if (s.n == 0) {

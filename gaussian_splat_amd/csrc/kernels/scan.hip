@@ -156,17 +156,18 @@ __global__ __launch_bounds__(kPartThreads) void scan_partials_kernel(uint64_t* _
         uint64_t run = carry + block1024_exclusive_scan<uint64_t>(s, tmp, &t);
 #pragma unroll
         for (int k = 0; k < kPartIpt; ++k) {
-            if (i0 + k < nb) partials[i0 + k] = run;  // (look-back: 0, every block's status cleared)
+            if (i0 + k < nb && partials) partials[i0 + k] = run;  // (look-back: 0, every block's status cleared)
             run += v[k];
         }
         carry += t;
     }
-    if (prow == kPartLookback && threadIdx.x == 0) partials[nb] = 0u;  // (the duplicate's block ticket)
+    if (prow == kPartLookback && partials && threadIdx.x == 0) partials[nb] = 0u;  // (the duplicate's block ticket)
     uint64_t vt, wt = 0, at = carry;
     block1024_exclusive_scan<uint64_t>(vis, tmp, &vt);
     if (src) block1024_exclusive_scan<uint64_t>(wmax, tmp, &wt);
     if (src && prow) block1024_exclusive_scan<uint64_t>(all, tmp, &at);
     if (threadIdx.x == 0) {
+        if (!seg_sample && !partials) total[2] = total[3] = 0u;  // (totals only: no sample this frame)
         total[0] = carry;
         total[1] = vt;
         total[4] = wt;
@@ -548,7 +549,9 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
                                                                      uint32_t nbins, uint64_t* __restrict__ lb = nullptr,
                                                                      uint32_t* np_out = nullptr,  // (may be npairs)
                                                                      uint32_t cap = 0u) {
-    if (*npairs == 0u) return;  // no pairs, or more than the buffers hold (the host re-runs)
+    // no pairs, or more than the buffers hold (the host re-runs); (LB: no
+    // guard, the capacity test below keeps every store in the buffers)
+    if (!LB && *npairs == 0u) return;
     __shared__ uint32_t tmp[kDupThreads / 64];
     __shared__ uint32_t lbs[2];  // (LB) the block's ticket, then its offset
     __shared__ uint32_t st[kScanItems + kScanItems / 32];
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(kDupThreads) void scan_duplicate_kernel(CountSrc sr
             const uint32_t e = lookback_prefix(lb, bid, t);
             if (tid == 0) {
                 lbs[1] = e;
-                if (bid == nblocks - 1u) *np_out = e + t;  // (every block has read *npairs before its status)
+                if (bid == nblocks - 1u) *np_out = e + t <= cap ? e + t : 0u;  // (the sort's count)
             }
         }
         block_lds_sync();
