@@ -74,6 +74,9 @@ gs_status fail(gs_status s, const std::string& msg) {
 #ifndef GS_AUX_TOTALS  // A/B knob: 1 = a look-back frame's totals kernel runs on a stream of its own, beside the duplicate
 #define GS_AUX_TOTALS 1
 #endif
+#ifndef GS_AUX_ALL  // A/B knob: 1 = every depth-cut frame (not only front-only ones) gets look-back + aux totals
+#define GS_AUX_ALL 0
+#endif
 #ifndef GS_DUP_LOOKBACK  // A/B knob: 1 = the front-only duplicate finds its offsets by look-back (no count kernel)
 #define GS_DUP_LOOKBACK 1
 #endif
@@ -738,7 +741,8 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     h->front_last = front;
     // (front-only, GS_DUP_LOOKBACK: no count kernel; the duplicate's blocks
     // count their front pairs and find their offsets by look-back)
-    const bool lookb = front && GS_DUP_LOOKBACK;
+    // (and every depth-cut frame whose totals run beside the duplicate, lp.aux)
+    const bool lookb = fused && GS_DUP_LOOKBACK && (front || lp.aux);
     // the host learns P by polling the totals kernel's sequence word in
     // host-mapped memory (GS_HOST_POLL) or by an event in its dispatch packet
     const unsigned long long seq = GS_HOST_POLL ? ++h->totals_seq : 0ull;
@@ -818,7 +822,9 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     // P: the pairs the duplicate writes; P_all: every pair of the frame (the
     // same unless front-only; the pair buffers hold P_all, so that the
     // fallback lists always fit)
-    const uint64_t P = h->host_total[0], P_all = h->host_total[8];
+    // (look-back: total[0] is not scanned; a frame that is not front-only
+    // writes every pair)
+    const uint64_t P_all = h->host_total[8], P = lookb && !front ? P_all : h->host_total[0];
     h->stats.visible = (int64_t)h->host_total[1];
     if (fused && P_all > 0) {  // the duplicate's wave-max work (PreFuse), for the binning-order model
         h->order.wmax = h->host_total[4];
@@ -862,7 +868,7 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
     }
     h->stats.sort_bits = bits;
     h->stats.sort_passes = gs::make_sort_plan(bits).passes;
-    h->pairs_emitted = lookb ? gs_handle::kEmittedOnDevice : P;
+    h->pairs_emitted = lookb && front ? gs_handle::kEmittedOnDevice : P;
     *pairs = P_all;
     return GS_OK;
 }
@@ -1737,7 +1743,11 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
             // (look-back frames: the preprocess clears the duplicate's statuses
             // and ticket, so its totals kernel can run beside the duplicate;
             // not while the preprocess's dispatch carries timing events)
-            h->fused_prep.aux = GS_AUX_TOTALS && GS_DUP_LOOKBACK && h->fused_prep.front && !kernel_event(h, 1);
+            // (depth-cut frames only: the aux totals carry no per-bin sort
+            // sample, which only frames without cuts use)
+            h->fused_prep.aux = GS_AUX_TOTALS && GS_DUP_LOOKBACK && cut_frame && h->cut_in && !kernel_event(h, 1) &&
+                                (h->fused_prep.front || (GS_AUX_ALL && T <= gs::kDupCutBins &&
+                                                         list_key_bits(U) + gs::kDepthBits <= 31));
             if (h->fused_prep.aux) {
                 fuse.zero64 = reinterpret_cast<unsigned long long*>(h->partials.as<uint64_t>());
                 fuse.nzero64 = nb + 1;

@@ -86,7 +86,7 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 // after the three atomic rows), total[0] = the front pairs; total[8] = every
 // pair of the frame (row 0) either way, and npairs is 0 when the pair buffers
 // cannot hold them all (the fallback lists may need them).
-// lookback (with front): no front sums; partials[0..nb] (nb + 1 words) are
+// lookback (front-only or not): no offsets; partials[0..nb] (nb + 1 words) are
 // cleared for the duplicate's look-back, total[0] = 0 and npairs = 1 (the
 // duplicate stores the front pairs' count there), or 0 as above.  partials
 // and npairs may then be null (the totals alone, on a stream of their own

@@ -880,7 +880,7 @@ hipError_t launch_tile_count_totals(const uint32_t* rect_lo, const uint32_t* rec
 hipError_t launch_scan_partials_fused(unsigned long long* part, uint32_t nb, uint64_t* partials, uint64_t* total,
                                       uint32_t* seg_sample, uint32_t* npairs, uint64_t cap, hipStream_t st,
                                       hipEvent_t done, unsigned long long seq, bool front, bool lookback) {
-    if (!part || (lookback && !front)) return hipErrorInvalidValue;
+    if (!part) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kPartThreads), 0, st, nullptr, done, 0, partials, nb,
                           total, seg_sample, npairs, cap, part, seq, lookback ? kPartLookback : front ? 3u : 0u,
                           nullptr, nullptr);
@@ -933,6 +933,7 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     if (dkey && bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     const CountSrc src{rect_lo, rect_hi, own, masked};
     // (the marks: index order, the cooperative emission, the flag above the depth key)
+    if (np_out && (order || own.owner)) return hipErrorInvalidValue;  // (look-back: index order, every row owned)
     if ((fcut || front) &&
         (!fcut || order || own.owner || !GS_DUP_COOP || !dkey || nbins > kDupCutBins || bin_bits + kDepthBits > 31))
         return hipErrorInvalidValue;
@@ -952,12 +953,18 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
     // (the cut table sized to the frame: a block that fits beside the previous
     // composite's workgroups starts sooner)
     const size_t lds = fcut ? tab_lds(nbins) : 0;
-    if (np_out && !front) return hipErrorInvalidValue;
-    if (front && np_out)  // (offsets by look-back: partials holds nb + 1 cleared words)
-        scan_duplicate_kernel<kDupFront, true><<<nb, kDupThreads, lds, st>>>(
-            src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals, npairs, pc, fcut, nbins,
-            const_cast<uint64_t*>(partials), np_out, cap);
-    else if (front)
+    if (np_out) {  // (offsets by look-back: partials holds nb + 1 cleared words)
+        uint64_t* lb = const_cast<uint64_t*>(partials);
+        if (front)
+            scan_duplicate_kernel<kDupFront, true><<<nb, kDupThreads, lds, st>>>(
+                src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals, npairs, pc, fcut, nbins, lb, np_out, cap);
+        else if (fcut)
+            scan_duplicate_kernel<kDupMark, true><<<nb, kDupThreads, lds, st>>>(
+                src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals, npairs, pc, fcut, nbins, lb, np_out, cap);
+        else
+            scan_duplicate_kernel<kDupPlain, true><<<nb, kDupThreads, lds, st>>>(
+                src, n, partials, order, dkey, bin_bits, tiles_x, keys, vals, npairs, pc, fcut, nbins, lb, np_out, cap);
+    } else if (front)
         scan_duplicate_kernel<kDupFront><<<nb, kDupThreads, lds, st>>>(src, n, partials, order, dkey, bin_bits, tiles_x,
                                                                        keys, vals, npairs, pc, fcut, nbins);
     else if (fcut)
