@@ -863,6 +863,11 @@ gs_status build_bin_lists(gs_handle* h, uint32_t m, const uint32_t* order, const
 #endif
         if (pc.C) GS_HIP(hipMemsetAsync(pc.C, 0, (size_t)(pc.mask + 1) * pc.ntiles * 4, st));
         if (tail) GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));  // (the no-op frame's composite counted into these)
+        // the bin ranges empty again: the no-op frame's tail may have written
+        // some (a front-only frame's fallback lists are regenerated from the
+        // rects, not from the empty pair arrays), and the re-queued sort's
+        // last pass writes only the bins its lists hold
+        GS_HIP(hipMemsetAsync(h->ranges.ptr, 0xFF, (size_t)T * sizeof(uint2), st));
         GS_HIP(enqueue_lists());
         if ((ts = lists_done()) != GS_OK) return ts;
     }

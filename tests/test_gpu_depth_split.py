@@ -318,3 +318,52 @@ def test_depth_cuts_cut_table_sizes(built, w, h, n, scale):
         opened += st["open_tiles"]
         sorted_lt += int(st["pairs_sorted"] < st["pairs"])
     assert sorted_lt > 0 and opened > 0
+
+
+@pytest.mark.parametrize("fif,scale", [(1, 1.0), (2, 1.0), (1, 3.0), (2, 3.0)])
+def test_front_only_retry_after_zoom_out(built, fif, scale):
+    """Front-only frames (a still camera with cuts: each duplicate block finds
+    its offsets by look-back, the totals run beside it) whose pair count then
+    outgrows the buffers: a zoom-out after several still frames brings the
+    whole scene into view, so the frame's pairs (x2.7) exceed the capacity
+    sized by the last frame's, so its lists
+    are queued again with larger buffers (look-back statuses cleared again),
+    and the frames after it re-grow their cuts.  Every frame is bit-identical
+    to the whole-list frame.  (scale 3: saturated tiles, so the cuts keep
+    part of the lists and the fallback lists run where a quadrant opens.)
+    Round 6 found the re-queued front-only frame wrong before its bin ranges
+    were emptied again (the no-op frame's tail regenerates fallback lists from
+    the rects and writes their ranges)."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd.api import default_camera
+    import torch
+
+    W, H = 800, 450
+    sc = _scene(300000, 23, 0, W / H, scale)
+    views = []
+    for d in (2.2,) * 5 + (6.0,) * 4 + (4.0,) * 3:
+        cam = default_camera(W, H)
+        cam.setDistance(d)
+        views.append((cam.getViewMatrix(), cam.getProjectionMatrix()))
+    ref = InstancedSplatRenderer(sc, Options(crop=False, binning="bin_first", depth_split=False))
+    ref.initialize(0)
+    refs = [ref.render_host(V, P, W, H) for V, P in views]
+    r = InstancedSplatRenderer(sc, Options(crop=False, binning="bin_first", depth_split=True, frames_in_flight=fif))
+    r.initialize(0)
+    pairs, fronts, outs = [], [], []
+    for V, P in views:
+        if fif == 2:
+            outs.append(r.render(V, P, W, H).clone())
+        else:
+            outs.append(r.render_host(V, P, W, H))
+        st = r.last_stats()
+        pairs.append(st["pairs"])
+        fronts.append(st["front_only"])
+    if fif == 2:
+        torch.cuda.synchronize()
+        outs = [o.cpu().numpy() for o in outs]
+    for k, o in enumerate(outs):
+        assert _bits(o, refs[k]) == 0, (k, pairs, fronts)
+    assert sum(fronts[1:5]) >= 3, fronts                      # the still frames emitted their front pairs only
+    grew = [k for k in range(1, len(pairs)) if pairs[k] > 1.2 * pairs[k - 1]]
+    assert grew and any(fronts[k] for k in grew), (pairs, fronts)  # a front-only frame outgrew the buffers
