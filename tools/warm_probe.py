@@ -24,4 +24,7 @@ for b in range(NB):
     for _ in range(B):
         r.render(view, proj, W, H, out=out)
     torch.cuda.synchronize()
-    print(f"block {b:2d} frames {b * B:3d}-{b * B + B - 1:3d}: {(time.perf_counter() - t0) * 1e3 / B:.4f} ms/frame", flush=True)
+    ms = (time.perf_counter() - t0) * 1e3 / B
+    st = r.last_stats()
+    print(f"block {b:2d} frames {b * B:3d}-{b * B + B - 1:3d}: {ms:.4f} ms/frame  front {st['front_only']} "
+          f"dilate {st['cut_dilate']} binning {st['binning']} sorted {st['pairs_sorted']}", flush=True)
