@@ -79,6 +79,7 @@ SIGNATURES = {
     "gs_shard_set_rows": (C.c_int, [_P, _P, C.c_int32]),
     "gs_shard_project": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, C.c_int64, _I64P, _P]),
     "gs_shard_render": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P]),
+    "gs_shard_render_split": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P]),
     "gs_band_render": (C.c_int, [_P, _FP, _FP, C.c_int32, C.c_int32, _P, _P]),
     "gs_exchange_record_bytes": (C.c_int32, []),
     "gs_exchange_regions": (C.c_int32, [C.c_void_p]),

@@ -165,6 +165,11 @@ struct gs_handle {
     int64_t stats_fixed_bytes = 0;      // composite bytes besides the records: range words + output
     hipEvent_t totals_ev = nullptr;     // P is in host_total
     hipStream_t aux = nullptr;          // (GS_AUX_TOTALS) a look-back frame's totals kernel
+    // gs_shard_render_split: the rank render's composite on a stream of its
+    // own; comp_done follows its tail, the next rank render's lists wait for
+    // it; the projection then leaves the fetch counters to the render
+    hipEvent_t comp_done = nullptr;
+    bool split_render = false;
     hipEvent_t pre_ev = nullptr;        // recorded by that frame's preprocess dispatch
     unsigned long long totals_seq = 0;  // (GS_HOST_POLL) the last totals kernel's sequence number, host_total[5]
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
@@ -286,6 +291,7 @@ struct gs_handle {
         if (sorted_ev) (void)hipEventDestroy(sorted_ev);
         if (totals_ev) (void)hipEventDestroy(totals_ev);
         if (pre_ev) (void)hipEventDestroy(pre_ev);
+        if (comp_done) (void)hipEventDestroy(comp_done);
         if (aux) (void)hipStreamDestroy(aux);
         for (auto& e : set_free)
             if (e) (void)hipEventDestroy(e);
@@ -1578,6 +1584,7 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
     GS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, high ? greatest : 0));
     GS_HIP(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, high ? greatest : 0));
     GS_HIP(hipEventCreateWithFlags(&h->pre_ev, hipEventDisableTiming));
+    GS_HIP(hipEventCreateWithFlags(&h->comp_done, hipEventDisableTiming));
     GS_HIP(hipEventCreateWithFlags(&h->sorted_ev, hipEventDisableTiming));
     for (auto& e : h->set_free) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->initialized = true;
@@ -1807,6 +1814,7 @@ gs_status gs_last_stats(gs_handle* h, gs_stats* out) {
         unsigned long long v = 0;
         GS_HIP(hipSetDevice(h->device));
         GS_HIP(hipEventSynchronize(h->set_free[h->stats_set]));
+        if (h->split_render) GS_HIP(hipEventSynchronize(h->comp_done));  // (its composite counts on its own stream)
         GS_HIP(hipMemcpy(&v, h->fetch.as<unsigned long long>() + 2 * h->stats_set, 8, hipMemcpyDeviceToHost));
         h->stats.records_fetched = (int64_t)v;
         h->stats.bytes_composite = h->stats_fixed_bytes + (int64_t)v * (4 + 48);
@@ -2017,6 +2025,9 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     h->band_local = false;  // (a shard frame bins with its owner table; an earlier band frame may have set it)
     begin_frame(h, st);
     gs::ShardFuse sf;
+    // (a split rank render's composite may still count into the fetch
+    // counters: that render clears them itself)
+    unsigned long long* const zero8 = h->split_render ? nullptr : fetch_counter(h);
     if (owner) {
         if ((s = reserve_exchange(h)) != GS_OK) return s;
         sf.owner = owner;
@@ -2028,7 +2039,7 @@ gs_status shard_preprocess(gs_handle* h, const float* view, const float* proj, i
     }
     GS_HIP(gs::launch_preprocess(h->scene_dev(), h->opt.sh_degree, *U, h->rec.as<float4>(), h->dkey.as<uint32_t>(),
                                  h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(), st, kernel_event(h, 0),
-                                 kernel_event(h, 1), fetch_counter(h), gs::PreFuse{}, sf));
+                                 kernel_event(h, 1), zero8, gs::PreFuse{}, sf));
     mark(h, 1, st);
     return GS_OK;
 }
@@ -2077,7 +2088,7 @@ gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, voi
 // Received records -> depth sort -> bin lists -> composite (rows: owned rows
 // into a compact band; slabs: transmittance pass over the full frame).
 gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba, float* slab_t,
-                          hipStream_t st) {
+                          hipStream_t st, const hipStream_t* sc = nullptr) {
     gs_status s = check_ready(h);
     if (s != GS_OK) return s;
     if ((m > 0 && !recv) || m < 0 || m >= (int64_t)UINT32_MAX || !(out_rgba || slab_t) || W <= 0 || H <= 0)
@@ -2096,6 +2107,18 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     const uint32_t* rhi = rlo + m;
     const uint32_t* rkey = rhi + m;
     h->fused_prep.ok = false;
+    // (a composite on its own stream, gs_shard_render_split: this render's
+    // lists overwrite what the last one's composite and tail read, and its
+    // cut setup reads the cuts that tail wrote; its fetch counters, which the
+    // projection clears otherwise, are cleared here, behind that composite)
+    // (also the first plain render after a split one: its projection left
+    // the counters alone too)
+    const bool was_split = h->split_render;
+    h->split_render = sc != nullptr;
+    if (sc || was_split) {
+        if (hipEventQuery(h->comp_done) != hipSuccess) GS_HIP(hipStreamWaitEvent(st, h->comp_done, 0));
+        GS_HIP(hipMemsetAsync(fetch_counter(h), 0, 16, st));
+    }
     // depth cuts of the owned bins: the cuts and the quadrant
     // records are indexed by global bin, the pixel states by global pixel;
     // the binning order is picked for them
@@ -2106,13 +2129,14 @@ gs_status render_received(gs_handle* h, void* recv, int64_t m, int32_t W, int32_
     h->order_pick = h->opt.mode == GS_MODE_MLAB ? -1 : bin_first_order(h, U, (uint32_t)m, own.nrows, cut_on) ? 1 : 0;
     mark(h, 8, st);
     if ((s = bin_sort_composite(h, (uint32_t)m, rkey, rlo, rhi, rv, gs::kXRecFloat4, U, slab_t ? 0 : 1,
-                                reinterpret_cast<float4*>(out_rgba), nullptr, st, slab_t)) != GS_OK)
+                                reinterpret_cast<float4*>(out_rgba), nullptr, st, slab_t, sc)) != GS_OK)
         return s;
     // stage times span both calls: preprocess (project) ... composite; the
     // exchange between them falls inside the depth-sort interval
     fill_stats(h, (uint64_t)h->stats.pairs, U);
     h->stats.tiles = T;
     GS_HIP(hipEventRecord(h->set_free[h->set], st));
+    if (sc) GS_HIP(hipEventRecord(h->comp_done, *sc));
     return GS_OK;
 }
 
@@ -2149,6 +2173,13 @@ gs_status gs_band_render(gs_handle* h, const float* view, const float* proj, int
     if (!out_band) return fail(GS_ERR_INVALID_ARG, "gs_band_render: null output");
     // (two frames in flight like gs_render when the options ask for them)
     return render_frame(h, view, proj, W, H, out_band, 1, false, stream, true);
+}
+
+gs_status gs_shard_render_split(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,
+                                void* stream, void* composite_stream) {
+    if (!out_rgba) return fail(GS_ERR_INVALID_ARG, "gs_shard_render_split: null output");
+    const hipStream_t sc = static_cast<hipStream_t>(composite_stream);
+    return render_received(h, recv, m, W, H, out_rgba, nullptr, static_cast<hipStream_t>(stream), &sc);
 }
 
 gs_status gs_shard_render(gs_handle* h, void* recv, int64_t m, int32_t W, int32_t H, float* out_rgba,

@@ -217,14 +217,26 @@ class HipShardBackend:
 
         return torch.empty(max(1, nbytes), dtype=torch.uint8, device=self.device)
 
-    def render(self, recv, nrec, width, height):
+    def render(self, recv, nrec, width, height, composite_stream=None):
+        """The band of the received records.  composite_stream (a torch
+        stream): the lists on the current stream, the composite there
+        (gs_shard_render_split), so the next projection on the current stream
+        runs beside it; the band is then complete on composite_stream."""
         import torch
 
         band = torch.empty((band_rows(height, self.world, self.owner), width, 4), dtype=torch.float32,
                            device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        check(lib().gs_shard_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
-                                    C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_shard_render")
+        if composite_stream is not None:
+            check(lib().gs_shard_render_split(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
+                                              C.c_void_p(band.data_ptr()), C.c_void_p(stream),
+                                              C.c_void_p(composite_stream.cuda_stream)), "gs_shard_render_split")
+            if recv.is_cuda:
+                recv.record_stream(composite_stream)  # (read by the composite)
+            band.record_stream(composite_stream)
+        else:
+            check(lib().gs_shard_render(self.r._h, C.c_void_p(recv.data_ptr()), int(nrec), width, height,
+                                        C.c_void_p(band.data_ptr()), C.c_void_p(stream)), "gs_shard_render")
         return band
 
 
@@ -462,6 +474,13 @@ class ShardedRenderer:
         # the next frame's exchange is issued from a stream that waited only
         # for its projection, so it does not queue behind this frame's render
         self._xs = torch.cuda.Stream(dev) if self._cs is not None else None
+        # the render's composite (and the gather behind it) on a stream of its
+        # own, so the next projection runs beside it (gs_shard_render_split;
+        # GS_ROWS_SPLIT=0: one stream, A/B)
+        import os
+
+        split = os.environ.get("GS_ROWS_SPLIT", "1") != "0" and hasattr(backend, "r")
+        self._ccs = torch.cuda.Stream(dev) if self._cs is not None and split else None
         self._inflight = []  # (band, frame) of the last gather, alive until the next frame
 
     def _finish(self, pend, width, height, gather, works=None):
@@ -522,13 +541,19 @@ class ShardedRenderer:
         if self._pending is not None:
             pend, w_, h_, g_ = self._pending
             recv, nrec = pend.wait()
-            band = self.b.render(recv, nrec, w_, h_)
+            band = self.b.render(recv, nrec, w_, h_, **({"composite_stream": self._ccs} if self._ccs else {}))
         with torch.cuda.stream(self._xs):
             self._xs.wait_event(projected)
             nxt = (exchange_start(send, counts, self.b.xregions, self.world, self.xgroup), width, height, gather)
         if nxt[0].recv.is_cuda:
             nxt[0].recv.record_stream(self._cs)  # (received on the exchange stream, read on the rank's)
-        out = self._gather(band, *self._pending[1:], works=works) if self._pending is not None else None
+        out = None
+        if self._pending is not None:
+            if self._ccs is not None:  # (the band is complete on the composite's stream: the gather starts there)
+                with torch.cuda.stream(self._ccs):
+                    out = self._gather(band, *self._pending[1:], works=works)
+            else:
+                out = self._gather(band, *self._pending[1:], works=works)
         del old  # (the previous gather's tensors: its transfers were waited for by the caller's stream)
         self._pending = nxt
         return out
@@ -537,6 +562,8 @@ class ShardedRenderer:
         """The frame's compute (the rank's stream) and the gather's transfers,
         waited for by the caller's stream; the frame is marked in use there."""
         user.wait_stream(self._cs)
+        if self._ccs is not None:
+            user.wait_stream(self._ccs)
         for w in works:
             w.wait()
         if out is not None:

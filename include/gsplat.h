@@ -252,6 +252,15 @@ gs_status gs_shard_project(gs_handle *h, const float view[16], const float proj[
  * wide, fp32 RGBA.  `recv` (device) is read only. */
 gs_status gs_shard_render(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height,
                           float *out_rgba, void *hip_stream);
+/* The same render with its composite on a second stream: the lists (scan,
+ * duplicate, sorts) run on hip_stream, the composite and the depth-cut tail
+ * on composite_stream once the lists are ready, so work the caller queues on
+ * hip_stream next (the next frame's gs_shard_project) runs beside this
+ * composite.  out_rgba is complete on composite_stream; recv must stay valid
+ * until then.  The next render's lists wait for this composite on the device.
+ * (Two frames in flight per rank: DESIGN.md §6e.) */
+gs_status gs_shard_render_split(gs_handle *h, void *recv, int64_t recv_count, int32_t width, int32_t height,
+                                float *out_rgba, void *hip_stream, void *composite_stream);
 
 /* Replicated-scene bands (SURVEY §8(e) fallback).  The handle
  * holds the WHOLE scene (gs_create / gs_create_subset over all splats) and is

@@ -114,6 +114,34 @@ for g in [int(x) for x in a.worlds.split(",")]:
     proj_ms = [float(np.median(x)) for x in times["p"]]
     render_ms = [float(np.median(x)) for x in times["r"]]
     pairs = [int(be.r.last_stats()["pairs"]) for be in bes]
+    # a rank's pipelined compute as ShardedRenderer(pipeline=True) queues it
+    # on its own stream: projection k+1, then the render of frame k, back to
+    # back, with the render's composite on a second stream beside the next
+    # projection (gs_shard_render_split; the exchange and the gather on their
+    # own streams and links are not run here); the received records of the
+    # last frame reused
+    pipe_ms = []
+    if g > 1:
+        cs, ccs = torch.cuda.Stream(), torch.cuda.Stream()
+        held = [rv.clone() for rv in recvs]
+        torch.cuda.synchronize()
+        for be, rv, m in zip(bes, held, nrecs):
+            def step(k, be=be, rv=rv, m=m):
+                with torch.cuda.stream(cs):
+                    be.project(V, P, W, H, slot=k & 1)
+                    be.render(rv, m, W, H, composite_stream=ccs)
+            for k in range(10):
+                step(k)
+            torch.cuda.synchronize()
+            runs = []  # (the median of three runs: the first frames of a rank can hit allocator growth)
+            for _ in range(3):
+                t = time.perf_counter()
+                for k in range(a.frames):
+                    step(k)
+                torch.cuda.synchronize()
+                runs.append((time.perf_counter() - t) * 1e3 / a.frames)
+            pipe_ms.append(float(np.median(runs)))
+        del held
     # bytes: records to every other rank (all_to_all) and the band to rank 0 (gather)
     sent = [sum(c for d, c in enumerate(sends[r][1]) if d != r) * xb for r in range(g)]
     max_peer = [max([c for d, c in enumerate(sends[r][1]) if d != r] or [0]) * xb for r in range(g)]
@@ -127,16 +155,18 @@ for g in [int(x) for x in a.worlds.split(",")]:
     # stream) holds up its next frame: a rank's period is the longer of its
     # compute and its busiest link (to rank 0: the largest per-peer exchange
     # plus the band; rank 0 takes the bands over separate links)
-    pipe = [max(proj_ms[r] + render_ms[r], (max_peer[r] + (band_bytes if r else 0)) / link, band_bytes / link)
-            for r in range(g)]
+    pipe = [max(pipe_ms[r] if pipe_ms else proj_ms[r] + render_ms[r], (max_peer[r] + (band_bytes if r else 0)) / link,
+                band_bytes / link) for r in range(g)]
     res[g] = {"project_ms": [round(x, 4) for x in proj_ms], "render_ms": [round(x, 4) for x in render_ms],
               "compute_max_ms": round(max(p + q for p, q in zip(proj_ms, render_ms)), 4),
+              "pipelined_compute_ms": [round(x, 4) for x in pipe_ms],
               "records_received": nrecs, "pairs": pairs, "bytes_sent": sent, "bytes_max_peer": max_peer,
               "band_bytes": band_bytes,
               "link_model_ms": round(max(model), 4), "pipelined_model_ms": round(max(pipe), 4)}
     print(f"[rows_probe] world {g}: compute max {res[g]['compute_max_ms']:.4f} ms  project "
           f"{[round(x, 3) for x in proj_ms]}  render {[round(x, 3) for x in render_ms]}  sent MB "
-          f"{[round(x / 1e6, 1) for x in sent]}  link model {res[g]['link_model_ms']:.4f} ms  pipelined "
+          f"{[round(x / 1e6, 1) for x in sent]}  pipelined compute {[round(x, 3) for x in pipe_ms]}  "
+          f"link model {res[g]['link_model_ms']:.4f} ms  pipelined "
           f"{res[g]['pipelined_model_ms']:.4f} ms", file=sys.stderr, flush=True)
     if g == a.stages:
         for be, rv, m in zip(bes, recvs, nrecs):
@@ -156,5 +186,7 @@ print(json.dumps({"splats": a.splats, "frame": [W, H], "sh_degree": a.sh,
                            "gs_shard_render (unpack + bin/sort + composite of the owned rows), one frame in flight; "
                            f"exchange and gather bytes recorded, priced by link_model_ms at {a.link_gbs} GB/s per "
                            "link and direction (a model, not a measurement); pipelined_model_ms: two frames in "
-                           "flight, the rank on its own compute stream: max(project + render, largest per-peer exchange + band)"),
+                           "flight, the rank on its own compute stream: max(pipelined_compute (projection k+1 and "
+                           "render k back to back, the composite on a second stream), largest per-peer exchange + "
+                           "band)"),
                   "worlds": res}))
