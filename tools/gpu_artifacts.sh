@@ -45,8 +45,9 @@ rows50m) step rows50m bash -c "timeout -k 10 900 python tools/rows_probe.py --sp
        tail -5 $O/rows_probe_50m.err ;;
 rows4k) step rows4k bash -c "timeout -k 10 600 python tools/rows_probe.py --splats 6000000 --width 3840 --height 2160 --sh 3 > $O/rows_probe_virtual_ranks_4k.json 2> $O/rows_probe_4k.err"
        tail -5 $O/rows_probe_4k.err ;;
-ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --launcher ranks --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.json 2> $O/rehearsal_2rank_gloo.err"
-       cat $O/rehearsal_2rank_gloo.json
+ranks) step ranks bash -c "GS_BENCH_BACKEND=gloo GS_BENCH_SAME_DEVICE=1 timeout -k 10 600 python bench.py --gpus 2 --launcher ranks --steps 5 --warmup 2 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_gloo.log 2> $O/rehearsal_2rank_gloo.err"
+       # (gloo's connection messages share stdout with the JSON line)
+       grep '^{' $O/rehearsal_2rank_gloo.log > $O/rehearsal_2rank_gloo.json; cat $O/rehearsal_2rank_gloo.json
        # the one-process launcher (bench.py's default outside torchrun) through the group's RCCL
        # branches, on device 0 with the test stub of the RCCL entry points
        step group bash -c "GS_BENCH_SAME_DEVICE=1 GS_RCCL_LIB=$PWD/tests/cpp/librccl_stub.so timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 3 --cpu-baseline 0 --pmc 0 > $O/rehearsal_2rank_group_stub.json 2> $O/rehearsal_2rank_group_stub.err"
