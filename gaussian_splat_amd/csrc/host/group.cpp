@@ -639,6 +639,10 @@ gs_status render_slabs(gs_group* g, const float* V, const float* P, int Wd, int 
 
 // ---- two frames in flight, rows scheme (gs_group_render_pipelined) ---------
 
+#ifndef GS_GROUP_SPLIT  // A/B knob: 1 = a pipelined rank render's composite on the rank's gather stream
+#define GS_GROUP_SPLIT 1
+#endif
+
 // The ranks' compute / exchange / gather streams and their events, and (RCCL)
 // a second communicator set for the all-to-all, so that frame k's exchange
 // and frame k-1's gather, issued on different streams, never share a
@@ -820,11 +824,17 @@ gs_status render_rows_pipelined(gs_group* g, const float* V, const float* P, int
                 GG_HIP(hipEventSynchronize(g->r[0].ev_gdone));
             }
             GG_HIP(k.band.reserve(k.dev, bb));
-            gs_status r = gs_shard_render(k.h, k.precv[prev.slot].ptr, prev.nrec[(size_t)d], prev.width, prev.height,
-                                          k.band.as<float>(), k.cs);
+            // (GS_GROUP_SPLIT: the render's composite on the rank's gather
+            // stream, after its last gather and before the next, so the next
+            // projection on the compute stream runs beside it)
+            const hipStream_t cq = GS_GROUP_SPLIT ? k.gs : k.cs;
+            gs_status r = GS_GROUP_SPLIT ? gs_shard_render_split(k.h, k.precv[prev.slot].ptr, prev.nrec[(size_t)d],
+                                                                 prev.width, prev.height, k.band.as<float>(), k.cs, k.gs)
+                                         : gs_shard_render(k.h, k.precv[prev.slot].ptr, prev.nrec[(size_t)d],
+                                                           prev.width, prev.height, k.band.as<float>(), k.cs);
             if (r != GS_OK) return r;
-            GG_HIP(hipEventRecord(k.ev_rdone[prev.slot], k.cs));
-            GG_HIP(hipEventRecord(k.ev_done, k.cs));
+            GG_HIP(hipEventRecord(k.ev_rdone[prev.slot], cq));
+            GG_HIP(hipEventRecord(k.ev_done, cq));
         }
         return GS_OK;
     });
