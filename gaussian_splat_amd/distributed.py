@@ -479,7 +479,7 @@ class ShardedRenderer:
         # GS_ROWS_SPLIT=0: one stream, A/B)
         import os
 
-        split = os.environ.get("GS_ROWS_SPLIT", "1") != "0" and hasattr(backend, "r")
+        split = os.environ.get("GS_ROWS_SPLIT", "1") != "0" and getattr(type(backend), "render", None) is HipShardBackend.render
         self._ccs = torch.cuda.Stream(dev) if self._cs is not None and split else None
         self._inflight = []  # (band, frame) of the last gather, alive until the next frame
 
