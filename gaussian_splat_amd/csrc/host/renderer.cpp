@@ -1697,6 +1697,10 @@ static gs_status render_frame(gs_handle* h, const float* view, const float* proj
         if (GS_HOST_SET_WAIT && pipe) GS_HIP(hipEventSynchronize(h->set_free[h->set]));
         else GS_HIP(hipStreamWaitEvent(sp, h->set_free[h->set], 0));
     }
+    if (h->split_render) {  // (a split rank render's composite may still count into this set's counters)
+        if (hipEventQuery(h->comp_done) != hipSuccess) GS_HIP(hipStreamWaitEvent(sp, h->comp_done, 0));
+        h->split_render = false;
+    }
     if (pipe && !h->last_pipe) {  // the side stream starts after everything the caller's stream holds
         GS_HIP(hipEventRecord(h->sorted_ev, st));
         GS_HIP(hipStreamWaitEvent(sp, h->sorted_ev, 0));
