@@ -170,6 +170,7 @@ struct gs_handle {
     // it; the projection then leaves the fetch counters to the render
     hipEvent_t comp_done = nullptr;
     bool split_render = false;
+    hipEvent_t xcount_ev = nullptr;  // (pack_exchange) the destination counts are in host_xtotal
     hipEvent_t pre_ev = nullptr;        // recorded by that frame's preprocess dispatch
     unsigned long long totals_seq = 0;  // (GS_HOST_POLL) the last totals kernel's sequence number, host_total[5]
     struct OrderModel {                 // inputs of the binning-order choice (bin_first_order)
@@ -292,6 +293,7 @@ struct gs_handle {
         if (totals_ev) (void)hipEventDestroy(totals_ev);
         if (pre_ev) (void)hipEventDestroy(pre_ev);
         if (comp_done) (void)hipEventDestroy(comp_done);
+        if (xcount_ev) (void)hipEventDestroy(xcount_ev);
         if (aux) (void)hipStreamDestroy(aux);
         for (auto& e : set_free)
             if (e) (void)hipEventDestroy(e);
@@ -1585,6 +1587,7 @@ gs_status gs_initialize(gs_handle* h, int32_t device) {
     GS_HIP(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, high ? greatest : 0));
     GS_HIP(hipEventCreateWithFlags(&h->pre_ev, hipEventDisableTiming));
     GS_HIP(hipEventCreateWithFlags(&h->comp_done, hipEventDisableTiming));
+    GS_HIP(hipEventCreateWithFlags(&h->xcount_ev, hipEventDisableTiming));
     GS_HIP(hipEventCreateWithFlags(&h->sorted_ev, hipEventDisableTiming));
     for (auto& e : h->set_free) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     h->initialized = true;
@@ -2063,6 +2066,7 @@ gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, voi
                                       h->xmask.as<uint32_t>(), h->xcounts.as<uint32_t>(), nb, st));
     GS_HIP(gs::launch_rows_scan(h->xcounts.as<uint32_t>(), nb, nb ? h->world : 0, h->xtotal.as<uint32_t>(), st));
     GS_HIP(hipMemcpyAsync(h->host_xtotal, h->xtotal.ptr, h->world * 4, hipMemcpyDeviceToHost, st));
+    GS_HIP(hipEventRecord(h->xcount_ev, st));
     auto pack = [&]() -> hipError_t {
         return gs::launch_shard_pack(h->rec.as<float4>(), h->rlo.as<uint32_t>(), h->rhi.as<uint32_t>(),
                                      h->dkey.as<uint32_t>(), h->xmask.as<uint32_t>(), n, h->world,
@@ -2072,9 +2076,11 @@ gs_status pack_exchange(gs_handle* h, const gs::DestRule& rule, bool masked, voi
     // A send buffer that holds every splat once per rank cannot overflow: the
     // pack is queued before the host waits for the counts (one round trip,
     // under the pack); a smaller one is checked against them first.
+    // (the host waits for the counts alone, not for the pack behind them: the
+    // caller queues its next work, a render, while the pack runs)
     const bool roomy = send && send_cap_bytes >= (int64_t)n * h->world * gs_exchange_record_bytes();
     if (roomy) GS_HIP(pack());
-    GS_HIP(hipStreamSynchronize(st));
+    GS_HIP(hipEventSynchronize(h->xcount_ev));
     int64_t total = 0;
     for (int d = 0; d < h->world; ++d) {
         send_counts[d] = h->host_xtotal[d];
