@@ -134,6 +134,10 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 #define GS_PRE_FULLREC 1
 #endif
 
+#ifndef GS_PRE_BAND_CULL  // A/B knob: 1 = band frames cull splats off the band before their covariance
+#define GS_PRE_BAND_CULL 1
+#endif
+
 #ifndef GS_PRE_WAVES  // A/B knob: min waves per SIMD (caps the VGPRs)
 #define GS_PRE_WAVES 8
 #endif
@@ -142,7 +146,32 @@ __device__ __forceinline__ void sh_color(const ShCoef<DEG>& coef, float px, floa
 // own); 1: the scan's reduce half and fills (PreFuse).  The epilogue is
 // compiled only into its own instance, so the plain kernel keeps its
 // registers (63 VGPRs, no scratch).
-template <int DEG, int EPI>
+// Band frames (U.band_y0 > 0 or U.band_y1 < H - 1): true when
+// the splat's rect provably misses the band's pixel rows, from its centre row
+// and a bound on its half-height that needs no covariance: the 2D
+// covariance's largest eigenvalue is at most 1.5 ||A||_F^2 s_max^2 + 1e-4
+// (A = J W, Gershgorin over A Sigma A^T with lambda_max(Sigma) = s_max^2),
+// so hy <= 1.0117 * 3 sqrt(l1) * 1.0001 + 1 (the rect code below); slack
+// factors and a pixel of margin each side cover the rounding.  A splat this
+// culls gets exactly what the full path gives it (an empty rect).
+__device__ __forceinline__ bool band_culled(const FrameUniforms& U, const float* V, float vx, float vy, float zf,
+                                            float ndcy, const float4& a2) {
+    const float fx = U.P[0] * ((float)U.width * 0.5f), fy = U.P[5] * ((float)U.height * 0.5f);
+    const float iz = 1.0f / zf, iz2 = iz * iz;
+    const float j00 = fx * iz, j02 = ((-fx) * vx) * iz2, j11 = fy * iz, j12 = ((-fy) * vy) * iz2;
+    const float a00 = __builtin_fmaf(j02, V[2], j00 * V[0]), a01 = __builtin_fmaf(j02, V[6], j00 * V[4]);
+    const float a02 = __builtin_fmaf(j02, V[10], j00 * V[8]), a10 = __builtin_fmaf(j12, V[2], j11 * V[1]);
+    const float a11 = __builtin_fmaf(j12, V[6], j11 * V[5]), a12 = __builtin_fmaf(j12, V[10], j11 * V[9]);
+    const float n2 = a00 * a00 + a01 * a01 + a02 * a02 + a10 * a10 + a11 * a11 + a12 * a12;
+    const float smax = fmaxf(fmaxf(fabsf(a2.x), fabsf(a2.y)), fabsf(a2.z));
+    const float l1 = (1.5f * n2) * (smax * smax) * 1.001f + 3e-4f;
+    const float hy = (1.0117f * 3.0f) * sqrtf(l1) * 1.0002f + 2.0f;
+    const float cy = (1.0f - ndcy) * ((float)U.height * 0.5f);
+    // (NaN anywhere: both false, not culled, the full path decides)
+    return cy - hy - 0.5f > (float)U.band_y1 + 1.0f || cy + hy - 0.5f < (float)U.band_y0 - 1.0f;
+}
+
+template <int DEG, int EPI, bool BAND = false>
 __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) void preprocess_kernel(SceneDev s, const FrameUniforms U,
                                                          float4* __restrict__ rec, uint32_t* __restrict__ dkey,
                                                          uint32_t* __restrict__ rect_lo,
@@ -196,8 +225,11 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
 #if GS_PRE_EARLY
             const float4 q = q_e, a2 = a2_e;
 #else
-            float4 q = scene_load(&s.p1[i]);
             float4 a2 = scene_load(&s.p2[i]);
+            // (BAND: a splat whose rect provably misses the band's rows is
+            // culled before its rotation is read and its covariance formed)
+            if (!BAND || !band_culled(U, V, vx, vy, zf, cly * invw, a2)) {
+            float4 q = scene_load(&s.p1[i]);
 #endif
             // K1 (tile.metal:40-49)
             float qs = q.x * q.x;
@@ -336,6 +368,9 @@ __global__ __launch_bounds__(256, (EPI == 2 && DEG == 3) ? 7 : GS_PRE_WAVES) voi
                     rhi = rect_with_mask(x1 | (y1 << 16), (bexcl >> 8) & 0xFu, bexcl >> 12);
                 }
             }
+#if !GS_PRE_EARLY
+            }  // (the band cull)
+#endif
         }
     }
 #if GS_PRE_FULLREC
@@ -432,11 +467,18 @@ hipError_t launch_preprocess(const SceneDev& s, int sh_degree, const FrameUnifor
                         shard.nblocks != (s.n + kShardItems - 1) / kShardItems))
         return hipErrorInvalidValue;
     const int epi = fuse.part ? 1 : shard.owner ? 2 : 0;
+    // (band frames: the band cull, its own instances, so the full frame's
+    // kernels keep their code; not with GS_PRE_EARLY, which loads before it)
+    const bool band = GS_PRE_BAND_CULL && !GS_PRE_EARLY && epi != 2 && (U.band_y0 > 0 || U.band_y1 < U.height - 1);
     switch (sh_degree * 3 + epi) {
 #define GS_PRE_CASE(D, E)                                                                                          \
     case D * 3 + E:                                                                                                \
-        hipExtLaunchKernelGGL((preprocess_kernel<D, E>), grid, block, 0, st, t0, t1, 0, s, U, rec, dkey, rect_lo, \
-                              rect_hi, zero8, fuse, shard);                                                        \
+        if (band && E != 2)                                                                                        \
+            hipExtLaunchKernelGGL((preprocess_kernel<D, E, (E != 2)>), grid, block, 0, st, t0, t1, 0, s, U, rec,  \
+                                  dkey, rect_lo, rect_hi, zero8, fuse, shard);                                     \
+        else                                                                                                       \
+            hipExtLaunchKernelGGL((preprocess_kernel<D, E>), grid, block, 0, st, t0, t1, 0, s, U, rec, dkey,       \
+                                  rect_lo, rect_hi, zero8, fuse, shard);                                           \
         break;
         GS_PRE_CASE(0, 0) GS_PRE_CASE(0, 1) GS_PRE_CASE(0, 2)
         GS_PRE_CASE(1, 0) GS_PRE_CASE(1, 1) GS_PRE_CASE(1, 2)
