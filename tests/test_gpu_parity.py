@@ -614,6 +614,56 @@ def _rank_worker(rank, world, port, q, scheme="rows"):
         dist.destroy_process_group()
 
 
+def _rccl_exchange_worker(port, q):
+    """(test_rccl_exchange_world1) puts ("ok", checks) or ("err", traceback)."""
+    import traceback
+    try:
+        import sys
+        from pathlib import Path
+        sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+        import torch
+        import torch.distributed as dist
+        from gaussian_splat_amd.distributed import exchange_regions, exchange_start, init_ranks
+        torch.cuda.set_device(0)
+        init_ranks("nccl", 60, device=torch.device("cuda:0"), init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                   world_size=1)
+        regions = exchange_regions()
+        checks = []
+        g = torch.Generator().manual_seed(5)
+        for n in (1000, 0):
+            send = torch.randint(0, 256, (max(1, n * sum(regions)),), generator=g, dtype=torch.uint8).cuda()
+            recv, got = exchange_start(send, [n], regions, 1, None).wait()
+            torch.cuda.synchronize()
+            checks.append((n, got, recv.device.type, bool(torch.equal(recv[: n * sum(regions)], send[: n * sum(regions)]))))
+        dist.destroy_process_group()
+        q.put(("ok", checks))
+    except Exception:  # (reported to the parent instead of leaving it waiting)
+        q.put(("err", traceback.format_exc()))
+
+
+def test_rccl_exchange_world1(built):
+    """The rows scheme's record exchange (exchange_start: the counts, then one
+    all_to_all_single per exchange region, asynchronous, on device buffers)
+    through torch.distributed over the real RCCL, the driver's backend, with
+    the one rank this box has (every record to itself; shard frames need a
+    second rank, gs_shard_project refuses a world of one).  The received
+    regions equal the sent ones; an empty send is received as empty."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_exchange_worker, args=(port, q))
+    p.start()
+    status, res = q.get(timeout=180)
+    p.join(timeout=60)
+    assert status == "ok", res
+    assert p.exitcode == 0
+    assert res == [(1000, 1000, "cuda", True), (0, 0, "cuda", True)]
+
+
 @pytest.mark.parametrize("scheme", ["rows", "slabs", "pipe"])
 def test_multiprocess_ranks_bitexact(built, scheme):
     """Two rank processes on the GPU through the product multi-GPU path
