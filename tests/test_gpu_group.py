@@ -176,6 +176,53 @@ def test_group_rccl_stub_bitexact(built):
     assert p.stdout.count("ok ") == 5, p.stdout
 
 
+_REAL_RCCL_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import orbit_views
+from gaussian_splat_amd import InstancedSplatRenderer, Options, ShardedGroup
+from gaussian_splat_amd import scene as S
+
+W, H = 640, 400
+sc = S.activate(S.synthetic_raw(60000, seed=116, aspect=W / H, rest=True), 3)
+r = InstancedSplatRenderer(sc, Options(sh_degree=3, crop=False))
+r.initialize(0)
+for scheme in ("rows", "bands"):
+    g = ShardedGroup(r, 1, replicated=scheme == "bands")
+    g.initialize([0], "rccl")
+    assert g.transport == "rccl", g.transport
+    if scheme == "rows":
+        g.set_scheme("rows")
+    for V, P in orbit_views(W, H, 2):
+        a, ref = g.render_host(V, P, W, H), r.render_host(V, P, W, H)
+        assert int(np.count_nonzero(a.view(np.uint32) != ref.view(np.uint32))) == 0, scheme
+    g.close()
+    print("ok", scheme)
+"""
+
+
+def test_group_real_rccl_one_rank(built):
+    """The group over the real RCCL library (the group's dlopen of librccl,
+    ncclCommInitAll, the grouped ncclSend/ncclRecv of the record exchange and
+    the band gather), with the one rank this box has (every record and band to
+    itself; RCCL takes one device per rank, so two ranks need two GPUs):
+    rows and bands frames equal the 1-GPU frame bit for bit.  Its own process,
+    GS_RCCL_LIB unset: RCCL is resolved once per process."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k != "GS_RCCL_LIB"}
+    p = subprocess.run([sys.executable, "-c", _REAL_RCCL_SCRIPT, str(root)], env=env, capture_output=True, text=True,
+                       timeout=170)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert p.stdout.count("ok ") == 2, p.stdout
+
+
 def test_group_bounded_wait(built):
     """Every host wait of a group is bounded (gs_group_set_timeout): a wait
     that cannot finish in time fails the frame with GS_ERR_COMM and leaves
