@@ -81,9 +81,11 @@ def test_filtered_sort_pass_budget(sort_res):
     assert r["VGPRs Spill"] == 0 and r["ScratchSize"] == 0, r
 
 
-def test_projection_budget(pre_res):
+@pytest.mark.parametrize("band", [0, 1])
+def test_projection_budget(pre_res, band):
+    # band 1: the band frames' instances (splats off the band culled before their covariance)
     for epi in (0, 1):  # plain, and with the scan sums of bin-first frames
-        r = _one(pre_res, rf"preprocess_kernelILi3ELi{epi}E")
+        r = _one(pre_res, rf"preprocess_kernelILi3ELi{epi}ELb{band}E")
         assert r["VGPRs Spill"] == 0 and r["ScratchSize"] == 0, (epi, r)
         assert r["Occupancy"] == 8, (epi, r)
         # SGPR class (blocks of 16, plus 16): shares SIMDs with the composite
