@@ -158,10 +158,15 @@ def gather_frame(band, width: int, height: int, world: int, rank: int, owner=Non
             return frame
         y0, y1 = spans[rank]
         if y1 > y0:
+            # (a batch of one, as rank 0's receives: every rank of the group
+            # enters its first point-to-point call through the same API, as
+            # torch.distributed asks of RCCL/NCCL)
+            reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, band[: y1 - y0], 0, group)])
             if pending is not None:
-                pending.append(dist.isend(band[: y1 - y0], 0, group=group))
+                pending.extend(reqs)
             else:
-                dist.send(band[: y1 - y0], 0, group=group)
+                for q in reqs:
+                    q.wait()
         return None
     if _host_staged(group):
         hb = band.cpu()
