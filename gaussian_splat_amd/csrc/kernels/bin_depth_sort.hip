@@ -229,8 +229,15 @@ __device__ void sort_list_global(uint32_t s, uint32_t m, uint32_t* keys, uint32_
 #ifndef GS_SEG_MINW  // min waves per SIMD (launch bounds: caps the VGPRs)
 #define GS_SEG_MINW 6
 #endif
+#ifndef GS_SEG_SMALL_MINW
+#define GS_SEG_SMALL_MINW 6
+#endif
 
-template <int NT, int IPT, int MINW = 1>
+// CLS (GS_SEG_CLASSES): 0 every list; 1 the lists of at most kSegSmallMax
+// pairs only; 2 the longer ones only (two launches over every bin, so that
+// short lists run in narrow workgroups, more bins at a time, and long ones
+// keep the wide workgroup's LDS capacity).
+template <int NT, int IPT, int MINW = 1, int CLS = 0>
 __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* __restrict__ ranges,
                                                                   uint32_t* __restrict__ keys,
                                                                   uint32_t* __restrict__ vals,
@@ -249,6 +256,10 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
         if (m > (uint32_t)NT * IPT) atomicAdd(&sample[0], m);
     }
     if (m < 2u) return;  // nothing to order
+    if constexpr (CLS == 1)
+        if (m > kSegSmallMax) return;
+    if constexpr (CLS == 2)
+        if (m <= kSegSmallMax) return;
     const uint32_t s = rg.x;
     if (m > (uint32_t)NT * IPT) {  // a hot bin: chunked LSD over global memory
         sort_list_global<NT, 8>(s, m, keys, vals, tmp_keys, tmp_vals, bin_bits, L, stage);
@@ -319,6 +330,22 @@ hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* 
     if (bin_bits < 0 || bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     // one workgroup per bin
     static_assert(GS_SEG_NT * GS_SEG_IPT == kSegLdsMax, "gs_kernels.h");
+    // Frames of many bins (4K: 8160; their lists are short) sort in two size
+    // classes: the long lists first (that launch samples every list), then the
+    // short ones in 256-lane workgroups, twice the bins at a time; the second
+    // launch's packet carries `done`.  Frames of few bins (1080p: 2040, lists
+    // of ~2-3k pairs, more of them past the short class) keep one launch: the
+    // long class alone then leaves the part idle (profiles/r06/ab_seg_classes.txt).
+    static_assert(GS_SEG_SMALL_NT * GS_SEG_SMALL_IPT == kSegSmallMax && kSegSmallMax < kSegLdsMax, "gs_kernels.h");
+    if (GS_SEG_CLASSES && nbins >= (uint32_t)GS_SEG_CLASS_MIN_BINS) {
+        hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW, 2>), dim3(nbins),
+                              dim3(GS_SEG_NT), 0, st, nullptr, nullptr, 0, ranges, keys, vals, tmp_keys, tmp_vals,
+                              bin_bits, sample, guard);
+        hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_SMALL_NT, GS_SEG_SMALL_IPT, GS_SEG_SMALL_MINW, 1>),
+                              dim3(nbins), dim3(GS_SEG_SMALL_NT), 0, st, nullptr, done, 0, ranges, keys, vals, tmp_keys,
+                              tmp_vals, bin_bits, nullptr, guard);
+        return hipGetLastError();
+    }
     hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>), dim3(nbins), dim3(GS_SEG_NT), 0,
                           st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals, bin_bits, sample, guard);
     return hipGetLastError();

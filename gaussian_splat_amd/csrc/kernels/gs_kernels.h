@@ -178,6 +178,19 @@ hipError_t launch_scan_duplicate(const uint32_t* order, const uint32_t* rect_lo,
 #define GS_SEG_IPT 16
 #endif
 constexpr uint32_t kSegLdsMax = GS_SEG_NT * GS_SEG_IPT;  // lists sorted inside one workgroup (bin_depth_sort.hip)
+#ifndef GS_SEG_CLASSES  // 1: frames of >= GS_SEG_CLASS_MIN_BINS bins sort short lists (<= kSegSmallMax) in a launch of narrower workgroups
+#define GS_SEG_CLASSES 1
+#endif
+#ifndef GS_SEG_CLASS_MIN_BINS
+#define GS_SEG_CLASS_MIN_BINS 4096
+#endif
+#ifndef GS_SEG_SMALL_NT
+#define GS_SEG_SMALL_NT 256
+#endif
+#ifndef GS_SEG_SMALL_IPT
+#define GS_SEG_SMALL_IPT 16
+#endif
+constexpr uint32_t kSegSmallMax = GS_SEG_SMALL_NT * GS_SEG_SMALL_IPT;
 constexpr uint32_t kSegSampleValid = 0x80000000u;
 // guard (optional): nothing is done while *guard == 0 (the fallback lists).
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,

@@ -382,6 +382,50 @@ def test_bin_first_equals_depth_first(built, n, w, h, mode, cap, wall, zr):
     assert linf <= TOL and nbit == 0, (linf, nbit)
 
 
+def test_bin_sort_size_classes(built):
+    """A frame of 4096 bins (2048 x 2048), where the per-bin sort runs in two
+    size classes (bin_depth_sort.hip: lists of <= 4096 pairs in 256-lane
+    workgroups, longer ones in 512-lane workgroups or through global memory),
+    with lists in every class: two clusters of splats over a uniform scene.
+    Bin-first equals depth-first (keys, vals, image) and the oracle."""
+    from gaussian_splat_amd import InstancedSplatRenderer, Options
+    from gaussian_splat_amd import scene as S
+    from oracle import oracle_py as O
+    w = h = 2048
+    sc = S.activate(S.synthetic_raw(200000, seed=21, aspect=1.0, zrange=(1, 9)), 0)
+    rng = np.random.default_rng(7)
+    eye = np.array([0.0, 2.0, 5.0])
+    fwd = -eye / np.linalg.norm(eye)
+    right = np.cross(fwd, [0.0, -1.0, 0.0])
+    right /= np.linalg.norm(right)
+    up = np.cross(right, fwd)
+    o = 0
+    for k, sig, (ox, oy) in ((60000, 0.15, (0.0, 0.0)), (60000, 0.015, (0.8, 0.5))):
+        a, b = rng.normal(0, sig, (2, k))
+        d = rng.uniform(3.0, 6.0, k)
+        sc.pos[o:o + k] = (eye + d[:, None] * fwd + (a + ox)[:, None] * right + (b + oy)[:, None] * up).astype(np.float32)
+        o += k
+    V, P = orbit_views(w, h, 1)[0]
+    out = {}
+    for b in ("depth_first", "bin_first"):
+        r = InstancedSplatRenderer(sc, Options(binning=b, depth_split=False))
+        r.initialize(0)
+        img = r.render_host(V, P, w, h)
+        keys, vals = r.sorted_pairs()
+        out[b] = (img, keys, vals)
+    img0, k0, v0 = out["depth_first"]
+    img1, k1, v1 = out["bin_first"]
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(v1, v0)
+    assert _compare(img1, img0) == (0.0, 0)
+    per_bin = np.bincount(k0, minlength=64 * 64)
+    assert per_bin.size == 4096 and (per_bin > 8192).any() and ((per_bin > 4096) & (per_bin <= 8192)).any()
+    assert ((per_bin > 1) & (per_bin <= 4096)).sum() > 3000
+    ref, _ = O.render(sc, V, P, w, h)
+    linf, nbit = _compare(img1, ref)
+    assert linf <= TOL and nbit == 0, (linf, nbit)
+
+
 def test_bin_first_frame_sequences(built):
     """Sequences of bin-first frames (repeats, camera and resolution
     switches, pipelined frames with host-output frames in between, which
