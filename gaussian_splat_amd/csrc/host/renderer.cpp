@@ -1229,7 +1229,8 @@ gs_status bin_sort_composite(gs_handle* h, uint32_t m, const uint32_t* dkey, con
             GS_HIP(gs::launch_bin_depth_sort(h->ranges.as<uint2>(), (uint32_t)(U.tiles_x * U.tiles_y), h->last_keys,
                                              h->last_vals, h->last_tmp_keys, h->last_tmp_vals, h->last_key_bits,
                                              cutf && h->cut_in ? nullptr : h->seg_sample.as<uint32_t>() + 2 * h->set,
-                                             sd, sc != st ? h->sorted_ev : nullptr));
+                                             sd, sc != st ? h->sorted_ev : nullptr, nullptr,
+                                             cutf && h->front_last));  // (front lists: short)
             mark(h, 6, sd);
             GS_HIP(handoff(true));
             GS_HIP(gs::launch_composite(c, h->opt.mode, sc, kernel_event(h, 2), kernel_event(h, 3)));

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(NT, MINW) void bin_depth_sort_kernel(const uint2* _
 
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
-                                 hipStream_t st, hipEvent_t done, const unsigned long long* guard) {
+                                 hipStream_t st, hipEvent_t done, const unsigned long long* guard, bool short_lists) {
     if (nbins == 0) return done ? hipEventRecord(done, st) : hipSuccess;
     if (bin_bits < 0 || bin_bits + kDepthBits > 32) return hipErrorInvalidValue;
     // one workgroup per bin
@@ -344,6 +344,12 @@ hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* 
         hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_SMALL_NT, GS_SEG_SMALL_IPT, GS_SEG_SMALL_MINW, 1>),
                               dim3(nbins), dim3(GS_SEG_SMALL_NT), 0, st, nullptr, done, 0, ranges, keys, vals, tmp_keys,
                               tmp_vals, bin_bits, nullptr, guard);
+        return hipGetLastError();
+    }
+    if (GS_SEG_SHORT && short_lists) {  // (a still camera's front lists: every list in 256-lane workgroups)
+        hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_SMALL_NT, GS_SEG_SMALL_IPT, GS_SEG_SMALL_MINW>), dim3(nbins),
+                              dim3(GS_SEG_SMALL_NT), 0, st, nullptr, done, 0, ranges, keys, vals, tmp_keys, tmp_vals,
+                              bin_bits, sample, guard);
         return hipGetLastError();
     }
     hipExtLaunchKernelGGL((bin_depth_sort_kernel<GS_SEG_NT, GS_SEG_IPT, GS_SEG_MINW>), dim3(nbins), dim3(GS_SEG_NT), 0,

@@ -184,6 +184,9 @@ constexpr uint32_t kSegLdsMax = GS_SEG_NT * GS_SEG_IPT;  // lists sorted inside 
 #ifndef GS_SEG_CLASS_MIN_BINS
 #define GS_SEG_CLASS_MIN_BINS 4096
 #endif
+#ifndef GS_SEG_SHORT  // A/B knob: 1 = frames of fewer bins whose lists are front lists (short_lists) sort in 256-lane workgroups
+#define GS_SEG_SHORT 1
+#endif
 #ifndef GS_SEG_SMALL_NT
 #define GS_SEG_SMALL_NT 256
 #endif
@@ -196,7 +199,7 @@ constexpr uint32_t kSegSampleValid = 0x80000000u;
 hipError_t launch_bin_depth_sort(const uint2* ranges, uint32_t nbins, uint32_t* keys, uint32_t* vals,
                                  uint32_t* tmp_keys, uint32_t* tmp_vals, int bin_bits, uint32_t* sample,
                                  hipStream_t st, hipEvent_t done = nullptr,
-                                 const unsigned long long* guard = nullptr);
+                                 const unsigned long long* guard = nullptr, bool short_lists = false);
 
 // ---- radix_sort.hip --------------------------------------------------------
 constexpr int kSortBins = 256;   // 8-bit digits
