@@ -169,7 +169,7 @@ __device__ __forceinline__ void seg_pass(uint32_t (&it)[IPT], uint32_t (&pos)[IP
 // NT * IPT pairs in list order; (keys, vals) -> (tmp_keys, tmp_vals) ->
 // (keys, vals) at the list's own offsets [s, s + m).  run: 256 words of LDS.
 template <int NT, int IPT>
-__device__ void sort_list_global(uint32_t s, uint32_t m, uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys,
+__device__ __forceinline__ void sort_list_global(uint32_t s, uint32_t m, uint32_t* keys, uint32_t* vals, uint32_t* tmp_keys,
                                  uint32_t* tmp_vals, int bin_bits, SegRankLds<NT>& L, uint32_t* run) {
     constexpr uint32_t CH = (uint32_t)NT * IPT;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;

@@ -61,6 +61,11 @@ def comp_res():
     return _resources("composite.hip")
 
 
+@pytest.fixture(scope="module")
+def seg_res():
+    return _resources("bin_depth_sort.hip")
+
+
 @pytest.mark.parametrize("bits", [5, 6, 7])
 def test_bin_sort_pass_budget(sort_res, bits):
     # one value array: the bin sort's passes (and the depth-cut frames'
@@ -102,3 +107,11 @@ def test_composite_budget(comp_res, pass_):
     # co-run with the preprocess lost 51 us a frame (composite.hip, GS_COMPOSITE_SGPRS)
     assert r["TotalSGPRs"] <= 64, r
     assert r["ScratchSize"] <= (8 if pass_ == 0 else 16), r
+
+
+def test_bin_depth_sort_budget(seg_res):
+    # the per-bin sort: one 512-lane launch (lists up to 8192 pairs in LDS), and the 256-lane
+    # short class of frames of many bins (GS_SEG_CLASSES): no spill, six waves per SIMD
+    for pat in (r"bin_depth_sort_kernelILi512ELi16ELi6ELi0EE", r"bin_depth_sort_kernelILi256ELi16ELi6ELi1EE"):
+        r = _one(seg_res, pat)
+        assert r["ScratchSize"] == 0 and r["Occupancy"] >= 6, (pat, r)
